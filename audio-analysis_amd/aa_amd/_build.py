@@ -1,0 +1,65 @@
+"""Build libaa.so in-tree with hipcc for gfx950 (no torch extension machinery:
+the library is a plain C-ABI shared object loaded with ctypes)."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG.parent / "csrc"
+INCLUDE = PKG.parent.parent / "include"
+LIB = PKG / "libaa.so"
+SOURCES = ["aa_api.cpp", "aa_frontend.hip", "aa_cnn.hip"]
+ARCH = os.environ.get("AA_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libaa.so)")
+
+
+def _stale() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    deps = [CSRC / s for s in SOURCES] + list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
+    return any(p.stat().st_mtime > t for p in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if not force and not _stale():
+        return LIB
+    cc = hipcc()
+    objdir = PKG.parent / "build"
+    objdir.mkdir(exist_ok=True)
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}",
+             "-Wall", "-Wno-unused-function"]
+
+    def compile_one(src: str) -> Path:
+        obj = objdir / (src.rsplit(".", 1)[0] + ".o")
+        cmd = [cc, *flags, "-c", str(CSRC / src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd))
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr}")
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1, 16)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

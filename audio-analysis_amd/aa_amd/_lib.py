@@ -1,0 +1,128 @@
+"""ctypes binding of libaa.so (include/aa.h).
+
+torch is imported first on purpose: the library's DT_NEEDED libamdhip64.so.7
+then resolves to the HIP runtime torch already loaded, so device pointers from
+torch tensors and the library's launches live in one runtime.  There is no
+fallback: if the shared object is missing or does not load, every compute call
+raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede loading libaa.so, see above)
+
+LIB_PATH = Path(__file__).resolve().parent / "libaa.so"
+ABI_VERSION = 1
+
+AA_PREC_F32 = 0
+AA_PREC_BF16 = 1
+
+AA_OP = {
+    "conv2d": 1,
+    "batchnorm": 2,
+    "leakyrelu": 3,
+    "maxpool2d": 4,
+    "globalmaxpool2d": 5,
+    "sigmoid": 6,
+    "magtransform": 7,
+    "relu": 8,
+}
+
+AA_WIN_OK = 0
+AA_WIN_NONFINITE = 1
+
+
+class AAError(RuntimeError):
+    pass
+
+
+class Window(C.Structure):
+    _fields_ = [("src", C.c_int64), ("n_valid", C.c_int32), ("pad_left", C.c_int32)]
+
+
+class FeConfig(C.Structure):
+    _fields_ = [
+        ("win_len", C.c_int32), ("n_fft", C.c_int32), ("hop", C.c_int32), ("n_mels", C.c_int32),
+        ("normalize", C.c_int32), ("db_scale", C.c_int32), ("power", C.c_float),
+        ("amin", C.c_float), ("top_db", C.c_float), ("mean_sub", C.c_int32),
+        ("channels", C.c_int32),
+    ]
+
+
+class Layer(C.Structure):
+    _fields_ = [
+        ("op", C.c_int32), ("kh", C.c_int32), ("kw", C.c_int32), ("filters", C.c_int32),
+        ("alpha", C.c_float), ("eps", C.c_float), ("off", C.c_int64 * 4),
+    ]
+
+
+_lib = None
+
+_SIGS = {
+    "aa_abi_version": (C.c_int, []),
+    "aa_last_error": (C.c_char_p, []),
+    "aa_fe_create": (C.c_int, [C.POINTER(FeConfig), C.c_void_p, C.POINTER(C.c_void_p)]),
+    "aa_fe_destroy": (C.c_int, [C.c_void_p]),
+    "aa_fe_n_frames": (C.c_int, [C.c_void_p]),
+    "aa_fe_workspace_bytes": (C.c_size_t, [C.c_void_p, C.c_int32]),
+    "aa_fe_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p,
+                            C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "aa_model_create": (C.c_int, [C.POINTER(Layer), C.c_int32, C.c_void_p, C.c_int64, C.c_int32,
+                                  C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "aa_model_destroy": (C.c_int, [C.c_void_p]),
+    "aa_model_n_outputs": (C.c_int, [C.c_void_p]),
+    "aa_model_workspace_bytes": (C.c_size_t, [C.c_void_p, C.c_int32]),
+    "aa_model_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_size_t, C.c_void_p]),
+    "aa_model_n_stages": (C.c_int, [C.c_void_p]),
+    "aa_model_stage_info": (C.c_int, [C.c_void_p, C.c_int32, C.c_char_p, C.c_int32,
+                                      C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "aa_model_set_timing": (C.c_int, [C.c_void_p, C.c_int32]),
+    "aa_model_stage_time": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_int64)]),
+    "aa_track_mean": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_void_p,
+                                C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+def lib():
+    """Load libaa.so once; raises if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise AAError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc gfx950)")
+        h = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in _SIGS.items():
+            f = getattr(h, name)
+            f.restype = res
+            f.argtypes = args
+        v = h.aa_abi_version()
+        if v != ABI_VERSION:
+            raise AAError(f"libaa.so ABI {v} != {ABI_VERSION}")
+        _lib = h
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().aa_last_error().decode(errors="replace")
+        raise AAError(f"{what or 'libaa'} failed ({rc}): {msg}")
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def dptr(t) -> int:
+    if t is None:
+        return 0
+    if not t.is_cuda:
+        raise AAError("libaa needs device tensors")
+    if not t.is_contiguous():
+        raise AAError("libaa needs contiguous tensors")
+    return int(t.data_ptr())

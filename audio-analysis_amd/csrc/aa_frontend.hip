@@ -1,0 +1,546 @@
+// Per-window log-mel front end for gfx950.
+//
+// Replaces, per analysis window (reference /root/reference):
+//   normalize_data                      src/identify_tracks.py:202-209
+//   np.abs(librosa.stft(x, n_fft, hop))  src/identify_tracks.py:243
+//   custommel.mel_spec (|S|**p, mel_f.)  src/custommel.py:59-63
+//   librosa.power_to_db(ref=np.max)     src/identify_tracks.py:266
+//   expand_dims / mean_sub / channels   src/identify_tracks.py:267-288
+//
+// Three launches per batch of windows (all on the caller's stream):
+//   fe_stats    min/max/finite partials of every window (HBM stream of the PCM)
+//   fe_stft_mel a block owns FPB consecutive frames of one window: the
+//               overlapped PCM segment is loaded once (coalesced) and normalised
+//               into LDS, each frame is windowed and transformed by an N/2-point
+//               complex Stockham FFT (radix 8, LDS ping-pong, table twiddles),
+//               split into the N-point real spectrum, |X|**power, and projected
+//               on the sparse mel filterbank (CSR rows, contiguous bins).
+//   fe_db       per-window max -> power_to_db, clamp, mean_sub, layout/channels.
+#include "aa_common.h"
+
+#include <cmath>
+#include <vector>
+
+namespace aa {
+
+constexpr int kStatSplit = 16;  // stats blocks per window
+constexpr int kFpb = 8;         // frames per stft block
+
+struct FePlan {
+    aa_fe_config cfg;
+    int T = 0;         // frames per window
+    int kmin = 0;      // first filterbank bin with a nonzero weight
+    int kmax = 0;      // last
+    int nfblk = 0;     // frame blocks per window
+    int nnz = 0;
+    float* d_win = nullptr;   // periodic Hann, f32 [n_fft]
+    float2* d_tw = nullptr;   // exp(-2 pi i m / Nc), m < Nc
+    float2* d_tw2 = nullptr;  // exp(-2 pi i k / n_fft), k <= Nc
+    int4* d_rows = nullptr;   // per band: (first bin, count, value offset, 0)
+    float* d_vals = nullptr;  // CSR values
+};
+
+// ---------------------------------------------------------------------------
+// fe_stats: min / max / non-finite over each virtual window (zeros outside the
+// valid view, exactly like np.pad before normalize_data).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fe_stats(const float* __restrict__ pcm,
+                                                const aa_window* __restrict__ wins,
+                                                int win_len, float4* __restrict__ stats) {
+    const int w = blockIdx.y;
+    const aa_window d = wins[w];
+    const int chunk = (win_len + kStatSplit - 1) / kStatSplit;
+    const int i0 = blockIdx.x * chunk;
+    const int i1 = min(win_len, i0 + chunk);
+    float mn = INFINITY, mx = -INFINITY;
+    int bad = 0;
+    // valid part of this chunk, in window coordinates; the rest is np.pad zeros
+    const int v0 = max(i0, d.pad_left);
+    const int v1 = min(i1, d.pad_left + d.n_valid);
+    if (i0 < i1 && !(v0 == i0 && v1 >= i1)) { mn = 0.f; mx = 0.f; }
+    if (v0 < v1) {
+        const float* p = pcm + d.src + (v0 - d.pad_left);
+        const int n = v1 - v0;
+        // scalar head up to 16-byte alignment, float4 body, scalar tail
+        const int head = min(n, (int)((16 - ((uintptr_t)p & 15)) & 15) / 4);
+        for (int i = threadIdx.x; i < head; i += blockDim.x) {
+            float x = p[i];
+            bad |= !isfinite(x);
+            mn = fminf(mn, x);
+            mx = fmaxf(mx, x);
+        }
+        const int nb = (n - head) / 4;
+        const float4* q = reinterpret_cast<const float4*>(p + head);
+        for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+            float4 x = q[i];
+            bad |= !isfinite(x.x) | !isfinite(x.y) | !isfinite(x.z) | !isfinite(x.w);
+            mn = fminf(fminf(mn, x.x), fminf(x.y, fminf(x.z, x.w)));
+            mx = fmaxf(fmaxf(mx, x.x), fmaxf(x.y, fmaxf(x.z, x.w)));
+        }
+        for (int i = head + nb * 4 + threadIdx.x; i < n; i += blockDim.x) {
+            float x = p[i];
+            bad |= !isfinite(x);
+            mn = fminf(mn, x);
+            mx = fmaxf(mx, x);
+        }
+    }
+    __shared__ float smn[4], smx[4];
+    __shared__ int sbad[4];
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    bad = wave_or(bad);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { smn[wv] = mn; smx[wv] = mx; sbad[wv] = bad; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
+            mn = fminf(mn, smn[k]);
+            mx = fmaxf(mx, smx[k]);
+            bad |= sbad[k];
+        }
+        stats[w * kStatSplit + blockIdx.x] = make_float4(mn, mx, (float)bad, 0.f);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// radix building blocks (forward transform, W = exp(-2 pi i / n))
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 mul_negi(float2 a) { return make_float2(a.y, -a.x); }  // a * (-i)
+
+__device__ __forceinline__ void dft2(float2& a, float2& b) {
+    float2 t = csub(a, b);
+    a = cadd(a, b);
+    b = t;
+}
+// in: a,b,c,d = x0..x3 ; out in natural order X0..X3
+__device__ __forceinline__ void dft4(float2& a, float2& b, float2& c, float2& d) {
+    float2 t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = mul_negi(csub(b, d));
+    a = cadd(t0, t2);
+    c = csub(t0, t2);
+    b = cadd(t1, t3);
+    d = csub(t1, t3);
+}
+__device__ __forceinline__ void dft8(float2* v) {
+    const float r = 0.70710678118654752440f;
+    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    dft4(e0, e1, e2, e3);
+    dft4(o0, o1, o2, o3);
+    // twiddles W8^k, k = 0..3
+    float2 w1 = make_float2(r * (o1.x + o1.y), r * (o1.y - o1.x));   // * (r, -r)
+    float2 w2 = mul_negi(o2);                                       // * (0, -1)
+    float2 w3 = make_float2(r * (o3.y - o3.x), -r * (o3.x + o3.y));  // * (-r, -r)
+    v[0] = cadd(e0, o0);
+    v[4] = csub(e0, o0);
+    v[1] = cadd(e1, w1);
+    v[5] = csub(e1, w1);
+    v[2] = cadd(e2, w2);
+    v[6] = csub(e2, w2);
+    v[3] = cadd(e3, w3);
+    v[7] = csub(e3, w3);
+}
+
+// One Stockham pass of radix R over NC points held in LDS (src -> dst), for
+// sub-transform size NS (product of the earlier radices).  Thread handles
+// butterflies j = tid, tid + NT, ...
+template <int NC, int R, int NT, int NS>
+__device__ __forceinline__ void stockham_pass(const float2* __restrict__ src, float2* __restrict__ dst,
+                                              const float2* __restrict__ tw) {
+    constexpr int NB = NC / R;
+#pragma unroll
+    for (int jj = 0; jj < (NB + NT - 1) / NT; ++jj) {
+        const int j = threadIdx.x + jj * NT;
+        if (NB % NT == 0 || j < NB) {
+            float2 v[R];
+            const int k = j % NS;
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = src[j + r * NB];
+            if constexpr (NS > 1) {
+                constexpr int step = NC / (NS * R);
+#pragma unroll
+                for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k * step]);
+            }
+            if constexpr (R == 8) dft8(v);
+            if constexpr (R == 4) dft4(v[0], v[1], v[2], v[3]);
+            if constexpr (R == 2) dft2(v[0], v[1]);
+            const int o = (j / NS) * NS * R + k;
+#pragma unroll
+            for (int r = 0; r < R; ++r) dst[o + r * NS] = v[r];
+        }
+    }
+}
+
+// Remaining passes after the first radix-8 pass; returns the buffer holding
+// the natural-order result (the other one is free).
+template <int NC, int NT, int NS>
+__device__ __forceinline__ float2* fft_rest(float2* src, float2* dst, const float2* __restrict__ tw) {
+    if constexpr (NS * 8 <= NC) {
+        stockham_pass<NC, 8, NT, NS>(src, dst, tw);
+        __syncthreads();
+        return fft_rest<NC, NT, NS * 8>(dst, src, tw);
+    } else if constexpr (NC / NS == 4) {
+        stockham_pass<NC, 4, NT, NS>(src, dst, tw);
+        __syncthreads();
+        return dst;
+    } else if constexpr (NC / NS == 2) {
+        stockham_pass<NC, 2, NT, NS>(src, dst, tw);
+        __syncthreads();
+        return dst;
+    } else {
+        return src;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// fe_stft_mel
+// ---------------------------------------------------------------------------
+template <int NFFT>
+__global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
+    const float* __restrict__ pcm, const aa_window* __restrict__ wins, const float4* __restrict__ stats,
+    const float* __restrict__ hann, const float2* __restrict__ tw, const float2* __restrict__ tw2,
+    const int4* __restrict__ rows, const float* __restrict__ vals, int win_len, int hop, int T,
+    int n_mels, int kmin, int kmax, int normalize, float power, float* __restrict__ melS,
+    float* __restrict__ blkmax) {
+    constexpr int NC = NFFT / 2;
+    constexpr int NT = NC / 8;
+    extern __shared__ float lds[];
+    const int w = blockIdx.y;
+    const int f0 = blockIdx.x * kFpb;
+    const int nf = min(kFpb, T - f0);
+    const int seg_len = (nf - 1) * hop + NFFT;
+    float* seg = lds;
+    const int seg_cap = ((kFpb - 1) * hop + NFFT + 3) & ~3;
+    float2* bufA = reinterpret_cast<float2*>(lds + seg_cap);
+    float2* bufB = bufA + NC;
+    float* melT = reinterpret_cast<float*>(bufB + NC);  // [n_mels][kFpb] staging
+
+    // --- normalisation constants (normalize_data, :203-208) ---
+    const aa_window d = wins[w];
+    float lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < kStatSplit; ++s) {
+        float4 st = stats[w * kStatSplit + s];
+        lo = fminf(lo, st.x);
+        hi = fmaxf(hi, st.y);
+    }
+    const float scale = __fsub_rn(hi, lo);  // == max(x - min) (monotone rounding)
+
+    // --- overlapped segment -> LDS, normalised ---
+    const int base = f0 * hop - NFFT / 2;  // window index of seg[0]
+    for (int q = threadIdx.x; q < seg_len; q += NT) {
+        const int i = base + q;
+        float v = 0.f;
+        if (i >= 0 && i < win_len) {
+            const int rel = i - d.pad_left;
+            const float raw = (rel >= 0 && rel < d.n_valid) ? pcm[d.src + rel] : 0.f;
+            if (normalize) {
+                float y = __fdiv_rn(__fsub_rn(raw, lo), scale);
+                y = __fadd_rn(y, 0.000001f);
+                y = __fsub_rn(y, 0.5f);
+                v = __fmul_rn(y, 2.0f);
+            } else {
+                v = raw;
+            }
+        }
+        seg[q] = v;
+    }
+    __syncthreads();
+
+    float bmax = 0.f;
+    for (int f = 0; f < nf; ++f) {
+        // pass 1 (Ns = 1) straight from the segment: z[n] = xw[2n] + i xw[2n+1]
+        {
+            const float* x = seg + f * hop;
+            constexpr int NB = NC / 8;
+            const int j = threadIdx.x;
+            float2 v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int n = j + r * NB;
+                v[r] = make_float2(x[2 * n] * hann[2 * n], x[2 * n + 1] * hann[2 * n + 1]);
+            }
+            dft8(v);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) bufA[j * 8 + r] = v[r];
+        }
+        __syncthreads();
+        float2* src = fft_rest<NC, NT, 8>(bufA, bufB, tw);
+        float2* dst = (src == bufA) ? bufB : bufA;
+        // src now holds Z[0..NC) in natural order; dst is free scratch for P.
+        float* Pf = reinterpret_cast<float*>(dst);
+        for (int k = kmin + threadIdx.x; k <= kmax; k += NT) {
+            float re, im;
+            if (k == 0 || k == NC) {
+                const float2 z0 = src[0];
+                re = (k == 0) ? z0.x + z0.y : z0.x - z0.y;
+                im = 0.f;
+            } else {
+                const float2 a = src[k];
+                const float2 b = src[NC - k];  // conj taken below
+                // E = (a + conj b)/2 ; O = -i (a - conj b)/2 ; X = E + W^k O
+                const float2 E = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+                const float2 O = make_float2(0.5f * (a.y + b.y), -0.5f * (a.x - b.x));
+                const float2 X = cadd(E, cmul(tw2[k], O));
+                re = X.x;
+                im = X.y;
+            }
+            // complex64 -> np.abs (hypot) -> ** power
+            const float mag = sqrtf(re * re + im * im);
+            float pw;
+            if (power == 2.f) pw = mag * mag;
+            else if (power == 1.f) pw = mag;
+            else pw = powf(mag, power);
+            Pf[k - kmin] = pw;
+        }
+        __syncthreads();
+        for (int m = threadIdx.x; m < n_mels; m += NT) {
+            const int4 rw = rows[m];
+            float s = 0.f;
+            for (int i = 0; i < rw.y; ++i) s = fmaf(vals[rw.z + i], Pf[rw.x - kmin + i], s);
+            melT[m * kFpb + f] = s;
+            bmax = fmaxf(bmax, s);
+        }
+        __syncthreads();  // P / buffers reused by the next frame
+    }
+    // staged [n_mels][nf] tile -> melS[w][m][f0 .. f0 + nf)
+    for (int idx = threadIdx.x; idx < n_mels * nf; idx += NT) {
+        const int m = idx / nf, f = idx - (idx / nf) * nf;
+        melS[((size_t)w * n_mels + m) * T + f0 + f] = melT[m * kFpb + f];
+    }
+    // block max -> blkmax[w][blockIdx.x]
+    __shared__ float red[NT / 64];
+    bmax = wave_max(bmax);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < NT / 64; ++k) bmax = fmaxf(bmax, red[k]);
+        blkmax[w * gridDim.x + blockIdx.x] = bmax;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// fe_db: power_to_db(ref=max), clamp at -top_db, mean_sub, channel repeat.
+// One wave per mel band row.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melS, const float* __restrict__ blkmax,
+                                             const float4* __restrict__ stats, int nfblk, int n_mels, int T,
+                                             int db_scale, float amin, float top_db, int mean_sub,
+                                             int channels, int normalize, float* __restrict__ out,
+                                             int* __restrict__ status) {
+    const int w = blockIdx.y;
+    float smax = 0.f;
+    for (int i = 0; i < nfblk; ++i) smax = fmaxf(smax, blkmax[w * nfblk + i]);
+    const float ref_db = __fmul_rn(10.0f, log10f(fmaxf(amin, smax)));
+    const int lane = threadIdx.x & 63;
+    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && status) {
+        float lo = INFINITY, hi = -INFINITY;
+        int bad = 0;
+        for (int s = 0; s < kStatSplit; ++s) {
+            float4 st = stats[w * kStatSplit + s];
+            lo = fminf(lo, st.x);
+            hi = fmaxf(hi, st.y);
+            bad |= st.z != 0.f;
+        }
+        // normalize_data divides by max(x - min): 0 -> NaN -> librosa raises
+        if (normalize && !(hi - lo > 0.f)) bad = 1;
+        status[w] = bad ? AA_WIN_NONFINITE : AA_WIN_OK;
+    }
+    if (m >= n_mels) return;
+    const float* row = melS + ((size_t)w * n_mels + m) * T;
+    auto val = [&](int t) {
+        float v = row[t];
+        if (db_scale) {
+            v = __fsub_rn(__fmul_rn(10.0f, log10f(fmaxf(amin, v))), ref_db);
+            v = fmaxf(v, -top_db);  // log_spec.max() == 0 exactly
+        }
+        return v;
+    };
+    float mean = 0.f;
+    if (mean_sub) {
+        float s = 0.f;
+        for (int t = lane; t < T; t += 64) s += val(t);
+        mean = wave_sum(s) / (float)T;
+    }
+    float* o = out + ((size_t)w * n_mels + m) * T * channels;
+    for (int t = lane; t < T; t += 64) {
+        const float v = val(t) - mean;
+        for (int c = 0; c < channels; ++c) o[t * channels + c] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static size_t fe_lds_bytes(const FePlan& p) {
+    const int nc = p.cfg.n_fft / 2;
+    const int seg_cap = ((kFpb - 1) * p.cfg.hop + p.cfg.n_fft + 3) & ~3;
+    return sizeof(float) * ((size_t)seg_cap + 4 * (size_t)nc + (size_t)p.cfg.n_mels * kFpb);
+}
+
+template <int NFFT>
+static int launch_stft(const FePlan& p, const float* pcm, const aa_window* wins, int n_win,
+                       const float4* stats, float* melS, float* blkmax, hipStream_t st) {
+    const size_t lds = fe_lds_bytes(p);
+    AA_CHECK(lds <= 150 * 1024, AA_ERR_UNSUPPORTED, "fe: hop %d needs %zu B of LDS", p.cfg.hop, lds);
+    static size_t attr_set = 0;  // dynamic LDS opt-in already granted (static LDS comes on top)
+    if (lds > attr_set) {
+        AA_HIP(hipFuncSetAttribute((const void*)fe_stft_mel<NFFT>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_set = lds;
+    }
+    dim3 grid(p.nfblk, n_win);
+    hipLaunchKernelGGL(fe_stft_mel<NFFT>, grid, dim3(NFFT / 16), lds, st, pcm, wins, stats, p.d_win,
+                       p.d_tw, p.d_tw2, p.d_rows, p.d_vals, p.cfg.win_len, p.cfg.hop, p.T,
+                       p.cfg.n_mels, p.kmin, p.kmax, p.cfg.normalize, p.cfg.power, melS, blkmax);
+    AA_LAUNCH_CHECK();
+    return AA_OK;
+}
+
+struct FeWs {
+    float4* stats;
+    float* melS;
+    float* blkmax;
+    size_t bytes;
+};
+
+static FeWs fe_ws_layout(const FePlan& p, int n_win, char* base) {
+    FeWs w{};
+    size_t off = 0;
+    w.stats = reinterpret_cast<float4*>(base + off);
+    off = align_up(off + sizeof(float4) * (size_t)n_win * kStatSplit, 256);
+    w.melS = reinterpret_cast<float*>(base + off);
+    off = align_up(off + sizeof(float) * (size_t)n_win * p.cfg.n_mels * p.T, 256);
+    w.blkmax = reinterpret_cast<float*>(base + off);
+    off = align_up(off + sizeof(float) * (size_t)n_win * p.nfblk, 256);
+    w.bytes = off;
+    return w;
+}
+
+}  // namespace aa
+
+using namespace aa;
+
+extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** plan) {
+    AA_CHECK(cfg && melfb && plan, AA_ERR_INVALID, "aa_fe_create: null argument");
+    const int n = cfg->n_fft;
+    AA_CHECK(n == 1024 || n == 2048 || n == 4096 || n == 8192, AA_ERR_UNSUPPORTED,
+             "aa_fe_create: n_fft %d not supported (power of two 1024..8192)", n);
+    AA_CHECK(cfg->hop > 0 && cfg->win_len > 0 && cfg->n_mels > 0 && cfg->channels >= 1,
+             AA_ERR_INVALID, "aa_fe_create: bad sizes");
+    FePlan* p = new FePlan();
+    p->cfg = *cfg;
+    p->T = 1 + cfg->win_len / cfg->hop;
+    p->nfblk = (p->T + kFpb - 1) / kFpb;
+    const int nbins = n / 2 + 1;
+    // CSR of the dense filterbank (rows are contiguous triangles; keep
+    // [first nonzero, last nonzero] per row)
+    std::vector<int4> rows(cfg->n_mels);
+    std::vector<float> vals;
+    int kmin = nbins, kmax = 0;
+    for (int m = 0; m < cfg->n_mels; ++m) {
+        const float* r = melfb + (size_t)m * nbins;
+        int a = -1, b = -1;
+        for (int k = 0; k < nbins; ++k)
+            if (r[k] != 0.f) { if (a < 0) a = k; b = k; }
+        if (a < 0) { a = 0; b = -1; }
+        rows[m] = make_int4(a, b - a + 1, (int)vals.size(), 0);
+        for (int k = a; k <= b; ++k) vals.push_back(r[k]);
+        if (b >= a) { kmin = std::min(kmin, a); kmax = std::max(kmax, b); }
+    }
+    if (kmax < kmin) { kmin = 0; kmax = 0; }
+    for (auto& r : rows) if (r.y == 0) r.x = kmin;
+    p->kmin = kmin;
+    p->kmax = kmax;
+    p->nnz = (int)vals.size();
+    if (vals.empty()) vals.push_back(0.f);
+    const int nc = n / 2;
+    std::vector<float> win(n);
+    for (int i = 0; i < n; ++i) win[i] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * i / n));
+    std::vector<float2> tw(nc), tw2(nc + 1);
+    for (int m = 0; m < nc; ++m) {
+        const double a = -2.0 * M_PI * m / nc;
+        tw[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    for (int k = 0; k <= nc; ++k) {
+        const double a = -2.0 * M_PI * k / n;
+        tw2[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    auto up = [](void** d, const void* h, size_t b) -> hipError_t {
+        hipError_t e = hipMalloc(d, b);
+        if (e != hipSuccess) return e;
+        return hipMemcpy(*d, h, b, hipMemcpyHostToDevice);
+    };
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = up((void**)&p->d_win, win.data(), sizeof(float) * n);
+    if (e == hipSuccess) e = up((void**)&p->d_tw, tw.data(), sizeof(float2) * nc);
+    if (e == hipSuccess) e = up((void**)&p->d_tw2, tw2.data(), sizeof(float2) * (nc + 1));
+    if (e == hipSuccess) e = up((void**)&p->d_rows, rows.data(), sizeof(int4) * rows.size());
+    if (e == hipSuccess) e = up((void**)&p->d_vals, vals.data(), sizeof(float) * vals.size());
+    if (e != hipSuccess) {
+        set_error("aa_fe_create: %s", hipGetErrorString(e));
+        aa_fe_destroy(p);
+        return AA_ERR_HIP;
+    }
+    AA_CHECK(fe_lds_bytes(*p) <= 150 * 1024, AA_ERR_UNSUPPORTED,
+             "aa_fe_create: hop %d too large for the LDS segment", cfg->hop);
+    *plan = p;
+    return AA_OK;
+}
+
+extern "C" int aa_fe_destroy(void* plan) {
+    FePlan* p = static_cast<FePlan*>(plan);
+    if (!p) return AA_OK;
+    (void)hipFree(p->d_win);
+    (void)hipFree(p->d_tw);
+    (void)hipFree(p->d_tw2);
+    (void)hipFree(p->d_rows);
+    (void)hipFree(p->d_vals);
+    delete p;
+    return AA_OK;
+}
+
+extern "C" int aa_fe_n_frames(const void* plan) {
+    return plan ? static_cast<const FePlan*>(plan)->T : -1;
+}
+
+extern "C" size_t aa_fe_workspace_bytes(const void* plan, int32_t max_windows) {
+    if (!plan || max_windows < 0) return 0;
+    return fe_ws_layout(*static_cast<const FePlan*>(plan), max_windows, nullptr).bytes;
+}
+
+extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa_window* windows,
+                         int32_t n_win, float* out, int32_t* win_status, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+    FePlan* p = static_cast<FePlan*>(plan);
+    AA_CHECK(p && pcm && windows && out, AA_ERR_INVALID, "aa_fe_run: null argument");
+    AA_CHECK(n_win >= 0, AA_ERR_INVALID, "aa_fe_run: n_win < 0");
+    (void)pcm_len;  // window views are validated by the host against pcm_len
+    if (n_win == 0) return AA_OK;
+    FeWs ws = fe_ws_layout(*p, n_win, static_cast<char*>(workspace));
+    AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE,
+             "aa_fe_run: workspace %zu < %zu bytes", workspace_bytes, ws.bytes);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(fe_stats, dim3(kStatSplit, n_win), dim3(256), 0, st, pcm, windows,
+                       p->cfg.win_len, ws.stats);
+    AA_LAUNCH_CHECK();
+    int rc;
+    switch (p->cfg.n_fft) {
+        case 1024: rc = launch_stft<1024>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
+        case 2048: rc = launch_stft<2048>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
+        case 4096: rc = launch_stft<4096>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
+        default: rc = launch_stft<8192>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
+    }
+    if (rc != AA_OK) return rc;
+    hipLaunchKernelGGL(fe_db, dim3((p->cfg.n_mels + 3) / 4, n_win), dim3(256), 0, st, ws.melS,
+                       ws.blkmax, ws.stats, p->nfblk, p->cfg.n_mels, p->T, p->cfg.db_scale,
+                       p->cfg.amin, p->cfg.top_db, p->cfg.mean_sub, p->cfg.channels,
+                       p->cfg.normalize, out, win_status);
+    AA_LAUNCH_CHECK();
+    return AA_OK;
+}

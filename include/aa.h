@@ -1,0 +1,155 @@
+/*
+ * aa.h -- C ABI of libaa.so, the MI355X (gfx950) hot path of the
+ * audio-analysis window classifier.
+ *
+ * Every entry point is plain C: device pointers, sizes, an opaque handle and a
+ * hipStream_t passed as void*.  No torch types cross this boundary.  Buffers
+ * are owned by the caller (the Python host keeps them in torch-ROCm tensors);
+ * the library allocates only per-handle constants (filterbank, twiddles,
+ * packed weights) at create time, never inside a *_run / *_forward call, so
+ * those calls can be captured into a HIP graph.
+ *
+ * Reference interfaces each group replaces (file:line in
+ * TheCacophonyProject/audio-analysis, mounted at /root/reference):
+ *   aa_fe_*      get_spect(...)                     src/identify_tracks.py:212-288
+ *                  + normalize_data                 src/identify_tracks.py:202-209
+ *                  + the per-window loop body       src/identify_tracks.py:163-193
+ *                  + custommel.mel_spec / mel_f     src/custommel.py:19-63
+ *   aa_model_*   load_model(path, meta)             src/identify_tracks.py:302-327
+ *                model.predict(np.array(d))         src/identify_tracks.py:544
+ *                MagTransform.call                  src/magtransformv2.py:19-21
+ *   aa_track_mean  np.mean over models, windows     src/identify_tracks.py:547-551
+ *
+ * Return values: AA_OK (0) or an aa_status code; aa_last_error() gives a
+ * thread-local message for the last failing call on this thread.
+ */
+#ifndef AA_H
+#define AA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AA_ABI_VERSION 1
+
+typedef enum aa_status {
+    AA_OK = 0,
+    AA_ERR_INVALID = 1,      /* bad argument / shape */
+    AA_ERR_HIP = 2,          /* HIP runtime error */
+    AA_ERR_UNSUPPORTED = 3,  /* layer pattern or size this build has no kernel for */
+    AA_ERR_WORKSPACE = 4,    /* workspace too small */
+} aa_status;
+
+/* One analysis window of `win_len` samples, as a view into the recording:
+ * samples [src, src + n_valid) of the PCM buffer, placed at offset pad_left
+ * inside the window; every other window sample is 0 (np.pad,
+ * src/identify_tracks.py:165-168).  16 bytes, device-resident array. */
+typedef struct aa_window {
+    int64_t src;
+    int32_t n_valid;
+    int32_t pad_left;
+} aa_window;
+
+/* Front-end configuration (the reference's metadata.txt keys,
+ * src/identify_tracks.py:466-497). */
+typedef struct aa_fe_config {
+    int32_t win_len;   /* samples per window: int(sr * segment_length) */
+    int32_t n_fft;     /* power of two, 1024..8192 */
+    int32_t hop;       /* hop_length */
+    int32_t n_mels;    /* rows of the filterbank */
+    int32_t normalize; /* normalize_data before the STFT */
+    int32_t db_scale;  /* librosa.power_to_db(ref=np.max) */
+    float power;       /* |S| ** power before the filterbank */
+    float amin;        /* power_to_db amin (1e-10) */
+    float top_db;      /* power_to_db top_db (80) */
+    int32_t mean_sub;  /* subtract each band's mean over time */
+    int32_t channels;  /* repeat the single channel this many times */
+} aa_fe_config;
+
+/* Per-window status flags written by aa_fe_run (device int32 array). */
+#define AA_WIN_OK 0
+#define AA_WIN_NONFINITE 1 /* librosa.util.valid_audio would raise */
+
+int aa_abi_version(void);
+const char* aa_last_error(void);
+
+/* ---------------- front end: PCM windows -> log-mel ---------------- */
+/* melfb: host float32 [n_mels][n_fft/2 + 1] dense filterbank (custommel.mel_f
+ * or the Slaney filterbank); stored on the device in CSR form. */
+int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** plan);
+int aa_fe_destroy(void* plan);
+/* frames per window T = 1 + win_len / hop */
+int aa_fe_n_frames(const void* plan);
+size_t aa_fe_workspace_bytes(const void* plan, int32_t max_windows);
+/* out: device float32 [n_win][n_mels][T][channels] (NHWC, H = mel band,
+ * W = frame), the tensor get_spect returns per window.
+ * win_status: device int32 [n_win] (AA_WIN_*), may be NULL. */
+int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa_window* windows,
+              int32_t n_win, float* out, int32_t* win_status, void* workspace,
+              size_t workspace_bytes, void* stream);
+
+/* ---------------- CNN: log-mel windows -> logits / probabilities ---------------- */
+typedef enum aa_op {
+    AA_OP_CONV2D = 1,       /* Keras Conv2D, padding="valid", stride 1 */
+    AA_OP_BATCHNORM = 2,    /* inference BatchNormalization (moving stats) */
+    AA_OP_LEAKYRELU = 3,
+    AA_OP_MAXPOOL2D = 4,    /* pool = strides, padding="valid" */
+    AA_OP_GLOBALMAXPOOL2D = 5,
+    AA_OP_SIGMOID = 6,
+    AA_OP_MAGTRANSFORM = 7, /* x ** sigmoid(a) */
+    AA_OP_RELU = 8,
+} aa_op;
+
+typedef struct aa_layer {
+    int32_t op;      /* aa_op */
+    int32_t kh, kw;  /* conv kernel or pool size */
+    int32_t filters; /* conv output channels */
+    float alpha;     /* leaky slope */
+    float eps;       /* batchnorm epsilon */
+    /* offsets (in floats) into the weight blob, -1 when absent:
+     * conv: [0]=kernel (HWIO [kh][kw][cin][cout]), [1]=bias
+     * batchnorm: [0]=gamma [1]=beta [2]=moving_mean [3]=moving_variance
+     * magtransform: [0]=a */
+    int64_t off[4];
+} aa_layer;
+
+typedef enum aa_precision {
+    AA_PREC_F32 = 0,  /* f32 MFMA (exact f32 fma chain): the parity mode */
+    AA_PREC_BF16 = 1, /* bf16 activations/weights, f32 accumulation */
+} aa_precision;
+
+int aa_model_create(const aa_layer* layers, int32_t n_layers, const float* blob, int64_t blob_len,
+                    int32_t in_h, int32_t in_w, int32_t in_c, int32_t precision, void** model);
+int aa_model_destroy(void* model);
+int aa_model_n_outputs(const void* model);
+size_t aa_model_workspace_bytes(const void* model, int32_t max_batch);
+/* x: device float32 [n][in_h][in_w][in_c]; logits: device float32 [n][L]
+ * (global-max outputs before the sigmoid); probs: [n][L] or NULL. */
+int aa_model_forward(void* model, const float* x, int32_t n, float* logits, float* probs,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* Per-stage timing of aa_model_forward (HIP events around each fused stage,
+ * on the launch stream).  Used by bench.py for the roofline of the dominant
+ * kernel. */
+int aa_model_n_stages(const void* model);
+int aa_model_stage_info(const void* model, int32_t stage, char* name, int32_t name_len,
+                        double* flops_per_item, double* bytes_per_item);
+int aa_model_set_timing(void* model, int32_t enable);
+int aa_model_stage_time(void* model, int32_t stage, double* total_ms, int64_t* count);
+
+/* ---------------- ensemble + window mean ---------------- */
+/* probs: device float32, model m / window w at probs[m * model_stride + w * n_labels].
+ * Track t averages windows [win_begin[t], win_begin[t] + win_count[t]) after
+ * averaging over models, both in float32 with sequential accumulation like
+ * numpy's axis-0 mean.  out: device float32 [n_tracks][n_labels]. */
+int aa_track_mean(const float* probs, int32_t n_models, int64_t model_stride, int32_t n_labels,
+                  const int32_t* win_begin, const int32_t* win_count, int32_t n_tracks,
+                  float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AA_H */

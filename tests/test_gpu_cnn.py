@@ -1,0 +1,69 @@
+"""GPU parity: libaa.so CNN vs the torch-CPU fp32 oracle (oracle/cnn_oracle.py).
+
+Gate (north star): max |delta logit| <= 1e-3 in the f32 MFMA mode (exact f32
+fma chains; the residual is summation order and the BN fold).  bf16 is the
+throughput mode: its delta is reported and bounded loosely, not gated at 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cnn_oracle
+from tools.make_models import calibration_input, make_model
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-3
+
+
+def _run(path, x, precision):
+    from aa_amd.model import Model
+    m = Model(path, x.shape[1:], precision=precision)
+    lg, pr = m.forward(torch.from_numpy(x).cuda())
+    torch.cuda.synchronize()
+    return lg.cpu().numpy(), pr.cpu().numpy()
+
+
+@pytest.mark.parametrize("T", [226, 513])
+def test_cnn_f32_parity(gpu, model_root, T):
+    path = model_root / "model1" / "audioModel.safetensors"
+    x = calibration_input(5, 160, T, True, np.random.default_rng(T))
+    lg, pr = _run(path, x, "f32")
+    rlg, rpr = cnn_oracle.forward(path, x)
+    err = np.abs(lg - rlg).max()
+    print(f"T={T} f32 max|dlogit|={err:.3e}")
+    assert err <= LOGIT_TOL
+    assert np.abs(pr - rpr).max() <= LOGIT_TOL
+
+
+def test_cnn_bf16_delta(gpu, model_root):
+    path = model_root / "model2" / "audioModel.safetensors"
+    x = calibration_input(8, 160, 226, True, np.random.default_rng(2))
+    lg, _ = _run(path, x, "bf16")
+    rlg, _ = cnn_oracle.forward(path, x)
+    err = np.abs(lg - rlg).max()
+    print(f"bf16 max|dlogit|={err:.3e} (logit range {rlg.min():.2f}..{rlg.max():.2f})")
+    assert err <= 0.25
+
+
+def test_cnn_magtransform(gpu, tmp_path):
+    path = make_model(tmp_path / "mag", name="magmodel", seed=11, mag=2)
+    x = calibration_input(3, 160, 226, False, np.random.default_rng(5))
+    lg, _ = _run(path, x, "f32")
+    rlg, _ = cnn_oracle.forward(path, x)
+    assert np.abs(lg - rlg).max() <= LOGIT_TOL
+
+
+def test_track_mean_matches_numpy(gpu):
+    from aa_amd.model import track_mean
+    rng = np.random.default_rng(0)
+    M, W, L = 3, 45, 24
+    probs = rng.random((M, W, L), dtype=np.float32)
+    begin = np.array([0, 39, 40], np.int32)
+    count = np.array([39, 1, 5], np.int32)
+    out = track_mean(torch.from_numpy(probs).cuda(), torch.from_numpy(begin).cuda(),
+                     torch.from_numpy(count).cuda()).cpu().numpy()
+    for t in range(3):
+        seg = probs[:, begin[t]:begin[t] + count[t]]
+        ref = np.mean(np.mean(list(seg), axis=0), axis=0)
+        assert np.array_equal(out[t], ref), t
