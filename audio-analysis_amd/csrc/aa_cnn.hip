@@ -335,13 +335,29 @@ __global__ void track_mean(const float* __restrict__ probs, int n_models, long l
     const int t = blockIdx.x;
     const int c = threadIdx.x;
     if (c >= L) return;
+    constexpr int U = 16;  // loads in flight; the adds stay in numpy's order
     float acc = 0.f;
     const int n = wc[t];
-    for (int w = 0; w < n; ++w) {
-        const size_t off = (size_t)(wb[t] + w) * L + c;
-        float m = 0.f;
-        for (int k = 0; k < n_models; ++k) m = __fadd_rn(m, probs[k * model_stride + off]);
-        acc = __fadd_rn(acc, __fdiv_rn(m, (float)n_models));
+    const float* base = probs + (size_t)wb[t] * L + c;
+    for (int w0 = 0; w0 < n; w0 += U) {
+        float v[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                v[u][k] = base[min(k, n_models - 1) * model_stride + (size_t)min(w0 + u, n - 1) * L];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (w0 + u < n) {
+                float m = 0.f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < n_models) m = __fadd_rn(m, v[u][k]);
+                for (int k = 4; k < n_models; ++k)
+                    m = __fadd_rn(m, base[k * model_stride + (size_t)(w0 + u) * L]);
+                acc = __fadd_rn(acc, __fdiv_rn(m, (float)n_models));
+            }
+        }
     }
     out[(size_t)t * L + c] = n > 0 ? __fdiv_rn(acc, (float)n) : NAN;
 }

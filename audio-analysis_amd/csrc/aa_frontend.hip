@@ -24,7 +24,7 @@
 namespace aa {
 
 constexpr int kStatSplit = 16;  // stats blocks per window
-constexpr int kFpb = 8;         // frames per stft block
+constexpr int kFpb = 6;         // frames per stft block
 
 struct FePlan {
     aa_fe_config cfg;
@@ -145,80 +145,115 @@ __device__ __forceinline__ void dft8(float2* v) {
     v[7] = csub(e3, w3);
 }
 
+// LDS index of complex point i: one float2 of padding per 8 keeps the radix-8
+// scatter of pass 1 (stride 8) and the NS = 8 scatter of pass 2 conflict-free.
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 3); }
+
 // One Stockham pass of radix R over NC points held in LDS (src -> dst), for
 // sub-transform size NS (product of the earlier radices).  Thread handles
-// butterflies j = tid, tid + NT, ...
+// butterflies j = tid + b*NT.  Its twiddles depend only on (j, NS), so they
+// are loaded once per block into registers (load) and reused for every frame.
 template <int NC, int R, int NT, int NS>
-__device__ __forceinline__ void stockham_pass(const float2* __restrict__ src, float2* __restrict__ dst,
-                                              const float2* __restrict__ tw) {
-    constexpr int NB = NC / R;
+struct Pass {
+    static constexpr int NB = NC / R;
+    static constexpr int PER = (NB + NT - 1) / NT;
+    float2 t[PER][R - 1];
+    __device__ __forceinline__ void load(const float2* __restrict__ tw) {
 #pragma unroll
-    for (int jj = 0; jj < (NB + NT - 1) / NT; ++jj) {
-        const int j = threadIdx.x + jj * NT;
-        if (NB % NT == 0 || j < NB) {
-            float2 v[R];
+        for (int b = 0; b < PER; ++b) {
+            const int j = threadIdx.x + b * NT;
             const int k = j % NS;
 #pragma unroll
-            for (int r = 0; r < R; ++r) v[r] = src[j + r * NB];
-            if constexpr (NS > 1) {
-                constexpr int step = NC / (NS * R);
-#pragma unroll
-                for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k * step]);
-            }
-            if constexpr (R == 8) dft8(v);
-            if constexpr (R == 4) dft4(v[0], v[1], v[2], v[3]);
-            if constexpr (R == 2) dft2(v[0], v[1]);
-            const int o = (j / NS) * NS * R + k;
-#pragma unroll
-            for (int r = 0; r < R; ++r) dst[o + r * NS] = v[r];
+            for (int r = 1; r < R; ++r)  // unconditional loads: all in flight together
+                t[b][r - 1] = tw[(r * k * (NC / (NS * R))) & (NC - 1)];
         }
     }
-}
-
-// Remaining passes after the first radix-8 pass; returns the buffer holding
-// the natural-order result (the other one is free).
-template <int NC, int NT, int NS>
-__device__ __forceinline__ float2* fft_rest(float2* src, float2* dst, const float2* __restrict__ tw) {
-    if constexpr (NS * 8 <= NC) {
-        stockham_pass<NC, 8, NT, NS>(src, dst, tw);
-        __syncthreads();
-        return fft_rest<NC, NT, NS * 8>(dst, src, tw);
-    } else if constexpr (NC / NS == 4) {
-        stockham_pass<NC, 4, NT, NS>(src, dst, tw);
-        __syncthreads();
-        return dst;
-    } else if constexpr (NC / NS == 2) {
-        stockham_pass<NC, 2, NT, NS>(src, dst, tw);
-        __syncthreads();
-        return dst;
-    } else {
-        return src;
+    __device__ __forceinline__ void run(const float2* __restrict__ src, float2* __restrict__ dst) const {
+#pragma unroll
+        for (int b = 0; b < PER; ++b) {
+            const int j = threadIdx.x + b * NT;
+            if (NB % NT == 0 || j < NB) {
+                float2 v[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[r] = src[pidx(j + r * NB)];
+                if constexpr (NS > 1) {
+#pragma unroll
+                    for (int r = 1; r < R; ++r) v[r] = cmul(v[r], t[b][r - 1]);
+                }
+                if constexpr (R == 8) dft8(v);
+                if constexpr (R == 4) dft4(v[0], v[1], v[2], v[3]);
+                if constexpr (R == 2) dft2(v[0], v[1]);
+                const int k = j % NS;
+                const int o = (j / NS) * NS * R + k;
+#pragma unroll
+                for (int r = 0; r < R; ++r) dst[pidx(o + r * NS)] = v[r];
+            }
+        }
     }
-}
+};
 
 // ---------------------------------------------------------------------------
 // fe_stft_mel
+// Transform plan for NC = NFFT/2 complex points with NT = NC/8 threads:
+//   pass 1  radix 8, NS = 1   (input read from the windowed PCM segment)
+//   pass 2  radix 8, NS = 8
+//   pass 3  radix 8, NS = 64
+//   pass 4  radix NC/512, NS = 512   (NC = 1024: 2, 2048: 4, 4096: 8)
 // ---------------------------------------------------------------------------
 template <int NFFT>
 __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
     const float* __restrict__ pcm, const aa_window* __restrict__ wins, const float4* __restrict__ stats,
     const float* __restrict__ hann, const float2* __restrict__ tw, const float2* __restrict__ tw2,
-    const int4* __restrict__ rows, const float* __restrict__ vals, int win_len, int hop, int T,
-    int n_mels, int kmin, int kmax, int normalize, float power, float* __restrict__ melS,
-    float* __restrict__ blkmax) {
+    const int4* __restrict__ rows, const float* __restrict__ vals, int nnz, int win_len, int hop, int T,
+    int n_mels, int kmin, int kmax, int normalize, float power, int nfblk, int n_items,
+    float* __restrict__ melS, float* __restrict__ blkmax) {
     constexpr int NC = NFFT / 2;
     constexpr int NT = NC / 8;
+    constexpr int R4 = NC / 512;
+    static_assert(NC >= 1024 && NC <= 4096, "NFFT 2048..8192");
+    constexpr int KREG = 4;  // post-processing bins per thread with register twiddles
     extern __shared__ float lds[];
-    const int w = blockIdx.y;
-    const int f0 = blockIdx.x * kFpb;
-    const int nf = min(kFpb, T - f0);
-    const int seg_len = (nf - 1) * hop + NFFT;
     float* seg = lds;
     const int seg_cap = ((kFpb - 1) * hop + NFFT + 3) & ~3;
     float2* bufA = reinterpret_cast<float2*>(lds + seg_cap);
-    float2* bufB = bufA + NC;
-    float* melT = reinterpret_cast<float*>(bufB + NC);  // [n_mels][kFpb] staging
+    constexpr int NCP = NC + NC / 8;  // padded buffer length (float2)
+    float2* bufB = bufA + NCP;
+    float* melT = reinterpret_cast<float*>(bufB + NCP);  // [n_mels][kFpb] staging
+    int4* srows = reinterpret_cast<int4*>(melT + ((n_mels * kFpb + 3) & ~3));
+    float* svals = reinterpret_cast<float*>(srows + n_mels);
 
+    // --- per-thread constants, loaded once per block ---
+    const int tid = threadIdx.x;
+    float hw[8][2];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int n = tid + r * (NC / 8);
+        const float2 h = reinterpret_cast<const float2*>(hann)[n];
+        hw[r][0] = h.x;
+        hw[r][1] = h.y;
+    }
+    Pass<NC, 8, NT, 8> p2;
+    Pass<NC, 8, NT, 64> p3;
+    Pass<NC, R4, NT, 512> p4;
+    p2.load(tw);
+    p3.load(tw);
+    p4.load(tw);
+    float2 w2r[KREG];
+#pragma unroll
+    for (int i = 0; i < KREG; ++i) {
+        w2r[i] = tw2[min(kmin + tid + i * NT, kmax)];
+    }
+    for (int i = tid; i < n_mels; i += NT) srows[i] = rows[i];
+    for (int i = tid; i < nnz; i += NT) svals[i] = vals[i];
+
+    __syncthreads();
+    // persistent loop over (window, frame block) items
+    for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const int w = item / nfblk;
+    const int fb = item - w * nfblk;
+    const int f0 = fb * kFpb;
+    const int nf = min(kFpb, T - f0);
+    const int seg_len = (nf - 1) * hop + NFFT;
     // --- normalisation constants (normalize_data, :203-208) ---
     const aa_window d = wins[w];
     float lo = INFINITY, hi = -INFINITY;
@@ -230,62 +265,89 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
     }
     const float scale = __fsub_rn(hi, lo);  // == max(x - min) (monotone rounding)
 
-    // --- overlapped segment -> LDS, normalised ---
+    // --- overlapped segment -> LDS, normalised; loads issued in batches of
+    // SEGU per thread before any is consumed ---
     const int base = f0 * hop - NFFT / 2;  // window index of seg[0]
-    for (int q = threadIdx.x; q < seg_len; q += NT) {
-        const int i = base + q;
-        float v = 0.f;
-        if (i >= 0 && i < win_len) {
+    constexpr int SEGU = 8;
+    const long long safe = d.n_valid > 0 ? d.src : 0;  // any in-bounds sample
+    for (int q0 = 0; q0 < seg_len; q0 += SEGU * NT) {
+        float raw[SEGU];
+        bool ok[SEGU];
+#pragma unroll
+        for (int u = 0; u < SEGU; ++u) {  // unconditional loads from clamped addresses
+            const int q = q0 + u * NT + tid;
+            const int i = base + q;
             const int rel = i - d.pad_left;
-            const float raw = (rel >= 0 && rel < d.n_valid) ? pcm[d.src + rel] : 0.f;
-            if (normalize) {
-                float y = __fdiv_rn(__fsub_rn(raw, lo), scale);
-                y = __fadd_rn(y, 0.000001f);
-                y = __fsub_rn(y, 0.5f);
-                v = __fmul_rn(y, 2.0f);
-            } else {
-                v = raw;
+            ok[u] = q < seg_len && i >= 0 && i < win_len && rel >= 0 && rel < d.n_valid;
+            raw[u] = pcm[ok[u] ? d.src + rel : safe];
+        }
+#pragma unroll
+        for (int u = 0; u < SEGU; ++u) {
+            const int q = q0 + u * NT + tid;
+            const int i = base + q;
+            if (q < seg_len) {
+                float v = 0.f;
+                if (i >= 0 && i < win_len) {
+                    v = ok[u] ? raw[u] : 0.f;
+                    if (normalize) {
+                        float y = __fdiv_rn(__fsub_rn(v, lo), scale);
+                        y = __fadd_rn(y, 0.000001f);
+                        y = __fsub_rn(y, 0.5f);
+                        v = __fmul_rn(y, 2.0f);
+                    }
+                }
+                seg[q] = v;
             }
         }
-        seg[q] = v;
     }
     __syncthreads();
 
     float bmax = 0.f;
     for (int f = 0; f < nf; ++f) {
-        // pass 1 (Ns = 1) straight from the segment: z[n] = xw[2n] + i xw[2n+1]
+        // pass 1 (NS = 1) straight from the segment: z[n] = xw[2n] + i xw[2n+1]
         {
             const float* x = seg + f * hop;
-            constexpr int NB = NC / 8;
-            const int j = threadIdx.x;
             float2 v[8];
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
-                const int n = j + r * NB;
-                v[r] = make_float2(x[2 * n] * hann[2 * n], x[2 * n + 1] * hann[2 * n + 1]);
+                const int n = tid + r * NT;
+                v[r] = make_float2(x[2 * n] * hw[r][0], x[2 * n + 1] * hw[r][1]);
             }
             dft8(v);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) bufA[j * 8 + r] = v[r];
+            for (int r = 0; r < 8; ++r) bufA[pidx(tid * 8 + r)] = v[r];
         }
         __syncthreads();
-        float2* src = fft_rest<NC, NT, 8>(bufA, bufB, tw);
-        float2* dst = (src == bufA) ? bufB : bufA;
-        // src now holds Z[0..NC) in natural order; dst is free scratch for P.
-        float* Pf = reinterpret_cast<float*>(dst);
-        for (int k = kmin + threadIdx.x; k <= kmax; k += NT) {
+        p2.run(bufA, bufB);
+        __syncthreads();
+        p3.run(bufB, bufA);
+        __syncthreads();
+        p4.run(bufA, bufB);
+        __syncthreads();
+        const float2* Z = bufB;             // natural order
+        float* Pf = reinterpret_cast<float*>(bufA);  // free scratch for |X|^p
+        for (int i = 0; kmin + tid + i * NT <= kmax; ++i) {
+            const int k = kmin + tid + i * NT;
             float re, im;
             if (k == 0 || k == NC) {
-                const float2 z0 = src[0];
+                const float2 z0 = Z[0];  // pidx(0) == 0
                 re = (k == 0) ? z0.x + z0.y : z0.x - z0.y;
                 im = 0.f;
             } else {
-                const float2 a = src[k];
-                const float2 b = src[NC - k];  // conj taken below
+                const float2 a = Z[pidx(k)];
+                const float2 b = Z[pidx(NC - k)];  // conj taken below
                 // E = (a + conj b)/2 ; O = -i (a - conj b)/2 ; X = E + W^k O
                 const float2 E = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
                 const float2 O = make_float2(0.5f * (a.y + b.y), -0.5f * (a.x - b.x));
-                const float2 X = cadd(E, cmul(tw2[k], O));
+                float2 wk;
+                if (i < KREG) {
+                    wk = w2r[0];
+#pragma unroll
+                    for (int q = 1; q < KREG; ++q) if (i == q) wk = w2r[q];
+                } else {
+                    wk = tw2[k];
+                }
+                const float2 X = cadd(E, cmul(wk, O));
                 re = X.x;
                 im = X.y;
             }
@@ -298,29 +360,43 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
             Pf[k - kmin] = pw;
         }
         __syncthreads();
-        for (int m = threadIdx.x; m < n_mels; m += NT) {
-            const int4 rw = rows[m];
+        for (int m = tid; m < n_mels; m += NT) {
+            const int4 rw = srows[m];
+            const float* wv = svals + rw.z;
+            const float* pv = Pf + (rw.x - kmin);
             float s = 0.f;
-            for (int i = 0; i < rw.y; ++i) s = fmaf(vals[rw.z + i], Pf[rw.x - kmin + i], s);
+            // predicated 16-wide chunks: all LDS reads of a chunk in flight at once
+            for (int i0 = 0; i0 < rw.y; i0 += 16) {
+                float a[16], b[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int ii = min(i0 + i, rw.y - 1);  // unconditional LDS reads
+                    a[i] = (i0 + i < rw.y) ? wv[ii] : 0.f;
+                    b[i] = pv[ii];
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i) s = fmaf(a[i], b[i], s);
+            }
             melT[m * kFpb + f] = s;
             bmax = fmaxf(bmax, s);
         }
         __syncthreads();  // P / buffers reused by the next frame
     }
     // staged [n_mels][nf] tile -> melS[w][m][f0 .. f0 + nf)
-    for (int idx = threadIdx.x; idx < n_mels * nf; idx += NT) {
+    for (int idx = tid; idx < n_mels * nf; idx += NT) {
         const int m = idx / nf, f = idx - (idx / nf) * nf;
         melS[((size_t)w * n_mels + m) * T + f0 + f] = melT[m * kFpb + f];
     }
-    // block max -> blkmax[w][blockIdx.x]
+    // item max -> blkmax[w][fb]
     __shared__ float red[NT / 64];
     bmax = wave_max(bmax);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bmax;
+    if ((tid & 63) == 0) red[tid >> 6] = bmax;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         for (int k = 1; k < NT / 64; ++k) bmax = fmaxf(bmax, red[k]);
-        blkmax[w * gridDim.x + blockIdx.x] = bmax;
+        blkmax[w * nfblk + fb] = bmax;
     }
+    }  // item loop
 }
 
 // ---------------------------------------------------------------------------
@@ -380,7 +456,8 @@ __global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melS, con
 static size_t fe_lds_bytes(const FePlan& p) {
     const int nc = p.cfg.n_fft / 2;
     const int seg_cap = ((kFpb - 1) * p.cfg.hop + p.cfg.n_fft + 3) & ~3;
-    return sizeof(float) * ((size_t)seg_cap + 4 * (size_t)nc + (size_t)p.cfg.n_mels * kFpb);
+    return sizeof(float) * ((size_t)seg_cap + 4 * (size_t)(nc + nc / 8) + (size_t)((p.cfg.n_mels * kFpb + 3) & ~3) + 4 * (size_t)p.cfg.n_mels +
+                            (size_t)std::max(p.nnz, 1));
 }
 
 template <int NFFT>
@@ -394,10 +471,14 @@ static int launch_stft(const FePlan& p, const float* pcm, const aa_window* wins,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr_set = lds;
     }
-    dim3 grid(p.nfblk, n_win);
-    hipLaunchKernelGGL(fe_stft_mel<NFFT>, grid, dim3(NFFT / 16), lds, st, pcm, wins, stats, p.d_win,
-                       p.d_tw, p.d_tw2, p.d_rows, p.d_vals, p.cfg.win_len, p.cfg.hop, p.T,
-                       p.cfg.n_mels, p.kmin, p.kmax, p.cfg.normalize, p.cfg.power, melS, blkmax);
+    const int n_items = p.nfblk * n_win;
+    // persistent grid: as many blocks as fit (LDS-limited) on 256 CUs
+    const int per_cu = std::max(1, (int)((160 * 1024) / (lds + 256)));
+    const int grid = std::min(n_items, 256 * per_cu);
+    hipLaunchKernelGGL(fe_stft_mel<NFFT>, dim3(grid), dim3(NFFT / 16), lds, st, pcm, wins, stats, p.d_win,
+                       p.d_tw, p.d_tw2, p.d_rows, p.d_vals, p.nnz, p.cfg.win_len, p.cfg.hop, p.T,
+                       p.cfg.n_mels, p.kmin, p.kmax, p.cfg.normalize, p.cfg.power, p.nfblk, n_items,
+                       melS, blkmax);
     AA_LAUNCH_CHECK();
     return AA_OK;
 }
@@ -429,8 +510,8 @@ using namespace aa;
 extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** plan) {
     AA_CHECK(cfg && melfb && plan, AA_ERR_INVALID, "aa_fe_create: null argument");
     const int n = cfg->n_fft;
-    AA_CHECK(n == 1024 || n == 2048 || n == 4096 || n == 8192, AA_ERR_UNSUPPORTED,
-             "aa_fe_create: n_fft %d not supported (power of two 1024..8192)", n);
+    AA_CHECK(n == 2048 || n == 4096 || n == 8192, AA_ERR_UNSUPPORTED,
+             "aa_fe_create: n_fft %d not supported (power of two 2048..8192)", n);
     AA_CHECK(cfg->hop > 0 && cfg->win_len > 0 && cfg->n_mels > 0 && cfg->channels >= 1,
              AA_ERR_INVALID, "aa_fe_create: bad sizes");
     FePlan* p = new FePlan();
@@ -531,7 +612,6 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
     AA_LAUNCH_CHECK();
     int rc;
     switch (p->cfg.n_fft) {
-        case 1024: rc = launch_stft<1024>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
         case 2048: rc = launch_stft<2048>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
         case 4096: rc = launch_stft<4096>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
         default: rc = launch_stft<8192>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;

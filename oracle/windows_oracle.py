@@ -42,6 +42,7 @@ def track_windows(frames, sr, track, segment_length, stride, fmin, fmax,
                     stop = len(frames)
                     lo = max(stop - size, 0)
                 hi = stop
+            assert hi - lo == size  # src/identify_tracks.py:146
         seg = frames[lo:hi]
     w_lo = 0
     w_hi = min(hi, size)

@@ -1,0 +1,44 @@
+"""libaa.so loads (CPU host, no GPU calls) and exports exactly the C ABI that
+include/aa.h declares; argument validation fails loudly before any HIP call."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+
+from aa_amd import _lib
+
+HEADER = Path(__file__).resolve().parent.parent / "include" / "aa.h"
+
+
+def declared():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(aa_\w+)\s*\(", text, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    names = declared()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(L, n), n
+    assert sorted(_lib.EXPORTED) == names
+
+
+def test_abi_version_and_struct_sizes():
+    assert _lib.lib().aa_abi_version() == _lib.ABI_VERSION
+    assert C.sizeof(_lib.Window) == 16
+    assert C.sizeof(_lib.Layer) == 6 * 4 + 4 * 8
+    assert C.sizeof(_lib.FeConfig) == 11 * 4
+
+
+def test_invalid_arguments_fail_without_gpu():
+    L = _lib.lib()
+    h = C.c_void_p()
+    cfg = _lib.FeConfig(win_len=144000, n_fft=1000, hop=640, n_mels=160, normalize=1,
+                        db_scale=1, power=2.0, amin=1e-10, top_db=80.0, mean_sub=0, channels=1)
+    fb = np.zeros((160, 501), np.float32)
+    rc = L.aa_fe_create(C.byref(cfg), fb.ctypes.data, C.byref(h))
+    assert rc == 3 and b"n_fft" in L.aa_last_error()
+    assert L.aa_model_create(None, 0, None, 0, 1, 1, 1, 0, C.byref(h)) == 1
+    assert L.aa_fe_run(None, None, 0, None, 0, None, None, None, 0, None) == 1

@@ -1,0 +1,111 @@
+"""Host-side logic of the product (no GPU): filterbanks, window scheduler,
+window packing, model-file parsing."""
+import json
+import types
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from aa_amd import melbank
+from aa_amd.frontend import FeSettings, pack_windows
+from aa_amd.windows import schedule, track_windows
+from oracle import fe_oracle
+
+G = Path(__file__).parent / "golden"
+
+
+def test_product_custom_mel_bitexact_vs_reference():
+    g = np.load(G / "mel_f.npz")
+    for k in [k for k in g.files if not k.endswith("__cfg")]:
+        sr, nm, fmin, fmax, nfft, brk = g[k + "__cfg"]
+        assert np.array_equal(melbank.htk_break(int(sr), int(nm), fmin, fmax, int(nfft), brk), g[k])
+
+
+def test_product_slaney_matches_oracle():
+    for (nfft, nm) in [(4096, 160), (2048, 80), (4096, 128)]:
+        a = melbank.slaney(48000, nfft, nm, 50, 11000)
+        b = fe_oracle.slaney_mel_filterbank(48000, nfft, nm, 50, 11000)
+        assert np.array_equal(a, b)
+
+
+def _tracks(c):
+    return [types.SimpleNamespace(start=s, end=e, length=e - s, freq_start=f0, freq_end=f1)
+            for s, e, f0, f1 in c["tracks"]]
+
+
+def test_scheduler_bitexact_vs_reference():
+    for c in json.load(open(G / "windows.json")):
+        np.random.seed(c["seed"])
+        if "error" in c:
+            with pytest.raises(AssertionError):
+                schedule(c["clip_samples"], c["sr"], _tracks(c), 3, 1.5, 50, 11000,
+                         c["pad_short_tracks"])
+            continue
+        got = schedule(c["clip_samples"], c["sr"], _tracks(c), 3, 1.5, 50, 11000,
+                       c["pad_short_tracks"])
+        assert len(got) == len(c["windows"])
+        for g_tr, w_tr in zip(got, c["windows"]):
+            assert len(g_tr) == len(w_tr)
+            for (src, nv, left), (wsrc, wnv, wleft) in zip(g_tr, w_tr):
+                assert nv == wnv
+                if nv:  # an empty window's pad offset is unobservable
+                    assert (src, left) == (wsrc, wleft)
+
+
+def test_scheduler_consumes_rng_like_reference():
+    """Windows after an empty/short one keep parity only if every randint
+    draw happens in the reference's order."""
+    np.random.seed(42)
+    a = track_windows(2_880_000, 48000, 55.0, 65.0, 10.0, 0, 24000, 3, 1.5, 50, 11000)
+    after_a = np.random.randint(0, 1 << 30)
+    np.random.seed(42)
+    from oracle.windows_oracle import track_windows as ref_tw
+    frames = np.arange(1, 2_880_001, dtype=np.float32)
+    b = ref_tw(frames, 48000, types.SimpleNamespace(start=55.0, end=65.0, length=10.0,
+                                                    freq_start=0, freq_end=24000),
+               3, 1.5, 50, 11000)
+    assert np.random.randint(0, 1 << 30) == after_a
+    assert len(a) == len(b)
+
+
+def test_sixty_second_track_gives_39_windows():
+    v = track_windows(2_880_000, 48000, 0.0, 60.0, 60.0, 0, 24000, 3, 1.5, 50, 11000)
+    assert len(v) == 39
+    assert v[0] == (0, 144000, 0) and v[-1] == (2_736_000, 144000, 0)
+
+
+def test_pack_windows_layout():
+    arr = pack_windows([(10, 144000, 0), (5, 7, 3)], 200000, offset=100)
+    assert arr.dtype == np.int64 and arr.shape == (2, 2)
+    raw = arr.tobytes()
+    src, nv, left = np.frombuffer(raw[:16], dtype=np.int64)[0], *np.frombuffer(raw[8:16], dtype=np.int32)
+    assert (src, nv, left) == (110, 144000, 0)
+    with pytest.raises(ValueError):
+        pack_windows([(199990, 20, 0)], 200000)
+    with pytest.raises(ValueError):
+        pack_windows([(0, 144000, 5)], 200000, win_len=144000)
+
+
+def test_fe_settings_defaults_follow_reference():
+    s = FeSettings()
+    assert (s.n_fft, s.hop_length, s.n_mels, s.fmin, s.fmax, s.break_freq) == (4096, 640, 160, 50, 11000, 1750)
+    assert s.htk is False and s.db_scale is True and s.normalize is True  # :482, :486, :497
+    assert s.win_len == 144000 and s.n_frames == 226
+    assert FeSettings(hop_length=281).n_frames == 513
+    assert FeSettings(htk=False, power=1).effective_power == 2.0  # melspectrogram ignores meta.power
+
+
+def test_layer_table_from_model_file(model_root):
+    from aa_amd.model import layer_table, load_model_meta, read_arch, weights_path
+    p = model_root / "model1" / "audioModel.keras"  # reference-style path resolves
+    assert weights_path(p) == model_root / "model1" / "audioModel.safetensors"
+    meta = load_model_meta(p)
+    assert meta["name"] == "model1" and len(meta["labels"]) == len(meta["ebird_ids"])
+    arch, tensors = read_arch(weights_path(p))
+    layers, blob = layer_table(arch, tensors)
+    assert len(layers) == len(arch)
+    conv = layers[0]
+    assert (conv.op, conv.kh, conv.kw, conv.filters) == (1, 3, 3, 32)
+    k = tensors["conv1.kernel"].reshape(-1)
+    assert np.array_equal(blob[conv.off[0]:conv.off[0] + k.size], k)
