@@ -400,6 +400,287 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
 }
 
 // ---------------------------------------------------------------------------
+// fe_stft_mel_4096: the n_fft = 4096 path, one WAVE per frame.
+//
+// z[n] = x[2n] + i x[2n+1] (2048 complex points), four-step FFT with 64 lanes:
+//   n = c + 64 r (lane c holds r = 0..31 in registers)
+//   1. DFT-32 over r in registers                   -> Y[k1][c]
+//   2. Y[k1][c] *= W2048^(c k1)                     (per-lane register twiddles)
+//   3. transpose through a per-wave LDS buffer (two half passes, rows padded
+//      to 66 float2 so both the row writes and the strided reads are
+//      conflict-free): lane L = 2 k1 + h gets Y[k1][h + 2m], m = 0..31
+//   4. DFT-32 over m in registers -> E_h[k2']
+//   5. radix-2 across the lane pair (DPP quad_perm swap):
+//      Z[k1 + 32 k2'] = E0 + W64^k2' E1, Z[k1 + 32 (k2' + 32)] = E0 - W64^k2' E1
+//   6. real split X[k] = E + W4096^k O from Z[k], conj Z[2048 - k]
+//   7. periodic Hann applied in frequency: Xw[k] = X[k]/2 - (X[k-1] + X[k+1])/4,
+//      |Xw|^power into LDS
+//   8. sparse mel rows (CSR in LDS) -> block staging tile -> melS
+// Block = 4 waves = 4 consecutive frames of one window sharing one normalised
+// PCM segment; 2 blocks per CU.  Only wave-level synchronisation inside a frame.
+// ---------------------------------------------------------------------------
+#include "aa_twiddles.h"
+
+constexpr int kFpg = 4;                 // frames (waves) per block
+constexpr int kRow = 66;                // padded transpose row (float2)
+constexpr int kHalf = 16 * kRow;        // per-wave buffer (float2)
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float2 wconst32(int k) { return make_float2(kW32[k][0], kW32[k][1]); }
+__device__ __forceinline__ float2 wconst64(int k) { return make_float2(kW64[k][0], kW64[k][1]); }
+
+// 32-point DFT in registers, in place: 4 interleaved DFT-8s, twiddles, DFT-4s.
+// Output X[k] is left in v[dperm(k)], dperm(k) = 4 (k % 8) + k / 8 (a
+// compile-time permutation, so no data moves).
+__device__ __forceinline__ constexpr int dperm(int k) { return 4 * (k & 7) + (k >> 3); }
+__device__ __forceinline__ void dft32(float2* v) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        float2 t[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) t[m] = v[4 * m + p];
+        dft8(t);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[4 * m + p] = t[m];
+    }
+#pragma unroll
+    for (int p = 1; p < 4; ++p)
+#pragma unroll
+        for (int k = 1; k < 8; ++k) v[4 * k + p] = cmul(v[4 * k + p], wconst32(p * k));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dft4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+}
+
+__device__ __forceinline__ float swap_pair(float x) {  // value of lane ^ 1
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
+}
+
+__global__ __launch_bounds__(256) void fe_stft_mel_4096(
+    const float* __restrict__ pcm, const aa_window* __restrict__ wins, const float4* __restrict__ stats,
+    const float2* __restrict__ tw, const float2* __restrict__ tw2, const int4* __restrict__ rows,
+    const float* __restrict__ vals, int nnz, int win_len, int hop, int T, int n_mels, int kmin, int kmax,
+    int normalize, float power, int ngrp, int n_items, float* __restrict__ melS,
+    float* __restrict__ blkmax) {
+    constexpr int NC = 2048;
+    extern __shared__ float lds[];
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int seg_cap = ((kFpg - 1) * hop + 4096 + 3) & ~3;
+    float* seg = lds;
+    float2* wb = reinterpret_cast<float2*>(seg + seg_cap) + wave * kHalf;  // this wave's buffer
+    float2* stw2 = reinterpret_cast<float2*>(seg + seg_cap) + kFpg * kHalf;  // W4096^k, k <= 1024
+    float* melT = reinterpret_cast<float*>(stw2 + 1026);                     // [n_mels][kFpg]
+    int4* srows = reinterpret_cast<int4*>(melT + ((n_mels * kFpg + 3) & ~3));
+    float* svals = reinterpret_cast<float*>(srows + n_mels);
+    const int xlo = max(kmin - 1, 0), xhi = min(kmax + 1, NC);  // X bins kept
+
+    // ---- per-block constants ----
+    for (int i = tid; i <= 1024; i += 256) stw2[i] = tw2[i];
+    for (int i = tid; i < n_mels; i += 256) srows[i] = rows[i];
+    for (int i = tid; i < nnz; i += 256) svals[i] = vals[i];
+    // step-2 twiddles W2048^(c k1) = (W^8c)^(k1/8) (W^c)^(k1%8): two short power
+    // ladders from two table entries (<= 4 roundings per twiddle)
+    float2 p1[8], p8[4];
+    p1[0] = make_float2(1.f, 0.f);
+    p1[1] = tw[lane];
+#pragma unroll
+    for (int i = 2; i < 8; ++i) p1[i] = cmul(p1[i - 1], p1[1]);
+    p8[0] = make_float2(1.f, 0.f);
+    p8[1] = tw[(8 * lane) & (NC - 1)];
+    p8[2] = cmul(p8[1], p8[1]);
+    p8[3] = cmul(p8[2], p8[1]);
+
+
+    const int k1 = lane >> 1, h = lane & 1;
+    {
+        const int item = blockIdx.x;
+        const int w = item / ngrp;
+        const int g = item - w * ngrp;
+        const int f0 = g * kFpg;
+        const int nf = min(kFpg, T - f0);
+        const int seg_len = (nf - 1) * hop + 4096;
+        const aa_window d = wins[w];
+        float lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+        for (int s = 0; s < kStatSplit; ++s) {
+            const float4 st = stats[w * kStatSplit + s];
+            lo = fminf(lo, st.x);
+            hi = fmaxf(hi, st.y);
+        }
+        const float scale = __fsub_rn(hi, lo);
+        // ---- normalised overlapped segment (all 512 threads) ----
+        {
+            const int base = f0 * hop - 2048;
+            constexpr int SEGU = 8;
+            const long long safe = d.n_valid > 0 ? d.src : 0;
+            for (int q0 = 0; q0 < seg_len; q0 += SEGU * 256) {
+                float raw[SEGU];
+                bool ok[SEGU];
+#pragma unroll
+                for (int u = 0; u < SEGU; ++u) {
+                    const int q = q0 + u * 256 + tid;
+                    const int i = base + q;
+                    const int rel = i - d.pad_left;
+                    ok[u] = q < seg_len && i >= 0 && i < win_len && rel >= 0 && rel < d.n_valid;
+                    raw[u] = pcm[ok[u] ? d.src + rel : safe];
+                }
+#pragma unroll
+                for (int u = 0; u < SEGU; ++u) {
+                    const int q = q0 + u * 256 + tid;
+                    const int i = base + q;
+                    if (q < seg_len) {
+                        float v = 0.f;
+                        if (i >= 0 && i < win_len) {
+                            v = ok[u] ? raw[u] : 0.f;
+                            if (normalize) {
+                                float y = __fdiv_rn(__fsub_rn(v, lo), scale);
+                                y = __fadd_rn(y, 0.000001f);
+                                y = __fsub_rn(y, 0.5f);
+                                v = __fmul_rn(y, 2.0f);
+                            }
+                        }
+                        seg[q] = v;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        float bmax = 0.f;
+        if (wave < nf) {
+            // ---- 1. load + DFT-32 over r ----
+            float2 y[32];
+            const float* x = seg + wave * hop + 2 * lane;
+#pragma unroll
+            for (int r = 0; r < 32; ++r) y[r] = make_float2(x[128 * r], x[128 * r + 1]);
+            dft32(y);
+            // ---- 2. twiddle ----
+#pragma unroll
+            for (int k = 1; k < 32; ++k) {
+                const float2 t = (k & 7) == 0 ? p8[k >> 3] : (k < 8 ? p1[k] : cmul(p8[k >> 3], p1[k & 7]));
+                y[dperm(k)] = cmul(y[dperm(k)], t);
+            }
+            // ---- 3. transpose in two halves ----
+            float2 u[32];
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) wb[k * kRow + lane] = y[dperm(half * 16 + k)];
+                wave_sync();
+                if ((lane >> 5) == half) {
+                    const float2* src = wb + (k1 - 16 * half) * kRow + h;
+#pragma unroll
+                    for (int m = 0; m < 32; ++m) u[m] = src[2 * m];
+                }
+                wave_sync();
+            }
+            // ---- 4. DFT-32 over m ----
+            dft32(u);
+            // ---- 5. radix-2 across the lane pair ----
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                const float2 e = u[dperm(j)];
+                const float2 o = make_float2(swap_pair(e.x), swap_pair(e.y));
+                const float2 E0 = h ? o : e, E1 = h ? e : o;
+                const float2 t = cmul(wconst64(j), E1);
+                u[dperm(j)] = h ? csub(E0, t) : cadd(E0, t);
+            }
+            // lane holds Z[k1 + 32 (32 h + j)] in u[dperm(j)]
+            // ---- 6. real split ----
+            if (h) {
+#pragma unroll
+                for (int j = 0; j < 32; ++j) wb[k1 + 32 * j] = u[dperm(j)];  // Z[1024 + k1 + 32 j]
+            }
+            wave_sync();
+            // h = 0 lanes: X[k], k = k1 + 32 j < 1024 (bands above NC/2 take the
+            // generic kernel, see fe_fast4096)
+            if (!h) {
+#pragma unroll
+                for (int j = 0; j < 32; ++j) {
+                    const int k = k1 + 32 * j;
+                    const float2 a = u[dperm(j)];
+                    const float2 zb = wb[k == 0 ? 0 : 1024 - k];
+                    const float2 b = (k == 0) ? a : zb;  // Z[NC - k]
+                    const float2 E = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+                    const float2 O = make_float2(0.5f * (a.y + b.y), -0.5f * (a.x - b.x));
+                    const float2 t = cmul(stw2[k], O);
+                    u[dperm(j)] = cadd(E, t);
+                }
+            }
+            wave_sync();
+            if (!h) {
+#pragma unroll
+                for (int j = 0; j < 32; ++j) {
+                    const int k = k1 + 32 * j;
+                    if (k >= xlo && k <= xhi) wb[k - xlo] = u[dperm(j)];
+                }
+            }
+            wave_sync();
+            // ---- 7. Hann in frequency, |.|^power ----
+            constexpr int PT = kHalf / 64 - 1;  // 15 bins per lane: nb <= 960 (host-checked)
+            float pw[PT];
+            const int nb = kmax - kmin + 1;
+#pragma unroll
+            for (int t = 0; t < PT; ++t) {
+                const int k = min(kmin + lane + 64 * t, kmax);  // clamped: unconditional LDS reads
+                const float2 c0 = wb[k - xlo];
+                float2 cm = wb[max(k - 1, 0) - xlo + (k == 0 ? 1 : 0)];
+                float2 cp = wb[min(k + 1, NC) - xlo - (k == NC ? 1 : 0)];
+                if (k == 0) cm.y = -cm.y;   // X[-1] = conj X[1]
+                if (k == NC) cp.y = -cp.y;  // X[2049] = conj X[2047]
+                const float re = 0.5f * c0.x - 0.25f * (cm.x + cp.x);
+                const float im = 0.5f * c0.y - 0.25f * (cm.y + cp.y);
+                const float mag = sqrtf(re * re + im * im);
+                pw[t] = (power == 2.f) ? mag * mag : (power == 1.f) ? mag : powf(mag, power);
+            }
+            wave_sync();
+            float* P = reinterpret_cast<float*>(wb);
+#pragma unroll
+            for (int t = 0; t < PT; ++t)
+                if (lane + 64 * t < nb) P[lane + 64 * t] = pw[t];
+            wave_sync();
+            // ---- 8. mel rows ----
+            for (int m = lane; m < n_mels; m += 64) {
+                const int4 rw = srows[m];
+                const float* wv = svals + rw.z;
+                const float* pv = P + (rw.x - kmin);
+                float s = 0.f;
+                for (int i0 = 0; i0 < rw.y; i0 += 16) {
+                    float a[16], b[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int ii = min(i0 + i, rw.y - 1);
+                        a[i] = (i0 + i < rw.y) ? wv[ii] : 0.f;
+                        b[i] = pv[ii];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) s = fmaf(a[i], b[i], s);
+                }
+                melT[m * kFpg + wave] = s;
+                bmax = fmaxf(bmax, s);
+            }
+        }
+        __syncthreads();
+        for (int idx = tid; idx < n_mels * nf; idx += 256) {
+            const int m = idx / nf, f = idx - (idx / nf) * nf;
+            melS[((size_t)w * n_mels + m) * T + f0 + f] = melT[m * kFpg + f];
+        }
+        __shared__ float red[kFpg];
+        bmax = wave_max(bmax);
+        if (lane == 0) red[wave] = bmax;
+        __syncthreads();
+        if (tid == 0) {
+            for (int k = 1; k < kFpg; ++k) bmax = fmaxf(bmax, red[k]);
+            blkmax[w * ngrp + g] = bmax;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // fe_db: power_to_db(ref=max), clamp at -top_db, mean_sub, channel repeat.
 // One wave per mel band row.
 // ---------------------------------------------------------------------------
@@ -483,6 +764,39 @@ static int launch_stft(const FePlan& p, const float* pcm, const aa_window* wins,
     return AA_OK;
 }
 
+// the wave-per-frame kernel covers n_fft 4096 whenever the kept band fits the
+// per-wave buffer (15 bins per lane)
+static bool fe_fast4096(const FePlan& p) {
+    return p.cfg.n_fft == 4096 && p.kmax - p.kmin + 1 <= (kHalf / 64 - 1) * 64 &&
+           p.kmax - p.kmin + 3 <= kHalf && p.kmax + 1 < 1024;
+}
+
+static size_t fe_lds_bytes4096(const FePlan& p) {
+    const int seg_cap = ((kFpg - 1) * p.cfg.hop + 4096 + 3) & ~3;
+    return sizeof(float) * ((size_t)seg_cap + 2 * (size_t)kFpg * kHalf + 2 * 1026 +
+                            (size_t)((p.cfg.n_mels * kFpg + 3) & ~3) + 4 * (size_t)p.cfg.n_mels +
+                            (size_t)std::max(p.nnz, 1));
+}
+
+static int launch_stft4096(const FePlan& p, const float* pcm, const aa_window* wins, int n_win,
+                           const float4* stats, float* melS, float* blkmax, hipStream_t st) {
+    const size_t lds = fe_lds_bytes4096(p);
+    AA_CHECK(lds <= 150 * 1024, AA_ERR_UNSUPPORTED, "fe4096: hop %d needs %zu B of LDS", p.cfg.hop, lds);
+    static size_t attr_set = 0;
+    if (lds > attr_set) {
+        AA_HIP(hipFuncSetAttribute((const void*)fe_stft_mel_4096, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds));
+        attr_set = lds;
+    }
+    const int ngrp = p.nfblk;
+    const int n_items = ngrp * n_win;
+    hipLaunchKernelGGL(fe_stft_mel_4096, dim3(n_items), dim3(256), lds, st, pcm, wins, stats, p.d_tw, p.d_tw2,
+                       p.d_rows, p.d_vals, p.nnz, p.cfg.win_len, p.cfg.hop, p.T, p.cfg.n_mels, p.kmin,
+                       p.kmax, p.cfg.normalize, p.cfg.power, ngrp, n_items, melS, blkmax);
+    AA_LAUNCH_CHECK();
+    return AA_OK;
+}
+
 struct FeWs {
     float4* stats;
     float* melS;
@@ -517,7 +831,7 @@ extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** 
     FePlan* p = new FePlan();
     p->cfg = *cfg;
     p->T = 1 + cfg->win_len / cfg->hop;
-    p->nfblk = (p->T + kFpb - 1) / kFpb;
+
     const int nbins = n / 2 + 1;
     // CSR of the dense filterbank (rows are contiguous triangles; keep
     // [first nonzero, last nonzero] per row)
@@ -539,6 +853,8 @@ extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** 
     p->kmin = kmin;
     p->kmax = kmax;
     p->nnz = (int)vals.size();
+    // per-window partial maxima: one per frame block of whichever kernel runs
+    p->nfblk = fe_fast4096(*p) ? (p->T + kFpg - 1) / kFpg : (p->T + kFpb - 1) / kFpb;
     if (vals.empty()) vals.push_back(0.f);
     const int nc = n / 2;
     std::vector<float> win(n);
@@ -611,7 +927,10 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
                        p->cfg.win_len, ws.stats);
     AA_LAUNCH_CHECK();
     int rc;
-    switch (p->cfg.n_fft) {
+    if (fe_fast4096(*p)) {
+        rc = launch_stft4096(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st);
+        if (rc != AA_OK) return rc;
+    } else switch (p->cfg.n_fft) {
         case 2048: rc = launch_stft<2048>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
         case 4096: rc = launch_stft<4096>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
         default: rc = launch_stft<8192>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
