@@ -12,7 +12,7 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG.parent / "csrc"
 INCLUDE = PKG.parent.parent / "include"
 LIB = PKG / "libaa.so"
-SOURCES = ["aa_api.cpp", "aa_frontend.hip", "aa_cnn.hip"]
+SOURCES = ["aa_api.cpp", "aa_frontend.hip", "aa_cnn.hip", "aa_scan.hip"]
 ARCH = os.environ.get("AA_OFFLOAD_ARCH", "gfx950")
 
 

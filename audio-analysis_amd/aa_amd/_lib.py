@@ -84,6 +84,8 @@ _SIGS = {
                                       C.POINTER(C.c_int64)]),
     "aa_track_mean": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_void_p,
                                 C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    "aa_span_nonzero": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p,
+                                  C.c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)

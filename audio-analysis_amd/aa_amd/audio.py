@@ -1,0 +1,63 @@
+"""Recording decode (host side, outside the hot path).
+
+The reference decodes with ffmpeg through audioread + librosa.load(sr=None)
+(src/identify_tracks.py:49-62): samples as float32 in [-1, 1) (int16 / 32768)
+mixed to mono by averaging channels.  This build reads RIFF/WAVE directly
+(PCM 8/16/24/32-bit and IEEE float32/64); other containers need an external
+decoder and are rejected.  Resampling to 48 kHz (librosa soxr_hq in the
+reference) uses a polyphase FIR -- parity unpinned: soxr is not available.
+"""
+from __future__ import annotations
+
+import struct
+from math import gcd
+
+import numpy as np
+
+
+def decode(path):
+    with open(path, "rb") as f:
+        data = f.read()
+    if len(data) < 12 or data[:4] not in (b"RIFF", b"RF64") or data[8:12] != b"WAVE":
+        raise ValueError(f"{path}: not a RIFF/WAVE file")
+    pos, fmt, payload = 12, None, None
+    while pos + 8 <= len(data):
+        cid, size = data[pos:pos + 4], struct.unpack("<I", data[pos + 4:pos + 8])[0]
+        body = data[pos + 8:pos + 8 + size]
+        if cid == b"fmt ":
+            fmt = struct.unpack("<HHIIHH", body[:16])
+            if fmt[0] == 0xFFFE and len(body) >= 26:  # WAVE_FORMAT_EXTENSIBLE: real tag in the GUID
+                fmt = (struct.unpack("<H", body[24:26])[0],) + fmt[1:]
+        elif cid == b"data":
+            payload = body
+        pos += 8 + size + (size & 1)
+    if fmt is None or payload is None:
+        raise ValueError(f"{path}: missing fmt/data chunk")
+    tag, channels, sr, _, _, bits = fmt
+    if tag == 1:  # PCM
+        if bits == 8:
+            x = (np.frombuffer(payload, np.uint8).astype(np.float32) - 128.0) / 128.0
+        elif bits == 16:
+            x = np.frombuffer(payload[:len(payload) // 2 * 2], "<i2").astype(np.float32) / 32768.0
+        elif bits == 24:
+            b = np.frombuffer(payload[:len(payload) // 3 * 3], np.uint8).reshape(-1, 3).astype(np.int32)
+            v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+            v = np.where(v >= 1 << 23, v - (1 << 24), v)
+            x = v.astype(np.float32) / float(1 << 23)
+        elif bits == 32:
+            x = np.frombuffer(payload[:len(payload) // 4 * 4], "<i4").astype(np.float32) / float(1 << 31)
+        else:
+            raise ValueError(f"{path}: {bits}-bit PCM unsupported")
+    elif tag == 3:  # IEEE float
+        x = np.frombuffer(payload, "<f4" if bits == 32 else "<f8").astype(np.float32)
+    else:
+        raise ValueError(f"{path}: WAVE format tag {tag} unsupported")
+    if channels > 1:
+        x = x[: len(x) // channels * channels].reshape(-1, channels).mean(axis=1, dtype=np.float32)
+    return np.ascontiguousarray(x, dtype=np.float32), int(sr)
+
+
+def resample_poly(x, sr_in, sr_out):
+    from scipy.signal import resample_poly as rp
+    g = gcd(int(sr_in), int(sr_out))
+    return rp(x, sr_out // g, sr_in // g).astype(np.float32)

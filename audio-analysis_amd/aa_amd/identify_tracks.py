@@ -1,0 +1,275 @@
+"""``classify()`` and its result types on the MI355X path.
+
+Surface kept from the reference (src/identify_tracks.py):
+  classify(file, models, analyse_tracks, meta_data=None)
+      -> (tracks, length, signals, raw_length, bird_labels)        :416-573
+  Signal (:915-1033), ModelResult (:869-912), Prediction (:845-866),
+  get_master_tag (:580-647), load_recording (:49-62), get_end (:387-413),
+  segment_overlap / mel_freq (:709-718), NON_BIRD / DEFAULT_* constants.
+
+What runs where: decode on the host; the window schedule on the host
+(integers only, aa_amd.windows); log-mel front end, CNN ensemble, per-track
+mean and the end-of-recording scan on the GPU through libaa.so.  The JSON-facing
+objects below are plain host bookkeeping, identical in content to the
+reference's.
+"""
+from __future__ import annotations
+
+import logging
+from pathlib import Path
+
+import numpy as np
+
+CALL_LENGTH = 1
+DEFAULT_SPECIES = ["kiwi", "whistler", "morepork"]
+NON_BIRD = ["human", "noise", "insect"]
+SPECIFIC_NOISE = ["insect"]
+DEFAULT_BIRDS = ["bird"] + DEFAULT_SPECIES
+SIGNAL_WIDTH = 0.25
+MAX_FRQUENCY = 48000 / 2
+
+
+def get_max_chirps(length):
+    return int(length / (SIGNAL_WIDTH + 0.01))
+
+
+def segment_overlap(first, second):
+    """Length of the intersection of two [start, end] spans (negative = gap)."""
+    return (first[1] - first[0]) + (second[1] - second[0]) - (
+        max(first[1], second[1]) - min(first[0], second[0]))
+
+
+def mel_freq(f):
+    return 2595.0 * np.log10(1.0 + f / 700.0)
+
+
+# ---------------------------------------------------------------------------
+# result types (JSON content identical to the reference's get_meta)
+# ---------------------------------------------------------------------------
+class Prediction:
+    def __init__(self, what, confidence, ebird_id, threshold_used=None, normalize_confidence=True):
+        self.what = what
+        # banker's rounding of the float32 score x 100, like round(100 * p)
+        self.confidence = round(100 * confidence) if normalize_confidence else confidence
+        self.ebird_id = ebird_id
+        self.filtered = False
+        self.threshold_used = threshold_used
+
+    def get_meta(self):
+        return {
+            "label": self.what,
+            "confidence": self.confidence,
+            "filtered": self.filtered,
+            "ebird_id": self.ebird_id,
+            "threshold_used": self.threshold_used,
+        }
+
+
+class ModelResult:
+    def __init__(self, model, pre_model):
+        self.model = model
+        self.pre_model = pre_model
+        self.raw_prediction = None
+        self.predictions = []
+
+    def add_prediction(self, what, confidence, ebird_ids, threshold_used, normalize_confidence=True):
+        eid = None if (ebird_ids is not None and len(ebird_ids) == 0) else ebird_ids
+        self.predictions.append(Prediction(what, confidence, eid, threshold_used, normalize_confidence))
+
+    def get_meta(self):
+        meta = {"model": self.model, "pre_model": self.pre_model,
+                "predictions": [p.get_meta() for p in self.predictions]}
+        if self.raw_prediction is not None:
+            meta["raw_prediction"] = self.raw_prediction.get_meta()
+        return meta
+
+
+class Signal:
+    def __init__(self, start, end, freq_start, freq_end):
+        self.start = start
+        self.end = end
+        self.freq_start = freq_start
+        self.freq_end = freq_end
+        self.mel_freq_start = mel_freq(freq_start)
+        self.mel_freq_end = mel_freq(freq_end)
+        self.results = []
+        self.master_tag = None
+        self.master_model = None
+        self.master_below_thresh = True
+        self.track_id = None
+
+    # geometry
+    @property
+    def length(self):
+        return self.end - self.start
+
+    @property
+    def freq_range(self):
+        return self.freq_end - self.freq_start
+
+    @property
+    def mel_freq_range(self):
+        return self.mel_freq_end - self.mel_freq_start
+
+    def time_overlap(self, other):
+        return segment_overlap((self.start, self.end), (other.start, other.end))
+
+    def mel_freq_overlap(self, other):
+        return segment_overlap((self.mel_freq_start, self.mel_freq_end),
+                               (other.mel_freq_start, other.mel_freq_end))
+
+    def freq_overlap(self, other):
+        return segment_overlap((self.freq_start, self.freq_end), (other.freq_start, other.freq_end))
+
+    def copy(self):
+        return Signal(self.start, self.end, self.freq_start, self.freq_end)
+
+    def _refresh_mel(self):
+        self.mel_freq_start = mel_freq(self.freq_start)
+        self.mel_freq_end = mel_freq(self.freq_end)
+
+    def enlarge(self, scale, min_track_length):
+        grown = max(self.length * scale, min_track_length)
+        pad = (grown - self.length) / 2
+        self.start = max(self.start - pad, 0)
+        self.end = self.end + pad
+        fpad = ((self.freq_end - self.freq_start) * scale - (self.freq_end - self.freq_start)) / 2
+        lo = self.freq_start - fpad
+        self.freq_end = int(self.freq_end + fpad)
+        self.freq_start = int(max(lo, 0))
+        self._refresh_mel()
+
+    def merge(self, other):
+        self.start = min(self.start, other.start)
+        self.end = max(self.end, other.end)
+        self.freq_start = min(self.freq_start, other.freq_start)
+        self.freq_end = max(self.freq_end, other.freq_end)
+        self._refresh_mel()
+
+    def to_array(self, decimals=1):
+        a = [self.start, self.end, self.freq_start, self.freq_end]
+        return a if decimals is None else list(np.round(np.array(a), decimals))
+
+    def set_master_tag(self):
+        tag = get_master_tag(self)
+        if tag is None:
+            return
+        self.master_tag, self.master_model, self.master_below_thresh = tag
+
+    def get_meta(self):
+        meta = {"begin_s": self.start, "end_s": self.end, "freq_start": self.freq_start,
+                "freq_end": self.freq_end}
+        if self.master_tag is not None:
+            meta["master_tag"] = {"below_thresh": self.master_below_thresh,
+                                  "prediction": self.master_tag.get_meta(),
+                                  "model": self.master_model}
+        meta["model_results"] = [r.get_meta() for r in self.results]
+        if self.track_id is not None:
+            meta["track_id"] = self.track_id
+        return meta
+
+    def __str__(self):
+        return f"Signal: {self.start}-{self.end} f: {self.freq_start}-{self.freq_end}"
+
+
+def get_master_tag(track):
+    """Pick the track's master tag (src/identify_tracks.py:580-647): the most
+    confident specific (non-"bird") unfiltered prediction of the main models,
+    unless the pre-model says noise/human over a morepork; else the pre-model's
+    first prediction; else the best raw (below-threshold) prediction."""
+    pre = None
+    sure, raws = [], []
+    for r in track.results:
+        if r.pre_model:
+            pre = r
+            continue
+        sure.extend((p, r.model) for p in r.predictions if not p.filtered)
+        if r.raw_prediction is not None:
+            raws.append((r.raw_prediction, r.model))
+    best = None
+    if sure:
+        ranked = sorted(sure, key=lambda pm: pm[0].confidence, reverse=True)
+        best = next((pm for pm in ranked if pm[0].what != "bird"), ranked[0])
+    pre_pick = None
+    if pre is not None and pre.predictions and not pre.predictions[0].filtered:
+        pre_pick = (pre.predictions[0], pre.model)
+    if best is None and pre_pick is not None:
+        return (*pre_pick, False)
+    if best is not None:
+        if pre_pick is not None and best[0].what == "morepork" and pre_pick[0].what in ("human", "noise"):
+            return (*pre_pick, False)
+        return (*best, False)
+    if raws:
+        return (*sorted(raws, key=lambda pm: pm[0].confidence, reverse=True)[0], True)
+    if pre is not None and pre.raw_prediction is not None:
+        return pre.raw_prediction, pre.model, True
+    return None
+
+
+# ---------------------------------------------------------------------------
+# decode (host) and the end-of-recording scan (GPU)
+# ---------------------------------------------------------------------------
+def load_recording(file, resample=48000):
+    from .audio import decode
+    try:
+        frames, sr = decode(file)
+        if resample is not None and resample != sr:
+            from .audio import resample_poly
+            frames = resample_poly(frames, sr, resample)
+            sr = resample
+        return frames, sr
+    except Exception:
+        logging.error("Could not load %s", file, exc_info=True)
+        raise Exception(f"Could not load {file}")
+
+
+def get_end(frames, sr, device=None):
+    """Reference get_end (:387-413): the start (whole seconds) of the first
+    170-frame chunk of the 4800/281 STFT whose 120-band mel block is constant,
+    else the recording length.  A block is constant exactly when every frame
+    in it sees only zero samples (any nonzero sample gives a nonzero windowed
+    spectrum), so the GPU scans sample spans for nonzero values instead of
+    computing the STFT."""
+    from . import gpu_ops
+    return gpu_ops.get_end(frames, sr, device=device)
+
+
+# ---------------------------------------------------------------------------
+# classify
+# ---------------------------------------------------------------------------
+def _group_models(models):
+    from .model import load_model_meta
+    pre, main = [], []
+    for m in models:
+        meta = load_model_meta(Path(m))
+        (pre if meta.get("pre_model", False) else main).append((m, meta))
+    groups = [main]
+    if pre:
+        groups.append(pre)
+    return groups
+
+
+def classify(file, models, analyse_tracks, meta_data=None, precision=None, device=None):
+    from .pipeline import Classifier
+    frames, sr = load_recording(file)
+    raw_length = len(frames) / sr
+    length = get_end(frames, sr, device=device)
+    if not analyse_tracks:
+        raise NotImplementedError(
+            "signal detection + track building (src/identify_tracks.py:650-842) is not on the "
+            "MI355X path yet; run with --analyse-tracks and metadata tracks")
+    signals = []  # only consumed by the analyse_tracks=False JSON branch (src/analyse.py:157)
+    if meta_data is None:
+        return None
+    tracks = []
+    for t in meta_data["Tracks"]:
+        s = Signal(t["start"], t["end"], t.get("minFreq", 0), t.get("maxFreq", MAX_FRQUENCY))
+        s.track_id = t["id"]
+        tracks.append(s)
+    if len(tracks) == 0:
+        return [], length, [], raw_length, []
+    clf = Classifier.shared(precision=precision, device=device)
+    bird_labels = clf.classify_tracks(frames, sr, tracks, _group_models(models))
+    if bird_labels is None:
+        return [], length, [], raw_length, []
+    return tracks, length, signals, raw_length, list(bird_labels)

@@ -1,0 +1,158 @@
+"""Device orchestration of one recording's classification.
+
+Mirrors the model-group loop of the reference classify()
+(src/identify_tracks.py:444-571): models split into the mean ensemble and
+the pre-model group; the FIRST model of the first group configures the front
+end and the windows are computed once and reused by later groups (:501-529);
+per group: every model predicts every window, np.mean over models then over
+each track's windows, threshold -> Prediction / raw_prediction.
+
+MI355X shape of the same work: the recording is uploaded once; all windows of
+all tracks form one batch (window views are integers, no sample copies); one
+aa_fe_run for the batch, one aa_model_forward per model, one aa_track_mean
+per group, then a single device->host copy of [n_tracks, n_labels] scores.
+Models and front-end plans are cached across recordings.
+"""
+from __future__ import annotations
+
+import logging
+import os
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from .frontend import FeSettings, FrontEnd, pack_windows
+from .model import Model, track_mean
+from .windows import schedule
+
+
+def fe_settings_from_meta(meta: dict, sr: int) -> FeSettings:
+    """Front-end keys with the reference's defaults (:466-497)."""
+    n_fft = meta.get("n_fft", 4096)
+    return FeSettings(
+        sr=sr,
+        segment_length=meta.get("segment_length", 3),
+        n_fft=4096 if n_fft is None else n_fft,
+        hop_length=meta.get("hop_length", 640),
+        n_mels=meta.get("n_mels", 160),
+        fmin=meta.get("fmin", 50),
+        fmax=meta.get("fmax", 11000),
+        break_freq=meta.get("break_freq", 1750),
+        htk=meta.get("htk", False),
+        power=meta.get("power", 2),
+        db_scale=meta.get("db_scale", True),
+        normalize=meta.get("normalize", True),
+        mean_sub=meta.get("mean_sub", False),
+        channels=meta.get("channels", 1),
+    )
+
+
+class Classifier:
+    _shared = {}
+
+    @classmethod
+    def shared(cls, precision=None, device=None):
+        precision = precision or os.environ.get("AA_PRECISION", "f32")
+        key = (precision, str(device or "cuda"))
+        if key not in cls._shared:
+            cls._shared[key] = cls(precision, device)
+        return cls._shared[key]
+
+    def __init__(self, precision="f32", device=None):
+        self.precision = precision
+        self.device = torch.device(device or "cuda")
+        self._models = {}
+        self._fes = {}
+
+    def frontend(self, s: FeSettings) -> FrontEnd:
+        if s not in self._fes:
+            self._fes[s] = FrontEnd(s, self.device)
+        return self._fes[s]
+
+    def model(self, path, meta, in_shape) -> Model:
+        key = (str(Path(path).resolve()), tuple(in_shape))
+        if key not in self._models:
+            logging.info("Loading %s", str(path))
+            self._models[key] = Model(path, in_shape, precision=self.precision, device=self.device,
+                                      meta=meta)
+        return self._models[key]
+
+    def classify_tracks(self, frames, sr, tracks, groups):
+        from .identify_tracks import DEFAULT_BIRDS
+        dev = self.device
+        pcm = torch.from_numpy(np.ascontiguousarray(frames, dtype=np.float32)).to(dev)
+        views = None
+        logmel = None
+        bird_labels = set()
+        for group in groups:
+            if len(group) > 1:
+                logging.info("Meaning predictions as have multiple models")
+            meta = group[0][1]  # IndexError on an empty group, as the reference
+            s = fe_settings_from_meta(meta, sr)
+            if meta.get("filter_freq", False) or meta.get("filter_below", None):
+                raise NotImplementedError("band-pass filtered tracks (filter_freq / filter_below)")
+            labels = meta.get("labels")
+            ebird_ids = meta.get("ebird_ids")
+            model_name = meta.get("name", False)
+            pre_model = meta.get("pre_model", False)
+            prob_thresh = meta.get("threshold", 0.7)
+            bird_labels.update(meta.get("bird_labels", DEFAULT_BIRDS))
+            if model_name == "embeddings":
+                raise NotImplementedError("tensorflow_hub embedding models need a network fetch")
+            if views is None:
+                views = schedule(len(frames), sr, tracks, s.segment_length, meta.get("segment_stride", 1.5),
+                                 s.fmin, s.fmax, meta.get("pad_short_tracks", False))
+                flat = [v for tv in views for v in tv]
+                fe = self.frontend(s)
+                if flat:
+                    rows = torch.from_numpy(pack_windows(flat, len(frames), win_len=s.win_len)).to(dev)
+                    status = torch.empty(len(flat), dtype=torch.int32, device=dev)
+                    logmel = fe.run(pcm, rows, status=status)
+                    if int(status.max().item()) != 0:
+                        raise ValueError("Audio buffer is not finite everywhere")  # librosa valid_audio
+            else:
+                logging.info("Re using track data this will cuase problems if the STFT settings are "
+                             "not the same for multiple models")
+            if "efficientnet" in model_name.lower():
+                raise NotImplementedError("efficientnet (3-channel) models")
+            counts = [len(tv) for tv in views]
+            if sum(counts) == 0:
+                continue
+            begin = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32)
+            probs = torch.empty((len(group), sum(counts), len(labels)), dtype=torch.float32, device=dev)
+            for k, (path, m_meta) in enumerate(group):
+                m = self.model(path, m_meta, logmel.shape[1:])
+                if m.n_labels != len(labels):
+                    raise ValueError(f"{path}: {m.n_labels} outputs for {len(labels)} labels")
+                m.forward(logmel, probs=probs[k])
+            sel = [i for i, c in enumerate(counts) if c > 0]
+            wb = torch.from_numpy(begin[sel]).to(dev)
+            wc = torch.from_numpy(np.asarray(counts, np.int32)[sel]).to(dev)
+            means = track_mean(probs, wb, wc).cpu().numpy()
+            apply_group_scores(tracks, sel, means, meta)
+        return bird_labels
+
+
+def apply_group_scores(tracks, track_idx, means, meta):
+    """Per-track mean scores of one model group -> ModelResult (reference
+    src/identify_tracks.py:552-571): labels with p >= threshold become
+    Predictions (confidence = round(100 p)); with none, the arg-max becomes
+    the raw_prediction.  ``means`` rows are float32 like numpy's mean."""
+    from .identify_tracks import ModelResult, Prediction
+    labels = meta.get("labels")
+    ebird_ids = meta.get("ebird_ids")
+    thr = meta.get("threshold", 0.7)
+    for row, ti in enumerate(track_idx):
+        prediction = means[row]
+        result = ModelResult(meta.get("name", False), meta.get("pre_model", False))
+        tracks[ti].results.append(result)
+        best = None
+        for i, p in enumerate(prediction):
+            if best is None or p > best[1]:
+                best = (i, p)
+            if p >= thr:
+                result.add_prediction(labels[i], p, None if ebird_ids is None else ebird_ids[i], thr)
+        if not result.predictions:
+            result.raw_prediction = Prediction(labels[best[0]], best[1],
+                                               None if ebird_ids is None else ebird_ids[best[0]])

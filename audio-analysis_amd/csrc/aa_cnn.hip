@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace aa {
@@ -134,39 +135,163 @@ __global__ __launch_bounds__(256) void conv_small(const float* __restrict__ in, 
 // conv_mfma: implicit-GEMM conv, C_in % 32 == 0, fused pool/bias/act.
 // Block = 4 waves = WM (pixel) x WN (channel); wave = MF x NF 16x16 tiles.
 // ---------------------------------------------------------------------------
-template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL>
-__global__ __launch_bounds__(256) void conv_mfma(const T* __restrict__ in, int Hin, int Win,
+// LDS of one conv_mfma block: [staged patch][f32 log-mel patch if FUSED]
+// [2 x weight slice], and afterwards the epilogue tile reusing it from 0.
+template <typename T, int KH, int KW, int CIN, int TH, int TW, bool FUSED>
+__host__ __device__ constexpr size_t conv_b_offset() {
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int CSTR = CIN + (sizeof(T) == 2 ? 2 * VEC : VEC);
+    size_t off = ((size_t)(TH + KH - 1) * (TW + KW - 1) * CSTR * sizeof(T) + 15) & ~(size_t)15;
+    if (FUSED) off += ((sizeof(float) * (TH + KH + 1) * (TW + KW + 1)) + 15) & ~(size_t)15;
+    return off;
+}
+
+template <typename T, int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool EBF16>
+constexpr size_t conv_lds_bytes() {
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int CSTR = CIN + (sizeof(T) == 2 ? 2 * VEC : VEC);
+    const size_t main = conv_b_offset<T, KH, KW, CIN, TH, TW, FUSED>() + 2 * (size_t)BN * CSTR * sizeof(T);
+    const size_t epi = (size_t)TH * TW * (BN + (EBF16 ? 8 : 4)) * (EBF16 ? 2 : 4);
+    return main > epi ? main : epi;
+}
+
+// First layer fused into the next conv's patch staging (FUSED = true): the
+// log-mel patch is staged in LDS and the C_in = 1, 3x3 conv (f32 VALU, folded
+// BN, activation, optional MagTransform prologue) writes the activations the
+// MFMA loop consumes straight into the LDS patch -- the first layer's output
+// never reaches HBM.
+struct FirstConv {
+    const float* w;  // [32][9] folded
+    const float* b;  // [32]
+    int act;
+    float alpha;
+    int has_mag;
+    float mag_exp;
+    int H0, W0;      // log-mel image
+};
+
+// DIAG (diagnostic builds only, tools/conv_bench.hip): bit 0 skips the patch
+// staging, bit 1 the MFMA loop, bit 2 the epilogue stores, bit 3 makes every
+// lane read pixel 0 (no LDS bank conflicts), bit 4 re-reads chunk 0's weights
+// (L1-resident, no L2 stream), bit 5 skips the weight loads in the loop.
+template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW,
+          bool FUSED = false, int DIAG = 0, bool EBF16 = false, bool APF = true>
+__global__ __launch_bounds__(WM * WN * 64) void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                                                  const T* __restrict__ wt, const float* __restrict__ bias,
                                                  T* __restrict__ out, int Hout, int Wout, int cout_store,
-                                                 int TH, int TW, int tiles_w, int act, float alpha) {
-    static_assert(WM * WN == 4, "4 waves");
+                                                 int tiles_w, int act, float alpha, FirstConv fc) {
+    static_assert(TH % POOL == 0 && TW % POOL == 0, "pool-aligned tile");
+    static_assert(TH * TW <= WM * MF * 16, "tile covered by the waves' fragments");
+    constexpr int NTHR = WM * WN * 64;
     static_assert(CIN % 32 == 0, "C_in multiple of 32");
     constexpr int BN = WN * NF * 16;
     constexpr int VEC = 16 / sizeof(T);
-    constexpr int CSTR = CIN + VEC;  // +16 B per pixel
+    // pixel stride: bf16 rows padded by 32 B (stride = 2 mod 4 16-B units), which
+    // makes every ds_read_b128 lane group of the A-fragment reads conflict-free;
+    // f32 (parity mode) keeps a 16-B pad
+    constexpr int CSTR = CIN + (sizeof(T) == 2 ? 2 * VEC : VEC);
     constexpr int KTOT = KH * KW * CIN;
-    constexpr int ESTR = BN + 4;     // f32 epilogue row stride (conflict-free b32 writes)
+    // epilogue tile: f32, or bf16 with the bias already added (rounding is
+    // monotone, so max-pooling the rounded values equals rounding the max)
+    using ET = typename std::conditional<EBF16, bf16, float>::type;
+    constexpr int ESTR = BN + (EBF16 ? 8 : 4);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* patch = reinterpret_cast<T*>(smem);
 
     const int n = blockIdx.z;
     const int th = blockIdx.x / tiles_w, tw = blockIdx.x - (blockIdx.x / tiles_w) * tiles_w;
     const int oh0 = th * TH, ow0 = tw * TW;
-    const int PH = TH + KH - 1, PW = TW + KW - 1;
+    constexpr int PH = TH + KH - 1, PW = TW + KW - 1;
 
     // ---- stage the input patch ----
-    {
+    if constexpr (DIAG & 1) {
+    } else if constexpr (!FUSED) {
+        // batched, unconditional 16-B loads from clamped addresses (a
+        // load-or-zero branch would serialise them); out-of-image pixels only
+        // feed discarded outputs but are zeroed anyway
         constexpr int VPP = CIN / VEC;  // 16-B vectors per pixel
+        constexpr int U = 4;
         const int total = PH * PW * VPP;
         const T* src = in + (size_t)n * Hin * Win * CIN;
-        for (int idx = threadIdx.x; idx < total; idx += 256) {
-            const int pix = idx / VPP, cv = idx - pix * VPP;
+        for (int i0 = 0; i0 < total; i0 += U * NTHR) {
+            uint4 v[U];
+            bool ok[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int idx = i0 + u * NTHR + threadIdx.x;
+                const int pix = idx / VPP, cv = idx - pix * VPP;
+                const int r = pix / PW, c = pix - r * PW;
+                const int gh = oh0 + r, gw = ow0 + c;
+                ok[u] = idx < total && gh < Hin && gw < Win;
+                const int ch = min(gh, Hin - 1), cw = min(gw, Win - 1);
+                v[u] = *reinterpret_cast<const uint4*>(src + ((size_t)ch * Win + cw) * CIN + cv * VEC);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int idx = i0 + u * NTHR + threadIdx.x;
+                if (idx < total) {
+                    const int pix = idx / VPP, cv = idx - pix * VPP;
+                    *reinterpret_cast<uint4*>(patch + pix * CSTR + cv * VEC) = ok[u] ? v[u] : make_uint4(0, 0, 0, 0);
+                }
+            }
+        }
+    } else {
+        static_assert(CIN == 32, "fused first layer produces 32 channels");
+        // (a) log-mel patch (PH+2) x (PW+2), f32, after the activation patch
+        constexpr int XW = PW + 2, XN = (PH + 2) * XW;
+        const size_t pbytes = ((size_t)PH * PW * CSTR * sizeof(T) + 15) & ~(size_t)15;
+        float* X = reinterpret_cast<float*>(smem + pbytes);
+        const float* lm = reinterpret_cast<const float*>(in) + (size_t)n * fc.H0 * fc.W0;
+        for (int i0 = 0; i0 < XN; i0 += 4 * NTHR) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int idx = min(i0 + u * NTHR + (int)threadIdx.x, XN - 1);
+                const int r = idx / XW, c = idx - r * XW;
+                v[u] = lm[(size_t)min(oh0 + r, fc.H0 - 1) * fc.W0 + min(ow0 + c, fc.W0 - 1)];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int idx = i0 + u * NTHR + threadIdx.x;
+                if (idx < XN) X[idx] = fc.has_mag ? powf(v[u], fc.mag_exp) : v[u];
+            }
+        }
+        // (b) this thread's 8 output channels of the first conv, in registers
+        const int cg = threadIdx.x & 3;
+        float w1[8][9], b1[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            b1[c] = fc.b[cg * 8 + c];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) w1[c][t] = fc.w[(cg * 8 + c) * 9 + t];
+        }
+        __syncthreads();
+        // (c) first conv over the (PH x PW) activation patch -> LDS (type T)
+        for (int pix = threadIdx.x >> 2; pix < PH * PW; pix += NTHR / 4) {
             const int r = pix / PW, c = pix - r * PW;
-            const int gh = oh0 + r, gw = ow0 + c;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (gh < Hin && gw < Win)
-                v = *reinterpret_cast<const uint4*>(src + ((size_t)gh * Win + gw) * CIN + cv * VEC);
-            *reinterpret_cast<uint4*>(patch + pix * CSTR + cv * VEC) = v;
+            float x[9];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) x[i * 3 + j] = X[(r + i) * XW + c + j];
+            float o[8];
+#pragma unroll
+            for (int ch = 0; ch < 8; ++ch) {
+                float acc1 = 0.f;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc1 = fmaf(x[t], w1[ch][t], acc1);
+                o[ch] = apply_act(acc1 + b1[ch], fc.act, fc.alpha);
+            }
+            T* dst = patch + pix * CSTR + cg * 8;
+            if constexpr (sizeof(T) == 2) {
+                bf16x8 v;
+#pragma unroll
+                for (int ch = 0; ch < 8; ++ch) v[ch] = (bf16)o[ch];
+                *reinterpret_cast<bf16x8*>(dst) = v;
+            } else {
+                reinterpret_cast<float4*>(dst)[0] = make_float4(o[0], o[1], o[2], o[3]);
+                reinterpret_cast<float4*>(dst)[1] = make_float4(o[4], o[5], o[6], o[7]);
+            }
         }
     }
     __syncthreads();
@@ -174,81 +299,144 @@ __global__ __launch_bounds__(256) void conv_mfma(const T* __restrict__ in, int H
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = wave % WM, wn = wave / WM;
     const int q8 = 8 * (lane >> 4);
-    const int TP = TH * TW;
+    constexpr int TP = TH * TW;
     int abase[MF];
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
         int p = (wm * MF + i) * 16 + (lane & 15);
-        if (p >= TP) p = 0;  // padding rows: computed, never stored
+        if (p >= TP || (DIAG & 8)) p = 0;  // padding rows: computed, never stored
         const int r = p / TW, c = p - (p / TW) * TW;
         abase[i] = (r * PW + c) * CSTR + q8;
     }
-    const int nblk = blockIdx.y * BN + wn * NF * 16;
-    const T* bptr[NF];
-#pragma unroll
-    for (int j = 0; j < NF; ++j) bptr[j] = wt + (size_t)(nblk + j * 16 + (lane & 15)) * KTOT + q8;
-
     f32x4 acc[MF][NF];
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
         for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int kh = 0; kh < KH; ++kh) {
+    // ---- K loop, one tap (kh, kw) at a time.  The tap's weight slice
+    // [BN][C_in] (weights are packed tap-major, [tap][cout_pad][C_in], so a
+    // slice is one contiguous block) goes global -> registers while the
+    // previous tap computes, then into the other half of a double-buffered LDS
+    // stage shared by every wave; A fragments come from the staged patch. ----
+    constexpr int NTAP = KH * KW;
+    constexpr int CPC = CIN / 32;
+    constexpr int BV = BN * CIN / VEC;  // 16-B vectors per weight slice
+    constexpr int BPT = (BV + NTHR - 1) / NTHR;
+    T* Bs = reinterpret_cast<T*>(smem + conv_b_offset<T, KH, KW, CIN, TH, TW, FUSED>());
+    const size_t tap_stride = (size_t)gridDim.y * BN * CIN;
+    const T* wsl = wt + (size_t)blockIdx.y * BN * CIN;
+    uint4 breg[BPT];
+#define AA_BLOAD(t)                                                                   \
+    _Pragma("unroll") for (int u = 0; u < BPT; ++u) {                                  \
+        const int idx_ = min((int)threadIdx.x + u * NTHR, BV - 1);                     \
+        breg[u] = reinterpret_cast<const uint4*>(wsl + (size_t)(t) * tap_stride)[idx_]; \
+    }
+#define AA_BSTORE(dst)                                                                \
+    _Pragma("unroll") for (int u = 0; u < BPT; ++u) {                                  \
+        const int idx_ = threadIdx.x + u * NTHR;                                       \
+        if (BV % NTHR == 0 || idx_ < BV) {                                             \
+            const int row_ = idx_ / (CIN / VEC), cv_ = idx_ - row_ * (CIN / VEC);      \
+            *reinterpret_cast<uint4*>((dst) + row_ * CSTR + cv_ * VEC) = breg[u];      \
+        }                                                                              \
+    }
+    AA_BLOAD(0)
+    AA_BSTORE(Bs)
+    __syncthreads();
+    const int brow = (wn * NF * 16 + (lane & 15)) * CSTR + q8;
+    for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); ++t) {
+        if (t + 1 < NTAP) { AA_BLOAD(t + 1) }
+        const T* Bt = Bs + (t & 1) * BN * CSTR;
+        const int kh = t / KW, kw = t - (t / KW) * KW;
+        const int atap = (kh * PW + kw) * CSTR;
 #pragma unroll
-        for (int kw = 0; kw < KW; ++kw) {
+        for (int cc = 0; cc < CPC; ++cc) {
+            Frag<T> b[NF];
 #pragma unroll
-            for (int cc = 0; cc < CIN / 32; ++cc) {
-                const int tap = (kh * PW + kw) * CSTR + cc * 32;
-                const int koff = (kh * KW + kw) * CIN + cc * 32;
-                Frag<T> b[NF];
+            for (int j = 0; j < NF; ++j) b[j].load(Bt + brow + j * 16 * CSTR + cc * 32);
 #pragma unroll
-                for (int j = 0; j < NF; ++j) b[j].load(bptr[j] + koff);
+            for (int i = 0; i < MF; ++i) {
+                Frag<T> a;
+                a.load(patch + abase[i] + atap + cc * 32);
 #pragma unroll
-                for (int i = 0; i < MF; ++i) {
-                    Frag<T> a;
-                    a.load(patch + abase[i] + tap);
-#pragma unroll
-                    for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(a, b[j], acc[i][j]);
-                }
+                for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(a, b[j], acc[i][j]);
             }
         }
+        if (t + 1 < NTAP) { AA_BSTORE(Bs + ((t + 1) & 1) * BN * CSTR) }
+        __syncthreads();
     }
+#undef AA_BLOAD
+#undef AA_BSTORE
     __syncthreads();  // patch no longer needed: reuse LDS for the f32 tile
 
-    float* E = reinterpret_cast<float*>(smem);
+    ET* E = reinterpret_cast<ET*>(smem);
 #pragma unroll
-    for (int i = 0; i < MF; ++i) {
-        const int prow = (wm * MF + i) * 16 + 4 * (lane >> 4);
+    for (int j = 0; j < NF; ++j) {
+        const int col = wn * NF * 16 + j * 16 + (lane & 15);
+        const float bj = EBF16 ? bias[blockIdx.y * BN + col] : 0.f;
 #pragma unroll
-        for (int j = 0; j < NF; ++j) {
-            const int col = wn * NF * 16 + j * 16 + (lane & 15);
+        for (int i = 0; i < MF; ++i) {
+            const int prow = (wm * MF + i) * 16 + 4 * (lane >> 4);
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                if (prow + r < TP) E[(prow + r) * ESTR + col] = acc[i][j][r];
+                if (prow + r < TP) E[(prow + r) * ESTR + col] = (ET)(acc[i][j][r] + bj);
         }
     }
     __syncthreads();
 
-    const int PHo = TH / POOL, PWo = TW / POOL;
+    // pooled outputs: each thread owns one 8-channel group (bias in registers)
+    // and writes 16-B (bf16) / 32-B (f32) vectors
+    constexpr int PHo = TH / POOL, PWo = TW / POOL;
+    constexpr int G = BN / 8;
+    static_assert(NTHR % G == 0, "fixed channel group per thread");
     const int oh0s = oh0 / POOL, ow0s = ow0 / POOL;
-    const int items = PHo * PWo * BN;
+    const int col = (threadIdx.x % G) * 8;
+    const int ch0 = blockIdx.y * BN + col;
+    float bv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bv[c] = EBF16 ? 0.f : bias[ch0 + c];  // bias is padded to cout_pad
     T* dst = out + (size_t)n * Hout * Wout * cout_store;
-    for (int idx = threadIdx.x; idx < items; idx += 256) {
-        const int col = idx % BN;
-        const int q = idx / BN;
+    for (int q = threadIdx.x / G; q < PHo * PWo; q += NTHR / G) {
         const int pr = q / PWo, pc = q - (q / PWo) * PWo;
         const int gh = oh0s + pr, gw = ow0s + pc;
-        const int ch = blockIdx.y * BN + col;
-        if (gh >= Hout || gw >= Wout || ch >= cout_store) continue;
-        float v = -INFINITY;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = -INFINITY;
 #pragma unroll
         for (int dy = 0; dy < POOL; ++dy)
 #pragma unroll
-            for (int dx = 0; dx < POOL; ++dx)
-                v = fmaxf(v, E[((pr * POOL + dy) * TW + pc * POOL + dx) * ESTR + col]);
-        v = apply_act(v + bias[ch], act, alpha);
-        dst[((size_t)gh * Wout + gw) * cout_store + ch] = to_t<T>(v);
+            for (int dx = 0; dx < POOL; ++dx) {
+                const ET* e = E + ((pr * POOL + dy) * TW + pc * POOL + dx) * ESTR + col;
+                if constexpr (EBF16) {
+                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(e);
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) v[c] = fmaxf(v[c], (float)a[c]);
+                } else {
+                    const float4 a = reinterpret_cast<const float4*>(e)[0], b = reinterpret_cast<const float4*>(e)[1];
+                    v[0] = fmaxf(v[0], a.x); v[1] = fmaxf(v[1], a.y); v[2] = fmaxf(v[2], a.z); v[3] = fmaxf(v[3], a.w);
+                    v[4] = fmaxf(v[4], b.x); v[5] = fmaxf(v[5], b.y); v[6] = fmaxf(v[6], b.z); v[7] = fmaxf(v[7], b.w);
+                }
+            }
+        if (gh >= Hout || gw >= Wout) continue;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = apply_act(v[c] + bv[c], act, alpha);
+        if constexpr ((DIAG & 4) != 0) {
+            if (v[0] != 12345.f) continue;  // keep the values live, store (almost) never
+        }
+        T* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
+        if (ch0 + 8 <= cout_store) {
+            if constexpr (sizeof(T) == 2) {
+                bf16x8 pk;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) pk[c] = (bf16)v[c];
+                *reinterpret_cast<bf16x8*>(o) = pk;
+            } else {
+                reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
+                reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        } else {
+            for (int c = 0; c < 8 && ch0 + c < cout_store; ++c) o[c] = to_t<T>(v[c]);
+        }
     }
 }
 
@@ -377,11 +565,12 @@ struct Stage {
     float mag_exp = 1.f;
     int sigmoid = 0;
     int Hin = 0, Win = 0, Hc = 0, Wc = 0, Hout = 0, Wout = 0;
-    int TH = 0, TW = 0;  // conv tile (ST_MFMA)
     void* d_w = nullptr;
     float* d_b = nullptr;
     double flops = 0, bytes = 0;  // algorithmic per window
     std::string name;
+    int skipped = 0;    // first layer computed inside the next stage
+    int fused_first = 0;  // this stage computes the previous (first) layer itself
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
 };
 
@@ -395,51 +584,64 @@ struct Model {
     std::vector<hipEvent_t> ev_pool;  // recycled timing events
 };
 
-// Tile configuration of each conv_mfma instantiation.
-struct MfmaCfg {
-    int kh, kw, cin, pool;
-    int BN, TH, TW;
-};
-static const MfmaCfg kMfmaCfgs[] = {
-    {3, 3, 32, 3, 32, 6, 48},   // conv2 + pool   : WM2 WN2 MF9 NF1
-    {3, 3, 32, 1, 64, 6, 24},   // conv3          : WM1 WN4 MF9 NF1
-    {3, 3, 64, 1, 64, 6, 24},   // conv4          : WM1 WN4 MF9 NF1
-    {9, 3, 64, 3, 128, 3, 33},  // conv5 + pool   : WM1 WN4 MF7 NF2
-    {1, 3, 128, 1, 128, 6, 24}, // conv6          : WM1 WN4 MF9 NF2
-};
 
-static const MfmaCfg* find_cfg(int kh, int kw, int cin, int pool) {
-    for (const auto& c : kMfmaCfgs)
-        if (c.kh == kh && c.kw == kw && c.cin == cin && c.pool == pool) return &c;
-    return nullptr;
-}
-
-template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL>
-static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStream_t st) {
-    auto k = conv_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL>;
+template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW,
+          bool FUSED = false, bool EBF16 = false, bool APF = true>
+static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStream_t st,
+                       const Stage* first = nullptr) {
+    auto k = conv_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, EBF16, APF>;
     constexpr int BN = WN * NF * 16;
-    constexpr int VEC = 16 / sizeof(T);
-    const size_t patch = (size_t)(s.TH + KH - 1) * (s.TW + KW - 1) * (CIN + VEC) * sizeof(T);
-    const size_t epi = (size_t)s.TH * s.TW * (BN + 4) * sizeof(float);
-    const size_t lds = std::max(patch, epi);
+    const size_t lds = conv_lds_bytes<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>();
+    FirstConv fc{};
+    if (FUSED) {
+        fc = FirstConv{(const float*)first->d_w, first->d_b, first->act, first->alpha, first->has_mag,
+                       first->mag_exp, first->Hin, first->Win};
+    }
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
     static size_t attr = 0;
     if (lds > attr) {
         AA_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr = lds;
     }
-    const int tiles_h = (s.Hout * POOL + s.TH - 1) / s.TH;
-    const int tiles_w = (s.Wout * POOL + s.TW - 1) / s.TW;
+    const int tiles_h = (s.Hout * POOL + TH - 1) / TH;
+    const int tiles_w = (s.Wout * POOL + TW - 1) / TW;
     dim3 grid(tiles_h * tiles_w, s.cout_pad / BN, n);
-    hipLaunchKernelGGL(k, grid, dim3(256), lds, st, (const T*)in, s.Hin, s.Win, (const T*)s.d_w, s.d_b,
-                       (T*)out, s.Hout, s.Wout, s.cout, s.TH, s.TW, tiles_w, s.act, s.alpha);
+    hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, st, (const T*)in, s.Hin, s.Win, (const T*)s.d_w, s.d_b,
+                       (T*)out, s.Hout, s.Wout, s.cout, tiles_w, s.act, s.alpha, fc);
     AA_LAUNCH_CHECK();
     return AA_OK;
 }
 
+// Tile configuration of every conv_mfma instantiation, one line per
+// (dtype, kernel, C_in, pool): waves (WM x WN), 16x16 fragments per wave
+// (MF x NF), output tile TH x TW, bf16 epilogue tile.  BN = WN * NF * 16
+// output channels per block.  The f32 rows are the parity mode (smaller
+// tiles: the same LDS budget holds half the elements).
+#define AA_CONV_CFGS(X)                                     \
+    X(bf16, 3, 3, 32, 3, 4, 1, 9, 2, 12, 48, true)          \
+    X(bf16, 3, 3, 32, 1, 4, 1, 4, 4, 8, 32, true)           \
+    X(bf16, 3, 3, 64, 1, 4, 1, 4, 4, 8, 32, true)           \
+    X(bf16, 9, 3, 64, 3, 4, 2, 5, 4, 9, 33, true)           \
+    X(bf16, 1, 3, 128, 1, 1, 4, 9, 2, 6, 24, false)         \
+    X(float, 3, 3, 32, 3, 2, 2, 9, 1, 6, 48, false)         \
+    X(float, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false)         \
+    X(float, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false)         \
+    X(float, 9, 3, 64, 3, 1, 4, 7, 1, 3, 33, false)         \
+    X(float, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)
+
+// output channels per block of the instantiation serving this stage (0: none)
+static int mfma_bn(int prec, int kh, int kw, int cin, int pool) {
+#define AA_BN(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB)                                       \
+    if ((prec == AA_PREC_BF16) == (sizeof(T_) == 2) && kh == KH && kw == KW && cin == CIN && pool == POOL) \
+        return WN * NF * 16;
+    AA_CONV_CFGS(AA_BN)
+#undef AA_BN
+    return 0;
+}
+
 template <typename T>
 static int launch_stage(const Model& m, const Stage& s, const void* in, void* out, float* logits,
-                        float* probs, int n, hipStream_t st) {
+                        float* probs, int n, hipStream_t st, const Stage* first) {
     if (s.kind == ST_SMALL) {
         AA_CHECK(s.kh == 3 && s.kw == 3 && s.cout == 32 && s.cin == 1, AA_ERR_UNSUPPORTED,
                  "first conv %dx%d %d->%d unsupported", s.kh, s.kw, s.cin, s.cout);
@@ -459,16 +661,24 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
         AA_LAUNCH_CHECK();
         return AA_OK;
     }
-    if (s.kh == 3 && s.kw == 3 && s.cin == 32 && s.pool == 3)
-        return launch_mfma<T, 3, 3, 32, 2, 2, 9, 1, 3>(s, in, out, n, st);
-    if (s.kh == 3 && s.kw == 3 && s.cin == 32 && s.pool == 1)
-        return launch_mfma<T, 3, 3, 32, 1, 4, 9, 1, 1>(s, in, out, n, st);
-    if (s.kh == 3 && s.kw == 3 && s.cin == 64 && s.pool == 1)
-        return launch_mfma<T, 3, 3, 64, 1, 4, 9, 1, 1>(s, in, out, n, st);
-    if (s.kh == 9 && s.kw == 3 && s.cin == 64 && s.pool == 3)
-        return launch_mfma<T, 9, 3, 64, 1, 4, 7, 2, 3>(s, in, out, n, st);
-    if (s.kh == 1 && s.kw == 3 && s.cin == 128 && s.pool == 1)
-        return launch_mfma<T, 1, 3, 128, 1, 4, 9, 2, 1>(s, in, out, n, st);
+    if (s.fused_first) {
+        AA_CHECK(s.kh == 3 && s.kw == 3 && s.cin == 32 && s.pool == 3, AA_ERR_UNSUPPORTED,
+                 "no fused first-layer kernel for %s", s.name.c_str());
+    }
+#define AA_LAUNCH(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB)                                        \
+    if constexpr (std::is_same<T, T_>::value) {                                                          \
+        if (s.kh == KH && s.kw == KW && s.cin == CIN && s.pool == POOL) {                                \
+            if (s.fused_first) {                                                                         \
+                if constexpr (CIN == 32 && KH == 3 && KW == 3)                                           \
+                    return launch_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, true, EB>(s, in, out, \
+                                                                                              n, st, first); \
+            } else {                                                                                     \
+                return launch_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, false, EB>(s, in, out, n, st); \
+            }                                                                                            \
+        }                                                                                                \
+    }
+    AA_CONV_CFGS(AA_LAUNCH)
+#undef AA_LAUNCH
     set_error("conv %dx%d cin %d pool %d: no kernel instantiation", s.kh, s.kw, s.cin, s.pool);
     return AA_ERR_UNSUPPORTED;
 }
@@ -604,17 +814,27 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         }
         int bn_tile = 32;
         if (s.kind == ST_MFMA) {
-            const MfmaCfg* cfg = find_cfg(s.kh, s.kw, s.cin, s.pool);
-            if (!cfg) { fail(AA_ERR_UNSUPPORTED, "no conv kernel for this shape"); break; }
-            bn_tile = cfg->BN;
-            s.TH = cfg->TH;
-            s.TW = cfg->TW;
+            bn_tile = mfma_bn(precision, s.kh, s.kw, s.cin, s.pool);
+            if (!bn_tile) { fail(AA_ERR_UNSUPPORTED, "no conv kernel for this shape"); break; }
         }
         s.cout_pad = (s.kind == ST_SMALL) ? s.cout : (s.cout + bn_tile - 1) / bn_tile * bn_tile;
         // pack weights: HWIO -> [cout_pad][kh][kw][cin] with the BN scale folded in
+        // pack weights with the BN scale folded in: conv_small [cout][K];
+        // MFMA stages tap-major [kh*KW + kw][cout_pad][C_in] (a block's
+        // per-tap slice is contiguous); the 1x1 head is the same with one tap
         std::vector<float> wpk((size_t)s.cout_pad * K, 0.f);
+        const int ntap = s.kh * s.kw;
         for (int o = 0; o < s.cout; ++o)
-            for (int k = 0; k < K; ++k) wpk[(size_t)o * K + k] = (float)(kern[(size_t)k * s.cout + o] * scale[o]);
+            for (int k = 0; k < K; ++k) {
+                const double v = kern[(size_t)k * s.cout + o] * scale[o];
+                if (s.kind == ST_SMALL) {
+                    wpk[(size_t)o * K + k] = (float)v;
+                } else {
+                    const int t = k / s.cin, c = k - t * s.cin;
+                    wpk[((size_t)t * s.cout_pad + o) * s.cin + c] = (float)v;
+                }
+            }
+        (void)ntap;
         std::vector<float> bias(s.cout_pad, 0.f);
         for (int o = 0; o < s.cout; ++o) bias[o] = (float)shift[o];
         const bool bf = (precision == AA_PREC_BF16) && s.kind != ST_SMALL;
@@ -658,9 +878,20 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         free_model(m);
         return rc;
     }
+    // fuse a C_in = 1 first conv (3x3 -> 32) into the following 3x3/32 pooled conv
+    if (m->st.size() >= 2 && m->st[0].kind == ST_SMALL && m->st[0].kh == 3 && m->st[0].kw == 3 &&
+        m->st[0].cin == 1 && m->st[0].cout == 32 && m->st[1].kind == ST_MFMA && m->st[1].cin == 32 &&
+        m->st[1].kh == 3 && m->st[1].kw == 3 && m->st[1].pool == 3) {
+        m->st[0].skipped = 1;
+        m->st[1].fused_first = 1;
+        m->st[1].flops += m->st[0].flops;
+        m->st[1].bytes = 4.0 * m->st[0].Hin * m->st[0].Win + m->st[1].bytes - 0.0;
+        m->st[1].name = m->st[0].name + "+" + m->st[1].name;
+    }
     // ping-pong activation buffers: stage s writes buffer s % 2
     for (size_t k = 0; k + 1 < m->st.size(); ++k) {
         const Stage& s = m->st[k];
+        if (s.skipped) continue;
         const size_t e = (size_t)s.Hout * s.Wout * s.cout;
         m->act_elems[k % 2] = std::max(m->act_elems[k % 2], e);
     }
@@ -699,7 +930,9 @@ extern "C" int aa_model_forward(void* model, const float* x, int32_t n, float* l
     const void* in = x;
     for (size_t k = 0; k < m->st.size(); ++k) {
         Stage& s = m->st[k];
+        if (s.skipped) continue;  // computed inside stage k + 1 (reads x directly)
         void* out = buf[k % 2];
+        const Stage* first = s.fused_first ? &m->st[k - 1] : nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (m->timing) {
             for (hipEvent_t* e : {&e0, &e1}) {
@@ -712,8 +945,8 @@ extern "C" int aa_model_forward(void* model, const float* x, int32_t n, float* l
             }
             AA_HIP(hipEventRecord(e0, st));
         }
-        int rc = (m->prec == AA_PREC_BF16) ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st)
-                                           : launch_stage<float>(*m, s, in, out, logits, probs, n, st);
+        int rc = (m->prec == AA_PREC_BF16) ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st, first)
+                                           : launch_stage<float>(*m, s, in, out, logits, probs, n, st, first);
         if (rc != AA_OK) return rc;
         if (m->timing) {
             AA_HIP(hipEventRecord(e1, st));

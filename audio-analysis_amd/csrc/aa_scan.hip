@@ -1,0 +1,42 @@
+// Span scans over the PCM buffer.
+//
+// aa_span_nonzero backs get_end (reference src/identify_tracks.py:387-413):
+// a 170-frame chunk of the 4800/281 STFT has a constant 120-band mel block
+// exactly when every sample its frames see is zero, so the GPU reports, per
+// sample span, whether any sample in it is nonzero (HBM-bound byte scan).
+#include "aa_common.h"
+
+namespace aa {
+
+__global__ __launch_bounds__(256) void span_nonzero(const float* __restrict__ pcm,
+                                                    const long long* __restrict__ spans,
+                                                    int* __restrict__ flags) {
+    const long long b = spans[2 * blockIdx.x], e = spans[2 * blockIdx.x + 1];
+    int any = 0;
+    // 16-byte body with scalar head/tail
+    long long a4 = (b + 3) & ~3LL, e4 = e & ~3LL;
+    if (a4 > e4) a4 = e4 = e;
+    for (long long i = b + threadIdx.x; i < a4; i += 256) any |= pcm[i] != 0.f;
+    const float4* q = reinterpret_cast<const float4*>(pcm + a4);
+    const long long n4 = (e4 - a4) / 4;
+    for (long long i = threadIdx.x; i < n4; i += 256) {
+        const float4 v = q[i];
+        any |= (v.x != 0.f) | (v.y != 0.f) | (v.z != 0.f) | (v.w != 0.f);
+    }
+    for (long long i = e4 + threadIdx.x; i < e; i += 256) any |= pcm[i] != 0.f;
+    any = __syncthreads_or(any);
+    if (threadIdx.x == 0) flags[blockIdx.x] = any;
+}
+
+}  // namespace aa
+
+extern "C" int aa_span_nonzero(const float* pcm, int64_t n, const int64_t* spans, int32_t n_spans,
+                               int32_t* flags, void* stream) {
+    AA_CHECK(pcm && spans && flags, AA_ERR_INVALID, "aa_span_nonzero: null argument");
+    AA_CHECK(n_spans >= 0 && n >= 0, AA_ERR_INVALID, "aa_span_nonzero: bad sizes");
+    if (n_spans == 0) return AA_OK;
+    hipLaunchKernelGGL(aa::span_nonzero, dim3(n_spans), dim3(256), 0, static_cast<hipStream_t>(stream), pcm,
+                       reinterpret_cast<const long long*>(spans), flags);
+    AA_LAUNCH_CHECK();
+    return AA_OK;
+}

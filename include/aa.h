@@ -149,6 +149,14 @@ int aa_track_mean(const float* probs, int32_t n_models, int64_t model_stride, in
                   const int32_t* win_begin, const int32_t* win_count, int32_t n_tracks,
                   float* out, void* stream);
 
+/* ---------------------------------------------------------------- span scan */
+/* flags[i] = 1 if any of pcm[spans[2i] .. spans[2i+1]) is nonzero, else 0.
+ * Spans are caller-validated to lie in [0, n).  Backs get_end
+ * (src/identify_tracks.py:387-413): a 170-frame chunk of the 4800/281 STFT has
+ * a constant mel block exactly when every sample its frames cover is zero. */
+int aa_span_nonzero(const float* pcm, int64_t n, const int64_t* spans, int32_t n_spans,
+                    int32_t* flags, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

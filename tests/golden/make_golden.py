@@ -162,11 +162,104 @@ def gen_windows():
         json.dump(out, f, indent=1)
 
 
+POSTPROC_CASES = [
+    # name, location, species file present, tracks (id, start, end, minFreq, maxFreq), seed
+    ("nz_default", None, True,
+     [(1, 0.0, 12.0, None, None), (2, 3.2, 4.1, 800, 6000), (3, 20.0, 29.5, 12000, 15000),
+      (4, 30.0, 45.0, 100, 9000), (5, 50.0, 60.0, None, None)], 11),
+    ("auckland", {"lat": -36.85, "lng": 174.76}, True,
+     [(7, 0.0, 9.0, None, None), (8, 10.5, 11.0, 500, 3000), (9, 40.0, 55.0, 200, 4000)], 12),
+    ("no_species_file", {"lat": -43.5, "lng": 172.6}, False,
+     [(3, 1.0, 7.0, None, None), (4, 8.0, 16.0, None, None)], 13),
+]
+
+
+def _model_metas():
+    sys.path.insert(0, str(OUT.parents[1]))
+    from tools.make_models import DEFAULT_META, EBIRD, LABELS
+    def meta(name, labels, pre=False, thr=0.7):
+        m = dict(DEFAULT_META)
+        m.update(name=name, labels=labels, ebird_ids=[EBIRD.get(l, []) for l in labels],
+                 pre_model=pre, threshold=thr)
+        return m
+    pre_labels = ["bird", "human", "insect", "morepork", "noise"]
+    return {"model1": meta("model1", LABELS), "model2": meta("model2", LABELS),
+            "premodel": meta("premodel", pre_labels, pre=True, thr=0.6)}
+
+
+def _fake_probs(name, call, W, L, seed):
+    rng = np.random.default_rng([seed, call, sum(map(ord, name))])
+    p = rng.beta(0.6, 1.4, size=(W, L))
+    hot = rng.choice(L, size=min(3, L), replace=False)
+    p[:, hot] = rng.uniform(0.55, 1.0, size=(W, len(hot)))
+    return p.astype(np.float32)
+
+
+def gen_postproc():
+    import tempfile
+    import identify_tracks as it
+    import analyse
+    metas = _model_metas()
+    out_json, arrays = {}, {}
+    for name, location, species_file, tracks, seed in POSTPROC_CASES:
+        calls = {"n": 0}
+        class FakeModel:
+            def __init__(self, mname):
+                self.mname = mname
+            def predict(self, x):
+                probs = _fake_probs(self.mname, calls["n"], len(x), len(metas[self.mname]["labels"]), seed)
+                arrays[f"{name}__call{calls['n']}"] = probs
+                calls["n"] += 1
+                return probs
+        it.load_recording = lambda f, resample=48000: (np.ones(60 * 48000, np.float32) * 0.01, 48000)
+        it.get_end = lambda frames, sr: 60.0
+        it.signal_noise = lambda frames, sr, hop=281: []
+        it.load_model_meta = lambda p: metas[Path(p).parent.name]
+        it.load_model = lambda p, meta: FakeModel(Path(p).parent.name)
+        it.get_spect = lambda data, *a, **k: np.zeros((1,), np.float32)
+        analyse.classify = it.classify
+        with tempfile.TemporaryDirectory() as d:
+            rec = Path(d) / "rec.wav"
+            rec.write_bytes(b"")
+            meta = {"Tracks": []}
+            for tid, s0, s1, f0, f1 in tracks:
+                t = {"id": tid, "start": s0, "end": s1}
+                if f0 is not None:
+                    t["minFreq"], t["maxFreq"] = f0, f1
+                meta["Tracks"].append(t)
+            if location is not None:
+                meta["location"] = location
+            (Path(d) / "rec.txt").write_text(json.dumps(meta))
+            models = [f"/m/{m}/audioModel.keras" for m in ("model1", "model2", "premodel")]
+            cwd = os.getcwd()
+            os.chdir(str(REF.parent) if species_file else d)
+            try:
+                np.random.seed(seed)
+                res = analyse.species_identify(str(rec), models, True)
+            finally:
+                os.chdir(cwd)
+        out_json[name] = {"meta": meta, "models": ["model1", "model2", "premodel"], "seed": seed,
+                          "species_file": species_file, "n_calls": calls["n"],
+                          "result": json.loads(json.dumps(res, sort_keys=True))}
+    with open(OUT / "postproc.json", "w") as f:
+        json.dump({"metas": metas, "cases": out_json}, f, indent=1, sort_keys=True)
+    np.savez_compressed(OUT / "postproc_probs.npz", **arrays)
+    # species lists restricted to the codes the build's labels use (data only)
+    codes = {c for m in metas.values() for ids in m["ebird_ids"] for c in ids}
+    with open(REF / "ebird_species.json") as f:
+        sp = json.load(f)
+    subset = {k: {"region": {"info": v["region"]["info"]},
+                  "species": [c for c in v["species"] if c in codes]} for k, v in sp.items()}
+    with open(OUT / "ebird_subset.json", "w") as f:
+        json.dump(subset, f, indent=1, sort_keys=True)
+
+
 def main():
     install_shims()
     gen_mel()
     gen_normalize()
     gen_windows()
+    gen_postproc()
     print("wrote", sorted(p.name for p in OUT.glob("*.npz")) + sorted(p.name for p in OUT.glob("*.json")))
 
 

@@ -1,0 +1,81 @@
+// Diagnostic harness: time conv_mfma variants (phases ablated) on random
+// bf16 data.  Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include
+//   tools/conv_bench.hip -o /tmp/conv_bench ; run on the GPU box.
+#include "../audio-analysis_amd/csrc/aa_cnn.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace aa;
+
+template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int DIAG,
+          bool EBF16 = false, bool APF = true, bool FUSED = false>
+static float time_one(int n, int Hin, int Win, int cout, void* in, void* w, float* b, void* out, FirstConv fc,
+                      int iters) {
+    auto k = conv_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, DIAG, EBF16, APF>;
+    constexpr int BN = WN * NF * 16;
+    const size_t lds = conv_lds_bytes<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>();
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const int Hc = Hin - KH + 1, Wc = Win - KW + 1;
+    const int Hout = Hc / POOL, Wout = Wc / POOL;
+    const int tiles_h = (Hout * POOL + TH - 1) / TH, tiles_w = (Wout * POOL + TW - 1) / TW;
+    dim3 grid(tiles_h * tiles_w, cout / BN, n);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int i = 0; i < 3; ++i)
+        hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, 0, (const T*)in, Hin, Win, (const T*)w, b, (T*)out, Hout,
+                           Wout, cout, tiles_w, 1, 0.3f, fc);
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < iters; ++i)
+        hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, 0, (const T*)in, Hin, Win, (const T*)w, b, (T*)out,
+                           Hout, Wout, cout, tiles_w, 1, 0.3f, fc);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return 1e3f * ms / iters;
+}
+
+int main() {
+    const int n = 64;
+    std::vector<uint16_t> h(200u << 20);  // 400 MB: larger than every layer's input
+    for (auto& x : h) x = 0x3c00 + (rand() & 0x3ff);  // bf16 ~1..2 with random mantissa
+    void *in, *w, *out;
+    float* b;
+    (void)hipMalloc(&in, h.size() * 2);
+    (void)hipMalloc(&w, 8u << 20);
+    (void)hipMalloc(&out, 400u << 20);
+    (void)hipMalloc(&b, 4096);
+    (void)hipMemcpy(in, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+    (void)hipMemcpy(w, h.data(), 8u << 20, hipMemcpyHostToDevice);
+    (void)hipMemset(b, 0, 4096);
+    FirstConv fc{};
+    const int it = 20;
+    // layer dims of model1 at T = 226 (hop 640)
+    auto dims = [](int kh, int kw, int cin, int pool, int& H, int& W, int& C) {
+        if (kh == 3 && cin == 32 && pool == 3) { H = 158; W = 224; C = 32; }
+        else if (kh == 3 && cin == 32) { H = 52; W = 74; C = 64; }
+        else if (kh == 3 && cin == 64) { H = 50; W = 72; C = 64; }
+        else if (kh == 9) { H = 48; W = 70; C = 128; }
+        else { H = 13; W = 22; C = 256; }
+    };
+#define AA_BENCH(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB)                                         \
+    {                                                                                                     \
+        int H, W, C;                                                                                      \
+        dims(KH, KW, CIN, POOL, H, W, C);                                                                 \
+        const float full = time_one<T_, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, 0, EB>(n, H, W, C, in, w, b, \
+                                                                                          out, fc, it);   \
+        const float mf = time_one<T_, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, 5, EB>(n, H, W, C, in, w, b,   \
+                                                                                        out, fc, it);     \
+        const double fl = 2.0 * n * (H - KH + 1) * (W - KW + 1) * KH * KW * CIN * C;                      \
+        printf("%-6s %dx%d cin %3d pool %d  WM%d WN%d MF%d NF%d %2dx%2d  full %7.1f us (%6.1f TF)  only-mfma %7.1f us\n", \
+               sizeof(T_) == 2 ? "bf16" : "f32", KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, full,        \
+               fl / full * 1e-6, mf);                                                                     \
+    }
+    AA_CONV_CFGS(AA_BENCH)
+    hipError_t e = hipGetLastError();
+    printf("last error: %s\n", hipGetErrorString(e));
+    return 0;
+}
