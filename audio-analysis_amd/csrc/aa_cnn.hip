@@ -135,24 +135,67 @@ __global__ __launch_bounds__(256) void conv_small(const float* __restrict__ in, 
 // conv_mfma: implicit-GEMM conv, C_in % 32 == 0, fused pool/bias/act.
 // Block = 4 waves = WM (pixel) x WN (channel); wave = MF x NF 16x16 tiles.
 // ---------------------------------------------------------------------------
+// Padded row length (elements) of the staged patch and of the weight slices:
+// bf16 rows padded by 32 B (stride = 2 mod 4 16-B units, which makes every
+// ds_read_b128 lane group of the fragment reads conflict-free); f32 (parity
+// mode) keeps a 16-B pad.
+template <typename T>
+__host__ __device__ constexpr int conv_cstr(int cin) {
+    return cin + (sizeof(T) == 2 ? 16 : 4);
+}
+
 // LDS of one conv_mfma block: [staged patch][f32 log-mel patch if FUSED]
 // [2 x weight slice], and afterwards the epilogue tile reusing it from 0.
 template <typename T, int KH, int KW, int CIN, int TH, int TW, bool FUSED>
 __host__ __device__ constexpr size_t conv_b_offset() {
-    constexpr int VEC = 16 / sizeof(T);
-    constexpr int CSTR = CIN + (sizeof(T) == 2 ? 2 * VEC : VEC);
+    constexpr int CSTR = conv_cstr<T>(CIN);
     size_t off = ((size_t)(TH + KH - 1) * (TW + KW - 1) * CSTR * sizeof(T) + 15) & ~(size_t)15;
     if (FUSED) off += ((sizeof(float) * (TH + KH + 1) * (TW + KW + 1)) + 15) & ~(size_t)15;
     return off;
 }
 
+// One tap's weight slice [BN][CSTR] in LDS, rounded up to whole 1-KiB
+// wave-instructions of global_load_lds (the tail lanes land in the rounding).
+template <typename T, int CIN, int BN>
+__host__ __device__ constexpr int conv_slice_lds_bytes() {
+    return (BN * conv_cstr<T>(CIN) * (int)sizeof(T) + 1023) / 1024 * 1024;
+}
+
 template <typename T, int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool EBF16>
-constexpr size_t conv_lds_bytes() {
-    constexpr int VEC = 16 / sizeof(T);
-    constexpr int CSTR = CIN + (sizeof(T) == 2 ? 2 * VEC : VEC);
-    const size_t main = conv_b_offset<T, KH, KW, CIN, TH, TW, FUSED>() + 2 * (size_t)BN * CSTR * sizeof(T);
+constexpr size_t conv_lds_bytes_nb(int nb) {
+    const size_t main = conv_b_offset<T, KH, KW, CIN, TH, TW, FUSED>() + (size_t)nb * conv_slice_lds_bytes<T, CIN, BN>();
     const size_t epi = (size_t)TH * TW * (BN + (EBF16 ? 8 : 4)) * (EBF16 ? 2 : 4);
     return main > epi ? main : epi;
+}
+
+// Depth of the LDS ring of weight slices: as many buffers (up to 8, at most
+// one per tap) as fit without lowering the blocks per CU that a 2-deep ring
+// allows.  Slices in flight = ring - 1.
+template <typename T, int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool EBF16>
+constexpr int conv_ring() {
+    constexpr size_t cap = 160 * 1024;
+    const size_t base = conv_lds_bytes_nb<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>(2);
+    const size_t blocks = cap / base;
+    int nb = 2;
+    while (nb < 8 && nb < KH * KW &&
+           blocks * conv_lds_bytes_nb<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>(nb + 1) <= cap)
+        ++nb;
+    return nb;
+}
+
+template <typename T, int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool EBF16>
+constexpr size_t conv_lds_bytes() {
+    return conv_lds_bytes_nb<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>(
+        conv_ring<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>());
+}
+
+// s_waitcnt vmcnt(N) with N = PER * k for a runtime k in [0, 7] (the
+// immediate must be a literal), lgkmcnt(0) alongside.
+template <int PER>
+__device__ __forceinline__ void wait_vm_lgkm(int k) {
+#define AA_W(K) case K: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER * K) : "memory"); break;
+    switch (k) { AA_W(0) AA_W(1) AA_W(2) AA_W(3) AA_W(4) AA_W(5) AA_W(6) default: AA_W(7) }
+#undef AA_W
 }
 
 // First layer fused into the next conv's patch staging (FUSED = true): the
@@ -174,9 +217,22 @@ struct FirstConv {
 // staging, bit 1 the MFMA loop, bit 2 the epilogue stores, bit 3 makes every
 // lane read pixel 0 (no LDS bank conflicts), bit 4 re-reads chunk 0's weights
 // (L1-resident, no L2 stream), bit 5 skips the weight loads in the loop.
+// Waves per SIMD a conv_mfma block shape reaches (LDS-limited), told to the
+// compiler so it schedules for latency at that occupancy instead of trimming
+// registers for an occupancy the LDS footprint never allows.
+template <typename T, int KH, int KW, int CIN, int WM, int WN, int NF, int TH, int TW, bool FUSED, bool EBF16>
+constexpr int conv_waves_per_simd() {
+    constexpr size_t lds = conv_lds_bytes<T, KH, KW, CIN, WN * NF * 16, TH, TW, FUSED, EBF16>();
+    constexpr int blocks = (int)((160 * 1024) / lds);
+    constexpr int w = blocks * WM * WN / 4;
+    return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
 template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW,
           bool FUSED = false, int DIAG = 0, bool EBF16 = false, bool APF = true>
-__global__ __launch_bounds__(WM * WN * 64) void conv_mfma(const T* __restrict__ in, int Hin, int Win,
+__global__ __launch_bounds__(WM * WN * 64)
+__attribute__((amdgpu_waves_per_eu(conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>())))
+void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                                                  const T* __restrict__ wt, const float* __restrict__ bias,
                                                  T* __restrict__ out, int Hout, int Wout, int cout_store,
                                                  int tiles_w, int act, float alpha, FirstConv fc) {
@@ -186,10 +242,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma(const T* __restrict__ 
     static_assert(CIN % 32 == 0, "C_in multiple of 32");
     constexpr int BN = WN * NF * 16;
     constexpr int VEC = 16 / sizeof(T);
-    // pixel stride: bf16 rows padded by 32 B (stride = 2 mod 4 16-B units), which
-    // makes every ds_read_b128 lane group of the A-fragment reads conflict-free;
-    // f32 (parity mode) keeps a 16-B pad
-    constexpr int CSTR = CIN + (sizeof(T) == 2 ? 2 * VEC : VEC);
+    constexpr int CSTR = conv_cstr<T>(CIN);  // padded pixel / weight-row stride
     constexpr int KTOT = KH * KW * CIN;
     // epilogue tile: f32, or bf16 with the bias already added (rounding is
     // monotone, so max-pooling the rounded values equals rounding the max)
@@ -296,7 +349,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma(const T* __restrict__ 
     }
     __syncthreads();
 
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int wm = wave % WM, wn = wave / WM;
     const int q8 = 8 * (lane >> 4);
     constexpr int TP = TH * TW;
@@ -314,59 +367,85 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma(const T* __restrict__ 
 #pragma unroll
         for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // ---- K loop, one tap (kh, kw) at a time.  The tap's weight slice
-    // [BN][C_in] (weights are packed tap-major, [tap][cout_pad][C_in], so a
-    // slice is one contiguous block) goes global -> registers while the
-    // previous tap computes, then into the other half of a double-buffered LDS
-    // stage shared by every wave; A fragments come from the staged patch. ----
+    // ---- K loop, one tap (kh, kw) at a time.  Weights are packed tap-major
+    // with padded rows, [tap][cout_pad][CSTR], so a block's slice of one tap
+    // is one contiguous [BN][CSTR] block whose bytes are exactly its LDS
+    // image.  global_load_lds streams the slices through a ring of NB LDS
+    // buffers, NB - 1 taps ahead of the one computing (an L2 round trip of
+    // a slice outlasts one tap's MFMAs): at the top of tap t each wave waits
+    // for its own loads of slice t with a counted vmcnt (later slices stay in
+    // flight), one barrier publishes slice t to every wave and retires all
+    // reads of the buffer slice t + NB - 1 will overwrite, then that slice is
+    // issued.  A fragments come from the staged patch. ----
     constexpr int NTAP = KH * KW;
     constexpr int CPC = CIN / 32;
-    constexpr int BV = BN * CIN / VEC;  // 16-B vectors per weight slice
-    constexpr int BPT = (BV + NTHR - 1) / NTHR;
-    T* Bs = reinterpret_cast<T*>(smem + conv_b_offset<T, KH, KW, CIN, TH, TW, FUSED>());
-    const size_t tap_stride = (size_t)gridDim.y * BN * CIN;
-    const T* wsl = wt + (size_t)blockIdx.y * BN * CIN;
-    uint4 breg[BPT];
-#define AA_BLOAD(t)                                                                   \
-    _Pragma("unroll") for (int u = 0; u < BPT; ++u) {                                  \
-        const int idx_ = min((int)threadIdx.x + u * NTHR, BV - 1);                     \
-        breg[u] = reinterpret_cast<const uint4*>(wsl + (size_t)(t) * tap_stride)[idx_]; \
+    constexpr int NW = WM * WN;
+    constexpr int NB = conv_ring<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>();
+    constexpr int SLICE = BN * CSTR;                               // elements
+    constexpr int SLICE_LDS = conv_slice_lds_bytes<T, CIN, BN>();  // bytes
+    constexpr int GPS = SLICE_LDS / 1024;                          // wave-instructions per slice
+    constexpr int GHI = (GPS + NW - 1) / NW, GLO = GPS / NW;       // this wave's share: GHI if wave < GPS % NW
+    char* Bs = smem + conv_b_offset<T, KH, KW, CIN, TH, TW, FUSED>();
+    const size_t tap_stride = (size_t)gridDim.y * SLICE;
+    const T* wsl = wt + (size_t)blockIdx.y * SLICE + lane * VEC;
+#define AA_GLDS(t)                                                                                       \
+    _Pragma("unroll") for (int u_ = 0; u_ < GHI; ++u_) {                                               \
+        const int g_ = u_ * NW + wave;                                                                  \
+        if (GPS % NW == 0 || g_ < GPS)                                                                  \
+            __builtin_amdgcn_global_load_lds(                                                           \
+                (const __attribute__((address_space(1))) void*)(wsl + (size_t)(t) * tap_stride + g_ * (1024 / sizeof(T))), \
+                (__attribute__((address_space(3))) void*)(Bs + ((t) % NB) * SLICE_LDS + g_ * 1024), 16, 0, 0); \
     }
-#define AA_BSTORE(dst)                                                                \
-    _Pragma("unroll") for (int u = 0; u < BPT; ++u) {                                  \
-        const int idx_ = threadIdx.x + u * NTHR;                                       \
-        if (BV % NTHR == 0 || idx_ < BV) {                                             \
-            const int row_ = idx_ / (CIN / VEC), cv_ = idx_ - row_ * (CIN / VEC);      \
-            *reinterpret_cast<uint4*>((dst) + row_ * CSTR + cv_ * VEC) = breg[u];      \
-        }                                                                              \
+    if constexpr (!(DIAG & 32)) {
+#pragma unroll
+        for (int t = 0; t < NB - 1; ++t) AA_GLDS(t)
     }
-    AA_BLOAD(0)
-    AA_BSTORE(Bs)
-    __syncthreads();
     const int brow = (wn * NF * 16 + (lane & 15)) * CSTR + q8;
+    const bool hi_share = (GPS % NW == 0) || wave < GPS % NW;
     for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); ++t) {
-        if (t + 1 < NTAP) { AA_BLOAD(t + 1) }
-        const T* Bt = Bs + (t & 1) * BN * CSTR;
+        // slices t+1 .. min(t+NB-2, NTAP-1) may stay in flight
+        const int ahead = min(NB - 2, NTAP - 1 - t);
+        if (DIAG & 32) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else if (hi_share) {
+            wait_vm_lgkm<GHI>(ahead);
+        } else {
+            wait_vm_lgkm<GLO>(ahead);
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(DIAG & 32)) {
+            if (t + NB - 1 < NTAP) { AA_GLDS(t + NB - 1) }
+        }
+        const T* Bt = reinterpret_cast<const T*>(Bs + ((DIAG & 16) ? 0 : (t % NB)) * SLICE_LDS);
         const int kh = t / KW, kw = t - (t / KW) * KW;
         const int atap = (kh * PW + kw) * CSTR;
 #pragma unroll
         for (int cc = 0; cc < CPC; ++cc) {
-            Frag<T> b[NF];
+            Frag<T> b[NF], a[MF];
 #pragma unroll
             for (int j = 0; j < NF; ++j) b[j].load(Bt + brow + j * 16 * CSTR + cc * 32);
 #pragma unroll
-            for (int i = 0; i < MF; ++i) {
-                Frag<T> a;
-                a.load(patch + abase[i] + atap + cc * 32);
+            for (int i = 0; i < MF; ++i) a[i].load(patch + abase[i] + atap + cc * 32);
 #pragma unroll
-                for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(a, b[j], acc[i][j]);
+            for (int i = 0; i < MF; ++i)
+#pragma unroll
+                for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(a[i], b[j], acc[i][j]);
+            if constexpr (sizeof(T) == 2) {
+                // issue order: the B fragments and two A fragments, then one
+                // A fragment ahead of each row of NF MFMAs (left alone, the
+                // scheduler reuses one A register and waits lgkmcnt(0) before
+                // every row)
+                __builtin_amdgcn_sched_group_barrier(0x100, NF + (MF > 1 ? 2 : 1), 0);
+#pragma unroll
+                for (int i = 0; i < MF; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
+                    if (i + 2 < MF) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
             }
         }
-        if (t + 1 < NTAP) { AA_BSTORE(Bs + ((t + 1) & 1) * BN * CSTR) }
-        __syncthreads();
     }
-#undef AA_BLOAD
-#undef AA_BSTORE
+#undef AA_GLDS
     __syncthreads();  // patch no longer needed: reuse LDS for the f32 tile
 
     ET* E = reinterpret_cast<ET*>(smem);
@@ -818,12 +897,16 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             if (!bn_tile) { fail(AA_ERR_UNSUPPORTED, "no conv kernel for this shape"); break; }
         }
         s.cout_pad = (s.kind == ST_SMALL) ? s.cout : (s.cout + bn_tile - 1) / bn_tile * bn_tile;
-        // pack weights: HWIO -> [cout_pad][kh][kw][cin] with the BN scale folded in
         // pack weights with the BN scale folded in: conv_small [cout][K];
-        // MFMA stages tap-major [kh*KW + kw][cout_pad][C_in] (a block's
-        // per-tap slice is contiguous); the 1x1 head is the same with one tap
-        std::vector<float> wpk((size_t)s.cout_pad * K, 0.f);
+        // MFMA stages tap-major with padded rows [kh*KW + kw][cout_pad][cstr]
+        // (a block's per-tap slice is one contiguous block, byte-identical to
+        // its LDS image) plus 1 KiB of slack for the last slice's rounding;
+        // the 1x1 head [cout_pad][C_in]
+        const bool bf = (precision == AA_PREC_BF16) && s.kind != ST_SMALL;
+        const int cstr = s.kind == ST_MFMA ? (bf ? conv_cstr<bf16>(s.cin) : conv_cstr<float>(s.cin)) : s.cin;
         const int ntap = s.kh * s.kw;
+        const size_t slack = s.kind == ST_MFMA ? 1024 / (bf ? 2 : 4) : 0;
+        std::vector<float> wpk(s.kind == ST_SMALL ? (size_t)s.cout * K : (size_t)ntap * s.cout_pad * cstr + slack, 0.f);
         for (int o = 0; o < s.cout; ++o)
             for (int k = 0; k < K; ++k) {
                 const double v = kern[(size_t)k * s.cout + o] * scale[o];
@@ -831,13 +914,11 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                     wpk[(size_t)o * K + k] = (float)v;
                 } else {
                     const int t = k / s.cin, c = k - t * s.cin;
-                    wpk[((size_t)t * s.cout_pad + o) * s.cin + c] = (float)v;
+                    wpk[((size_t)t * s.cout_pad + o) * cstr + c] = (float)v;
                 }
             }
-        (void)ntap;
         std::vector<float> bias(s.cout_pad, 0.f);
         for (int o = 0; o < s.cout; ++o) bias[o] = (float)shift[o];
-        const bool bf = (precision == AA_PREC_BF16) && s.kind != ST_SMALL;
         const size_t wbytes = wpk.size() * (bf ? 2 : 4);
         hipError_t e = hipMalloc(&s.d_w, wbytes);
         if (e == hipSuccess) {

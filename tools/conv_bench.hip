@@ -75,6 +75,16 @@ int main() {
                fl / full * 1e-6, mf);                                                                     \
     }
     AA_CONV_CFGS(AA_BENCH)
+    // ablations of the 9x3 layer: staging / MFMA / stores / weight stream
+    {
+        int H, W, C;
+        dims(9, 3, 64, 3, H, W, C);
+#define AA_ABL(D)                                                                                          \
+    printf("abl 9x3 DIAG %2d: %7.1f us\n", D,                                                             \
+           time_one<bf16, 9, 3, 64, 4, 2, 5, 4, 3, 9, 33, D, true>(n, H, W, C, in, w, b, out, fc, it));
+        AA_ABL(0) AA_ABL(1) AA_ABL(4) AA_ABL(5) AA_ABL(5 | 32) AA_ABL(5 | 16) AA_ABL(5 | 8) AA_ABL(7) AA_ABL(7 | 32)
+#undef AA_ABL
+    }
     hipError_t e = hipGetLastError();
     printf("last error: %s\n", hipGetErrorString(e));
     return 0;
