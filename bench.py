@@ -160,9 +160,12 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        # the per-file result gather (§8e): every rank's per-track means to all
-        gathered = [torch.empty_like(tmean) for _ in range(world)]
-        dist.all_gather(gathered, tmean)
+        # the per-file result gather (§8e): every rank's per-track records to all
+        from aa_amd import shard
+        rec = torch.from_numpy(shard.pack_records([2 * rank, 2 * rank + 1], [0, 0], tmean.cpu().numpy(),
+                                                  width=model.n_labels)).to(dev)
+        gathered = shard.gather_records(rec)
+        assert gathered.shape[0] == 2 * world
     elapsed = float(t.item())
 
     stages = []
