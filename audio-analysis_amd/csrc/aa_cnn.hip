@@ -33,6 +33,7 @@ namespace aa {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __bf16 bf16;
 
 // ---- 8-element fragments and the MFMA step over one 32-deep K chunk -------
@@ -309,41 +310,67 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                 if (idx < XN) X[idx] = fc.has_mag ? powf(v[u], fc.mag_exp) : v[u];
             }
         }
-        // (b) this thread's 8 output channels of the first conv, in registers
-        const int cg = threadIdx.x & 3;
-        float w1[8][9], b1[8];
+        // (b) first conv: wave -> 8 output channels (wave-uniform, so its 72
+        // weights and 8 biases are scalar loads), lane -> one patch column; the
+        // lane slides the 3x3 window down its column (3 new LDS reads per
+        // output row) and computes channel pairs with packed FMAs.  Per
+        // channel the arithmetic is the same f32 fma chain (taps in order,
+        // then + bias) as conv_small.  Activation as max(v, a v): the planner
+        // fuses only when the activation has 0 <= a <= 1 (none: 1, relu: 0).
+        static_assert(NTHR == 256 && PW <= 64, "fused first layer: 4 waves, patch width <= 64");
+        const int cg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int col = threadIdx.x & 63;
+        f32x2 w1[9][4];
+        f32x2 b1[4];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            b1[c] = fc.b[cg * 8 + c];
+        for (int k = 0; k < 4; ++k) {
+            b1[k] = f32x2{fc.b[cg * 8 + 2 * k], fc.b[cg * 8 + 2 * k + 1]};
 #pragma unroll
-            for (int t = 0; t < 9; ++t) w1[c][t] = fc.w[(cg * 8 + c) * 9 + t];
+            for (int t = 0; t < 9; ++t)
+                w1[t][k] = f32x2{fc.w[(cg * 8 + 2 * k) * 9 + t], fc.w[(cg * 8 + 2 * k + 1) * 9 + t]};
         }
+        const float ae = fc.alpha;  // host: act folded to a slope in [0, 1]
         __syncthreads();
-        // (c) first conv over the (PH x PW) activation patch -> LDS (type T)
-        for (int pix = threadIdx.x >> 2; pix < PH * PW; pix += NTHR / 4) {
-            const int r = pix / PW, c = pix - r * PW;
-            float x[9];
+        if (col < PW) {
+            float xr[3][3];
 #pragma unroll
-            for (int i = 0; i < 3; ++i)
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 3; ++j) x[i * 3 + j] = X[(r + i) * XW + c + j];
-            float o[8];
+                for (int j = 0; j < 3; ++j) xr[i][j] = X[i * XW + col + j];
 #pragma unroll
-            for (int ch = 0; ch < 8; ++ch) {
-                float acc1 = 0.f;
+            for (int r = 0; r < PH; ++r) {
 #pragma unroll
-                for (int t = 0; t < 9; ++t) acc1 = fmaf(x[t], w1[ch][t], acc1);
-                o[ch] = apply_act(acc1 + b1[ch], fc.act, fc.alpha);
-            }
-            T* dst = patch + pix * CSTR + cg * 8;
-            if constexpr (sizeof(T) == 2) {
-                bf16x8 v;
+                for (int j = 0; j < 3; ++j) xr[(r + 2) % 3][j] = X[(r + 2) * XW + col + j];
+                f32x2 acc[4];
 #pragma unroll
-                for (int ch = 0; ch < 8; ++ch) v[ch] = (bf16)o[ch];
-                *reinterpret_cast<bf16x8*>(dst) = v;
-            } else {
-                reinterpret_cast<float4*>(dst)[0] = make_float4(o[0], o[1], o[2], o[3]);
-                reinterpret_cast<float4*>(dst)[1] = make_float4(o[4], o[5], o[6], o[7]);
+                for (int k = 0; k < 4; ++k) acc[k] = f32x2{0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        const float xv = xr[(r + i) % 3][j];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            acc[k] = __builtin_elementwise_fma(f32x2{xv, xv}, w1[i * 3 + j][k], acc[k]);
+                    }
+                float o[8];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const f32x2 v = acc[k] + b1[k];
+                    const f32x2 sv = v * ae;
+                    o[2 * k] = fmaxf(v.x, sv.x);
+                    o[2 * k + 1] = fmaxf(v.y, sv.y);
+                }
+                T* dst = patch + (r * PW + col) * CSTR + cg * 8;
+                if constexpr (sizeof(T) == 2) {
+                    bf16x8 v;
+#pragma unroll
+                    for (int ch = 0; ch < 8; ++ch) v[ch] = (bf16)o[ch];
+                    *reinterpret_cast<bf16x8*>(dst) = v;
+                } else {
+                    reinterpret_cast<float4*>(dst)[0] = make_float4(o[0], o[1], o[2], o[3]);
+                    reinterpret_cast<float4*>(dst)[1] = make_float4(o[4], o[5], o[6], o[7]);
+                }
             }
         }
     }
@@ -673,7 +700,8 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     const size_t lds = conv_lds_bytes<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>();
     FirstConv fc{};
     if (FUSED) {
-        fc = FirstConv{(const float*)first->d_w, first->d_b, first->act, first->alpha, first->has_mag,
+        const float slope = first->act == ACT_LEAKY ? first->alpha : first->act == ACT_RELU ? 0.f : 1.f;
+        fc = FirstConv{(const float*)first->d_w, first->d_b, first->act, slope, first->has_mag,
                        first->mag_exp, first->Hin, first->Win};
     }
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
@@ -962,7 +990,8 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
     // fuse a C_in = 1 first conv (3x3 -> 32) into the following 3x3/32 pooled conv
     if (m->st.size() >= 2 && m->st[0].kind == ST_SMALL && m->st[0].kh == 3 && m->st[0].kw == 3 &&
         m->st[0].cin == 1 && m->st[0].cout == 32 && m->st[1].kind == ST_MFMA && m->st[1].cin == 32 &&
-        m->st[1].kh == 3 && m->st[1].kw == 3 && m->st[1].pool == 3) {
+        m->st[1].kh == 3 && m->st[1].kw == 3 && m->st[1].pool == 3 &&
+        (m->st[0].act != ACT_LEAKY || (m->st[0].alpha >= 0.f && m->st[0].alpha <= 1.f))) {
         m->st[0].skipped = 1;
         m->st[1].fused_first = 1;
         m->st[1].flops += m->st[0].flops;

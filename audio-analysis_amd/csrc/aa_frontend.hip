@@ -19,6 +19,7 @@
 #include "aa_common.h"
 
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 namespace aa {
@@ -38,6 +39,8 @@ struct FePlan {
     float2* d_tw2 = nullptr;  // exp(-2 pi i k / n_fft), k <= Nc
     int4* d_rows = nullptr;   // per band: (first bin, count, value offset, 0)
     float* d_vals = nullptr;  // CSR values
+    char* d_cimg = nullptr;   // fe_stft_mel_4096 block constants (W4096^k | rows | values), 1-KiB padded
+    int cimg_bytes = 0;
 };
 
 // ---------------------------------------------------------------------------
@@ -200,7 +203,35 @@ struct Pass {
 //   pass 3  radix 8, NS = 64
 //   pass 4  radix NC/512, NS = 512   (NC = 1024: 2, 2048: 4, 4096: 8)
 // ---------------------------------------------------------------------------
-template <int NFFT>
+// Correctly rounded (x - lo) / scale as three instructions: with
+// y = RN(1/scale), q0 = RN(a y) is within an ulp of a/scale, the residual
+// a - q0 scale is exact in one fma, and RN(q0 + r y) is the correctly rounded
+// quotient (Markstein's theorem; tools/div_check.hip compares it with
+// __fdiv_rn on 3.4e10 operand pairs: no mismatch).  Then normalize_data's
+// remaining steps in reference order (src/identify_tracks.py:205-208).
+__device__ __forceinline__ float normalize_sample(float x, float lo, float scale, float inv) {
+    const float a = __fsub_rn(x, lo);
+    const float q0 = __fmul_rn(a, inv);
+    const float r = fmaf(-q0, scale, a);
+    float y = fmaf(r, inv, q0);
+    y = __fadd_rn(y, 0.000001f);
+    y = __fsub_rn(y, 0.5f);
+    return __fmul_rn(y, 2.0f);
+}
+
+// complex64 -> np.abs (hypot) -> ** power.  The power mode is a template
+// parameter: a runtime select between the three forms would make every bin
+// pay for the inlined powf.
+enum { PM_GENERAL = 0, PM_ABS = 1, PM_SQUARE = 2 };
+template <int PM>
+__device__ __forceinline__ float pow_mag(float re, float im, float power) {
+    const float mag = sqrtf(re * re + im * im);
+    if constexpr (PM == PM_SQUARE) return mag * mag;
+    else if constexpr (PM == PM_ABS) return mag;
+    else return powf(mag, power);
+}
+
+template <int NFFT, int PM>
 __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
     const float* __restrict__ pcm, const aa_window* __restrict__ wins, const float4* __restrict__ stats,
     const float* __restrict__ hann, const float2* __restrict__ tw, const float2* __restrict__ tw2,
@@ -264,6 +295,7 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
         hi = fmaxf(hi, st.y);
     }
     const float scale = __fsub_rn(hi, lo);  // == max(x - min) (monotone rounding)
+    const float inv = __fdiv_rn(1.f, scale);
 
     // --- overlapped segment -> LDS, normalised; loads issued in batches of
     // SEGU per thread before any is consumed ---
@@ -289,12 +321,7 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
                 float v = 0.f;
                 if (i >= 0 && i < win_len) {
                     v = ok[u] ? raw[u] : 0.f;
-                    if (normalize) {
-                        float y = __fdiv_rn(__fsub_rn(v, lo), scale);
-                        y = __fadd_rn(y, 0.000001f);
-                        y = __fsub_rn(y, 0.5f);
-                        v = __fmul_rn(y, 2.0f);
-                    }
+                    if (normalize) v = normalize_sample(v, lo, scale, inv);
                 }
                 seg[q] = v;
             }
@@ -351,13 +378,7 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
                 re = X.x;
                 im = X.y;
             }
-            // complex64 -> np.abs (hypot) -> ** power
-            const float mag = sqrtf(re * re + im * im);
-            float pw;
-            if (power == 2.f) pw = mag * mag;
-            else if (power == 1.f) pw = mag;
-            else pw = powf(mag, power);
-            Pf[k - kmin] = pw;
+            Pf[k - kmin] = pow_mag<PM>(re, im, power);
         }
         __syncthreads();
         for (int m = tid; m < n_mels; m += NT) {
@@ -424,6 +445,10 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
 constexpr int kFpg = 4;                 // frames (waves) per block
 constexpr int kRow = 66;                // padded transpose row (float2)
 constexpr int kHalf = 16 * kRow;        // per-wave buffer (float2)
+constexpr int kCimgRows = 1026 * 8;     // byte offset of the CSR rows in the constant image
+
+// PCM segment of one block, rounded to whole 64-sample global_load_lds rows
+__host__ __device__ constexpr int fe4096_seg_cap(int hop) { return ((kFpg - 1) * hop + 4096 + 63) & ~63; }
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -460,41 +485,41 @@ __device__ __forceinline__ float swap_pair(float x) {  // value of lane ^ 1
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
 }
 
+template <int PM>
 __global__ __launch_bounds__(256) void fe_stft_mel_4096(
     const float* __restrict__ pcm, const aa_window* __restrict__ wins, const float4* __restrict__ stats,
-    const float2* __restrict__ tw, const float2* __restrict__ tw2, const int4* __restrict__ rows,
-    const float* __restrict__ vals, int nnz, int win_len, int hop, int T, int n_mels, int kmin, int kmax,
-    int normalize, float power, int ngrp, int n_items, float* __restrict__ melS,
+    const float2* __restrict__ tw, const char* __restrict__ cimg, int cimg_bytes, int win_len, int hop, int T,
+    int n_mels, int kmin, int kmax, int normalize, float power, int ngrp, int n_items, float* __restrict__ melS,
     float* __restrict__ blkmax) {
     constexpr int NC = 2048;
     extern __shared__ float lds[];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const int seg_cap = ((kFpg - 1) * hop + 4096 + 3) & ~3;
+    const int seg_cap = fe4096_seg_cap(hop);
     float* seg = lds;
     float2* wb = reinterpret_cast<float2*>(seg + seg_cap) + wave * kHalf;  // this wave's buffer
-    float2* stw2 = reinterpret_cast<float2*>(seg + seg_cap) + kFpg * kHalf;  // W4096^k, k <= 1024
-    float* melT = reinterpret_cast<float*>(stw2 + 1026);                     // [n_mels][kFpg]
-    int4* srows = reinterpret_cast<int4*>(melT + ((n_mels * kFpg + 3) & ~3));
-    float* svals = reinterpret_cast<float*>(srows + n_mels);
+    // block constants, one contiguous image (fe4096_cimg): W4096^k | CSR rows | CSR values
+    char* cl = reinterpret_cast<char*>(reinterpret_cast<float2*>(seg + seg_cap) + kFpg * kHalf);
+    const float2* stw2 = reinterpret_cast<const float2*>(cl);
+    const int4* srows = reinterpret_cast<const int4*>(cl + kCimgRows);
+    const float* svals = reinterpret_cast<const float*>(srows + n_mels);
+    float* melT = reinterpret_cast<float*>(cl + cimg_bytes);  // [n_mels][kFpg]
     const int xlo = max(kmin - 1, 0), xhi = min(kmax + 1, NC);  // X bins kept
 
-    // ---- per-block constants ----
-    for (int i = tid; i <= 1024; i += 256) stw2[i] = tw2[i];
-    for (int i = tid; i < n_mels; i += 256) srows[i] = rows[i];
-    for (int i = tid; i < nnz; i += 256) svals[i] = vals[i];
+    // ---- block prologue: every global read is issued before the first wait.
+    // The constant image and the overlapped PCM segment go global -> LDS by
+    // global_load_lds (no registers, no per-iteration waits); the window
+    // descriptor is the only dependent round trip. ----
+    for (int g = wave; g < cimg_bytes / 1024; g += kFpg)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(cimg + g * 1024 + lane * 16),
+                                         (__attribute__((address_space(3))) void*)(cl + g * 1024), 16, 0, 0);
     // step-2 twiddles W2048^(c k1) = (W^8c)^(k1/8) (W^c)^(k1%8): two short power
     // ladders from two table entries (<= 4 roundings per twiddle)
     float2 p1[8], p8[4];
     p1[0] = make_float2(1.f, 0.f);
     p1[1] = tw[lane];
-#pragma unroll
-    for (int i = 2; i < 8; ++i) p1[i] = cmul(p1[i - 1], p1[1]);
     p8[0] = make_float2(1.f, 0.f);
     p8[1] = tw[(8 * lane) & (NC - 1)];
-    p8[2] = cmul(p8[1], p8[1]);
-    p8[3] = cmul(p8[2], p8[1]);
-
 
     const int k1 = lane >> 1, h = lane & 1;
     {
@@ -505,6 +530,19 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
         const int nf = min(kFpg, T - f0);
         const int seg_len = (nf - 1) * hop + 4096;
         const aa_window d = wins[w];
+        const int base = f0 * hop - 2048;
+        const long long safe = d.n_valid > 0 ? d.src : 0;
+        // raw segment: lane q of wave-instruction gg loads sample base + q (a
+        // clamped in-bounds address where the window has no sample; the
+        // normalisation pass below rewrites those)
+        for (int gg = wave; gg * 64 < seg_len; gg += kFpg) {
+            const int q = gg * 64 + lane;
+            const int i = base + q;
+            const int rel = i - d.pad_left;
+            const bool ok = q < seg_len && i >= 0 && i < win_len && rel >= 0 && rel < d.n_valid;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(pcm + (ok ? d.src + rel : safe)),
+                                             (__attribute__((address_space(3))) void*)(seg + gg * 64), 4, 0, 0);
+        }
         float lo = INFINITY, hi = -INFINITY;
 #pragma unroll
         for (int s = 0; s < kStatSplit; ++s) {
@@ -513,38 +551,31 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
             hi = fmaxf(hi, st.y);
         }
         const float scale = __fsub_rn(hi, lo);
-        // ---- normalised overlapped segment (all 512 threads) ----
-        {
-            const int base = f0 * hop - 2048;
-            constexpr int SEGU = 8;
-            const long long safe = d.n_valid > 0 ? d.src : 0;
-            for (int q0 = 0; q0 < seg_len; q0 += SEGU * 256) {
-                float raw[SEGU];
-                bool ok[SEGU];
+        const float inv = __fdiv_rn(1.f, scale);
 #pragma unroll
-                for (int u = 0; u < SEGU; ++u) {
+        for (int i = 2; i < 8; ++i) p1[i] = cmul(p1[i - 1], p1[1]);
+        p8[2] = cmul(p8[1], p8[1]);
+        p8[3] = cmul(p8[2], p8[1]);
+        __syncthreads();  // vmcnt(0): segment and constants have landed
+        // ---- normalise in place (np.pad zeros, centre padding stays 0) ----
+        {
+            constexpr int U = 8;
+            for (int q0 = 0; q0 < seg_len; q0 += U * 256) {
+                float v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) v[u] = seg[min(q0 + u * 256 + tid, seg_cap - 1)];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
                     const int q = q0 + u * 256 + tid;
                     const int i = base + q;
                     const int rel = i - d.pad_left;
-                    ok[u] = q < seg_len && i >= 0 && i < win_len && rel >= 0 && rel < d.n_valid;
-                    raw[u] = pcm[ok[u] ? d.src + rel : safe];
-                }
-#pragma unroll
-                for (int u = 0; u < SEGU; ++u) {
-                    const int q = q0 + u * 256 + tid;
-                    const int i = base + q;
                     if (q < seg_len) {
-                        float v = 0.f;
+                        float x = 0.f;
                         if (i >= 0 && i < win_len) {
-                            v = ok[u] ? raw[u] : 0.f;
-                            if (normalize) {
-                                float y = __fdiv_rn(__fsub_rn(v, lo), scale);
-                                y = __fadd_rn(y, 0.000001f);
-                                y = __fsub_rn(y, 0.5f);
-                                v = __fmul_rn(y, 2.0f);
-                            }
+                            x = (rel >= 0 && rel < d.n_valid) ? v[u] : 0.f;
+                            if (normalize) x = normalize_sample(x, lo, scale, inv);
                         }
-                        seg[q] = v;
+                        seg[q] = x;
                     }
                 }
             }
@@ -634,8 +665,7 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
                 if (k == NC) cp.y = -cp.y;  // X[2049] = conj X[2047]
                 const float re = 0.5f * c0.x - 0.25f * (cm.x + cp.x);
                 const float im = 0.5f * c0.y - 0.25f * (cm.y + cp.y);
-                const float mag = sqrtf(re * re + im * im);
-                pw[t] = (power == 2.f) ? mag * mag : (power == 1.f) ? mag : powf(mag, power);
+                pw[t] = pow_mag<PM>(re, im, power);
             }
             wave_sync();
             float* P = reinterpret_cast<float*>(wb);
@@ -741,14 +771,14 @@ static size_t fe_lds_bytes(const FePlan& p) {
                             (size_t)std::max(p.nnz, 1));
 }
 
-template <int NFFT>
+template <int NFFT, int PM>
 static int launch_stft(const FePlan& p, const float* pcm, const aa_window* wins, int n_win,
                        const float4* stats, float* melS, float* blkmax, hipStream_t st) {
     const size_t lds = fe_lds_bytes(p);
     AA_CHECK(lds <= 150 * 1024, AA_ERR_UNSUPPORTED, "fe: hop %d needs %zu B of LDS", p.cfg.hop, lds);
     static size_t attr_set = 0;  // dynamic LDS opt-in already granted (static LDS comes on top)
     if (lds > attr_set) {
-        AA_HIP(hipFuncSetAttribute((const void*)fe_stft_mel<NFFT>,
+        AA_HIP(hipFuncSetAttribute((const void*)fe_stft_mel<NFFT, PM>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr_set = lds;
     }
@@ -756,7 +786,7 @@ static int launch_stft(const FePlan& p, const float* pcm, const aa_window* wins,
     // persistent grid: as many blocks as fit (LDS-limited) on 256 CUs
     const int per_cu = std::max(1, (int)((160 * 1024) / (lds + 256)));
     const int grid = std::min(n_items, 256 * per_cu);
-    hipLaunchKernelGGL(fe_stft_mel<NFFT>, dim3(grid), dim3(NFFT / 16), lds, st, pcm, wins, stats, p.d_win,
+    hipLaunchKernelGGL((fe_stft_mel<NFFT, PM>), dim3(grid), dim3(NFFT / 16), lds, st, pcm, wins, stats, p.d_win,
                        p.d_tw, p.d_tw2, p.d_rows, p.d_vals, p.nnz, p.cfg.win_len, p.cfg.hop, p.T,
                        p.cfg.n_mels, p.kmin, p.kmax, p.cfg.normalize, p.cfg.power, p.nfblk, n_items,
                        melS, blkmax);
@@ -772,27 +802,26 @@ static bool fe_fast4096(const FePlan& p) {
 }
 
 static size_t fe_lds_bytes4096(const FePlan& p) {
-    const int seg_cap = ((kFpg - 1) * p.cfg.hop + 4096 + 3) & ~3;
-    return sizeof(float) * ((size_t)seg_cap + 2 * (size_t)kFpg * kHalf + 2 * 1026 +
-                            (size_t)((p.cfg.n_mels * kFpg + 3) & ~3) + 4 * (size_t)p.cfg.n_mels +
-                            (size_t)std::max(p.nnz, 1));
+    return sizeof(float) * (size_t)fe4096_seg_cap(p.cfg.hop) + sizeof(float2) * (size_t)kFpg * kHalf +
+           (size_t)p.cimg_bytes + sizeof(float) * (size_t)p.cfg.n_mels * kFpg;
 }
 
+template <int PM>
 static int launch_stft4096(const FePlan& p, const float* pcm, const aa_window* wins, int n_win,
                            const float4* stats, float* melS, float* blkmax, hipStream_t st) {
     const size_t lds = fe_lds_bytes4096(p);
     AA_CHECK(lds <= 150 * 1024, AA_ERR_UNSUPPORTED, "fe4096: hop %d needs %zu B of LDS", p.cfg.hop, lds);
     static size_t attr_set = 0;
     if (lds > attr_set) {
-        AA_HIP(hipFuncSetAttribute((const void*)fe_stft_mel_4096, hipFuncAttributeMaxDynamicSharedMemorySize,
+        AA_HIP(hipFuncSetAttribute((const void*)fe_stft_mel_4096<PM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds));
         attr_set = lds;
     }
     const int ngrp = p.nfblk;
     const int n_items = ngrp * n_win;
-    hipLaunchKernelGGL(fe_stft_mel_4096, dim3(n_items), dim3(256), lds, st, pcm, wins, stats, p.d_tw, p.d_tw2,
-                       p.d_rows, p.d_vals, p.nnz, p.cfg.win_len, p.cfg.hop, p.T, p.cfg.n_mels, p.kmin,
-                       p.kmax, p.cfg.normalize, p.cfg.power, ngrp, n_items, melS, blkmax);
+    hipLaunchKernelGGL(fe_stft_mel_4096<PM>, dim3(n_items), dim3(256), lds, st, pcm, wins, stats, p.d_tw, p.d_cimg,
+                       p.cimg_bytes, p.cfg.win_len, p.cfg.hop, p.T, p.cfg.n_mels, p.kmin, p.kmax,
+                       p.cfg.normalize, p.cfg.power, ngrp, n_items, melS, blkmax);
     AA_LAUNCH_CHECK();
     return AA_OK;
 }
@@ -879,6 +908,16 @@ extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** 
     if (e == hipSuccess) e = up((void**)&p->d_tw2, tw2.data(), sizeof(float2) * (nc + 1));
     if (e == hipSuccess) e = up((void**)&p->d_rows, rows.data(), sizeof(int4) * rows.size());
     if (e == hipSuccess) e = up((void**)&p->d_vals, vals.data(), sizeof(float) * vals.size());
+    if (e == hipSuccess && n == 4096) {
+        // constant image of the wave-per-frame kernel, byte-identical to its LDS region
+        const size_t raw = kCimgRows + sizeof(int4) * rows.size() + sizeof(float) * vals.size();
+        std::vector<char> img((raw + 1023) / 1024 * 1024, 0);
+        memcpy(img.data(), tw2.data(), sizeof(float2) * 1025);
+        memcpy(img.data() + kCimgRows, rows.data(), sizeof(int4) * rows.size());
+        memcpy(img.data() + kCimgRows + sizeof(int4) * rows.size(), vals.data(), sizeof(float) * vals.size());
+        p->cimg_bytes = (int)img.size();
+        e = up((void**)&p->d_cimg, img.data(), img.size());
+    }
     if (e != hipSuccess) {
         set_error("aa_fe_create: %s", hipGetErrorString(e));
         aa_fe_destroy(p);
@@ -898,6 +937,7 @@ extern "C" int aa_fe_destroy(void* plan) {
     (void)hipFree(p->d_tw2);
     (void)hipFree(p->d_rows);
     (void)hipFree(p->d_vals);
+    (void)hipFree(p->d_cimg);
     delete p;
     return AA_OK;
 }
@@ -926,15 +966,20 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
     hipLaunchKernelGGL(fe_stats, dim3(kStatSplit, n_win), dim3(256), 0, st, pcm, windows,
                        p->cfg.win_len, ws.stats);
     AA_LAUNCH_CHECK();
+    const int pm = p->cfg.power == 2.f ? PM_SQUARE : p->cfg.power == 1.f ? PM_ABS : PM_GENERAL;
     int rc;
-    if (fe_fast4096(*p)) {
-        rc = launch_stft4096(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st);
-        if (rc != AA_OK) return rc;
-    } else switch (p->cfg.n_fft) {
-        case 2048: rc = launch_stft<2048>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
-        case 4096: rc = launch_stft<4096>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
-        default: rc = launch_stft<8192>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;
+#define AA_FE_PM(PM)                                                                                    \
+    if (fe_fast4096(*p)) {                                                                              \
+        rc = launch_stft4096<PM>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st);            \
+    } else switch (p->cfg.n_fft) {                                                                      \
+        case 2048: rc = launch_stft<2048, PM>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break; \
+        case 4096: rc = launch_stft<4096, PM>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break; \
+        default: rc = launch_stft<8192, PM>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st); break;   \
     }
+    if (pm == PM_SQUARE) { AA_FE_PM(PM_SQUARE) }
+    else if (pm == PM_ABS) { AA_FE_PM(PM_ABS) }
+    else { AA_FE_PM(PM_GENERAL) }
+#undef AA_FE_PM
     if (rc != AA_OK) return rc;
     hipLaunchKernelGGL(fe_db, dim3((p->cfg.n_mels + 3) / 4, n_win), dim3(256), 0, st, ws.melS,
                        ws.blkmax, ws.stats, p->nfblk, p->cfg.n_mels, p->T, p->cfg.db_scale,

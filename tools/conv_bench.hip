@@ -75,6 +75,24 @@ int main() {
                fl / full * 1e-6, mf);                                                                     \
     }
     AA_CONV_CFGS(AA_BENCH)
+    // first conv (1 -> 32, VALU) fused into the 3x3/32 pool-3 stage, on a
+    // 160 x 226 log-mel input
+    {
+        float* w1;
+        float* b1;
+        (void)hipMalloc(&w1, 32 * 9 * 4);
+        (void)hipMalloc(&b1, 32 * 4);
+        std::vector<float> hw(32 * 9, 0.05f), hb(32, 0.01f);
+        (void)hipMemcpy(w1, hw.data(), hw.size() * 4, hipMemcpyHostToDevice);
+        (void)hipMemcpy(b1, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
+        FirstConv f1{w1, b1, 1, 0.3f, 0, 1.f, 160, 226};
+        const int H = 158, W = 224;
+#define AA_FUSED(D)                                                                                        \
+    printf("fused c1+c2 DIAG %2d: %7.1f us\n", D,                                                         \
+           time_one<bf16, 3, 3, 32, 4, 1, 9, 2, 3, 12, 48, D, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
+        AA_FUSED(0) AA_FUSED(2) AA_FUSED(4) AA_FUSED(6)
+#undef AA_FUSED
+    }
     // ablations of the 9x3 layer: staging / MFMA / stores / weight stream
     {
         int H, W, C;

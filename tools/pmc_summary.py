@@ -5,7 +5,7 @@ import glob
 import sys
 
 for path in sys.argv[1:]:
-    for f in glob.glob(path.rstrip("/") + "/*/*counter_collection.csv"):
+    for f in glob.glob(path.rstrip("/") + "/*counter_collection.csv") + glob.glob(path.rstrip("/") + "/*/*counter_collection.csv"):
         rows = list(csv.DictReader(open(f)))
         agg = collections.defaultdict(float)
         meta = {}

@@ -7,7 +7,7 @@ path = sys.argv[1]
 files = glob.glob(path) if ("*" in path or not path.endswith(".csv")) else [path]
 files = [f for f in files if f.endswith(".csv")]
 if not files:
-    files = glob.glob(path.rstrip("/") + "/*/*_kernel_stats.csv")
+    files = glob.glob(path.rstrip("/") + "/*_kernel_stats.csv") + glob.glob(path.rstrip("/") + "/*/*_kernel_stats.csv")
 for f in files:
     rows = list(csv.DictReader(open(f)))
     print(f"{'kernel':64s} {'calls':>6s} {'avg_us':>9s} {'min_us':>9s} {'tot%':>6s}")
