@@ -93,7 +93,7 @@ class FrontEnd:
         return (n_win, self.s.n_mels, self.T, self.s.channels)
 
     def run(self, pcm: torch.Tensor, windows: torch.Tensor, out: torch.Tensor = None,
-            status: torch.Tensor = None, stream=None) -> torch.Tensor:
+            status: torch.Tensor = None, stream=None, workspace: torch.Tensor = None) -> torch.Tensor:
         """pcm: float32 [N] on device; windows: int64 [n_win, 2] packed aa_window
         rows (see ``pack_windows``) on device."""
         n_win = int(windows.shape[0])
@@ -103,7 +103,7 @@ class FrontEnd:
             return out
         assert pcm.dtype == torch.float32 and windows.dtype == torch.int64
         assert tuple(out.shape) == self.out_shape(n_win)
-        ws = self._workspace(n_win)
+        ws = workspace if workspace is not None else self._workspace(n_win)
         _lib.check(_lib.lib().aa_fe_run(
             self._h, _lib.dptr(pcm), int(pcm.numel()), _lib.dptr(windows), n_win, _lib.dptr(out),
             _lib.dptr(status), _lib.dptr(ws), int(ws.numel()), _lib.stream_ptr(stream)), "aa_fe_run")

@@ -217,7 +217,8 @@ struct FirstConv {
 // DIAG (diagnostic builds only, tools/conv_bench.hip): bit 0 skips the patch
 // staging, bit 1 the MFMA loop, bit 2 the epilogue stores, bit 3 makes every
 // lane read pixel 0 (no LDS bank conflicts), bit 4 re-reads chunk 0's weights
-// (L1-resident, no L2 stream), bit 5 skips the weight loads in the loop.
+// (L1-resident, no L2 stream), bit 5 skips the weight loads in the loop, bit 7
+// skips the fragment reads after the first (MFMA issue alone).
 // Waves per SIMD a conv_mfma block shape reaches (LDS-limited), told to the
 // compiler so it schedules for latency at that occupancy instead of trimming
 // registers for an occupancy the LDS footprint never allows.
@@ -232,7 +233,8 @@ constexpr int conv_waves_per_simd() {
 template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW,
           bool FUSED = false, int DIAG = 0, bool EBF16 = false, bool APF = true>
 __global__ __launch_bounds__(WM * WN * 64)
-__attribute__((amdgpu_waves_per_eu(conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>())))
+__attribute__((amdgpu_waves_per_eu(conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>(),
+                                    conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>())))
 void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                                                  const T* __restrict__ wt, const float* __restrict__ bias,
                                                  T* __restrict__ out, int Hout, int Wout, int cout_store,
@@ -429,6 +431,27 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
     }
     const int brow = (wn * NF * 16 + (lane & 15)) * CSTR + q8;
     const bool hi_share = (GPS % NW == 0) || wave < GPS % NW;
+    // Fragments are double-buffered in registers: while chunk q's MFMAs run,
+    // chunk q+1's fragments are in flight.  Across a tap boundary only the A
+    // fragments (from the static patch) can run ahead; the next slice's B
+    // fragments follow the barrier that publishes it.
+    Frag<T> fa[MF], fb[NF], na[MF], nb[NF];
+#define AA_LOAD_A(dst, tap, cc_)                                                             \
+    if (!(DIAG & 128) || (tap) == 0)                                                         \
+    {                                                                                        \
+        const int kh_ = (tap) / KW, kw_ = (tap) - ((tap) / KW) * KW;                         \
+        const int at_ = (kh_ * PW + kw_) * CSTR + (cc_) * 32;                                \
+        _Pragma("unroll") for (int i = 0; i < MF; ++i) dst[i].load(patch + abase[i] + at_); \
+    }
+#define AA_LOAD_B(dst, buf, cc_)                                                             \
+    if (!(DIAG & 128) || (buf) < 0)                                                          \
+    {                                                                                        \
+        const T* bt_ = reinterpret_cast<const T*>(Bs + (buf) * SLICE_LDS) + brow + (cc_) * 32; \
+        _Pragma("unroll") for (int j = 0; j < NF; ++j) dst[j].load(bt_ + j * 16 * CSTR);   \
+    }
+    // f32 (parity mode) fragments are twice as wide: single-buffered there
+    constexpr bool DB = sizeof(T) == 2;
+    if constexpr (DB) AA_LOAD_A(fa, 0, 0)
     for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); ++t) {
         // slices t+1 .. min(t+NB-2, NTAP-1) may stay in flight
         const int ahead = min(NB - 2, NTAP - 1 - t);
@@ -444,34 +467,42 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
         if constexpr (!(DIAG & 32)) {
             if (t + NB - 1 < NTAP) { AA_GLDS(t + NB - 1) }
         }
-        const T* Bt = reinterpret_cast<const T*>(Bs + ((DIAG & 16) ? 0 : (t % NB)) * SLICE_LDS);
-        const int kh = t / KW, kw = t - (t / KW) * KW;
-        const int atap = (kh * PW + kw) * CSTR;
+        const int buf = (DIAG & 16) ? 0 : (t % NB);
+        if constexpr (!DB) {
+#pragma unroll
+            for (int cc = 0; cc < CPC; ++cc) {
+                AA_LOAD_A(fa, t, cc)
+                AA_LOAD_B(fb, buf, cc)
+#pragma unroll
+                for (int i = 0; i < MF; ++i)
+#pragma unroll
+                    for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(fa[i], fb[j], acc[i][j]);
+            }
+            continue;
+        }
+        AA_LOAD_B(fb, buf, 0)
 #pragma unroll
         for (int cc = 0; cc < CPC; ++cc) {
-            Frag<T> b[NF], a[MF];
-#pragma unroll
-            for (int j = 0; j < NF; ++j) b[j].load(Bt + brow + j * 16 * CSTR + cc * 32);
-#pragma unroll
-            for (int i = 0; i < MF; ++i) a[i].load(patch + abase[i] + atap + cc * 32);
+            if (cc + 1 < CPC) {
+                AA_LOAD_A(na, t, cc + 1)
+                AA_LOAD_B(nb, buf, cc + 1)
+            } else if (t + 1 < NTAP) {
+                AA_LOAD_A(na, t + 1, 0)
+            }
 #pragma unroll
             for (int i = 0; i < MF; ++i)
 #pragma unroll
-                for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(a[i], b[j], acc[i][j]);
-            if constexpr (sizeof(T) == 2) {
-                // issue order: the B fragments and two A fragments, then one
-                // A fragment ahead of each row of NF MFMAs (left alone, the
-                // scheduler reuses one A register and waits lgkmcnt(0) before
-                // every row)
-                __builtin_amdgcn_sched_group_barrier(0x100, NF + (MF > 1 ? 2 : 1), 0);
+                for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(fa[i], fb[j], acc[i][j]);
 #pragma unroll
-                for (int i = 0; i < MF; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
-                    if (i + 2 < MF) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
+            for (int i = 0; i < MF; ++i) fa[i] = na[i];
+            if (cc + 1 < CPC) {
+#pragma unroll
+                for (int j = 0; j < NF; ++j) fb[j] = nb[j];
             }
         }
     }
+#undef AA_LOAD_A
+#undef AA_LOAD_B
 #undef AA_GLDS
     __syncthreads();  // patch no longer needed: reuse LDS for the f32 tile
 

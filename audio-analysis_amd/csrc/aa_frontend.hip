@@ -485,7 +485,10 @@ __device__ __forceinline__ float swap_pair(float x) {  // value of lane ^ 1
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
 }
 
-template <int PM>
+// DIAG (tools/fe_bench.hip only): 1 skip the global->LDS staging, 2 the
+// normalisation pass, 4 the FFT (steps 1-5), 8 the real split, 16 Hann and
+// power, 32 the mel rows, 64 the output stores.
+template <int PM, int DIAG = 0>
 __global__ __launch_bounds__(256) void fe_stft_mel_4096(
     const float* __restrict__ pcm, const aa_window* __restrict__ wins, const float4* __restrict__ stats,
     const float2* __restrict__ tw, const char* __restrict__ cimg, int cimg_bytes, int win_len, int hop, int T,
@@ -504,13 +507,12 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
     const int4* srows = reinterpret_cast<const int4*>(cl + kCimgRows);
     const float* svals = reinterpret_cast<const float*>(srows + n_mels);
     float* melT = reinterpret_cast<float*>(cl + cimg_bytes);  // [n_mels][kFpg]
-    const int xlo = max(kmin - 1, 0), xhi = min(kmax + 1, NC);  // X bins kept
 
     // ---- block prologue: every global read is issued before the first wait.
     // The constant image and the overlapped PCM segment go global -> LDS by
     // global_load_lds (no registers, no per-iteration waits); the window
     // descriptor is the only dependent round trip. ----
-    for (int g = wave; g < cimg_bytes / 1024; g += kFpg)
+    for (int g = wave; g < ((DIAG & 1) ? 0 : cimg_bytes / 1024); g += kFpg)
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(cimg + g * 1024 + lane * 16),
                                          (__attribute__((address_space(3))) void*)(cl + g * 1024), 16, 0, 0);
     // step-2 twiddles W2048^(c k1) = (W^8c)^(k1/8) (W^c)^(k1%8): two short power
@@ -535,7 +537,7 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
         // raw segment: lane q of wave-instruction gg loads sample base + q (a
         // clamped in-bounds address where the window has no sample; the
         // normalisation pass below rewrites those)
-        for (int gg = wave; gg * 64 < seg_len; gg += kFpg) {
+        for (int gg = wave; gg * 64 < ((DIAG & 1) ? 0 : seg_len); gg += kFpg) {
             const int q = gg * 64 + lane;
             const int i = base + q;
             const int rel = i - d.pad_left;
@@ -560,7 +562,7 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
         // ---- normalise in place (np.pad zeros, centre padding stays 0) ----
         {
             constexpr int U = 8;
-            for (int q0 = 0; q0 < seg_len; q0 += U * 256) {
+            for (int q0 = 0; q0 < ((DIAG & 2) ? 0 : seg_len); q0 += U * 256) {
                 float v[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) v[u] = seg[min(q0 + u * 256 + tid, seg_cap - 1)];
@@ -583,6 +585,11 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
         __syncthreads();
         float bmax = 0.f;
         if (wave < nf) {
+            float2 u[32];
+            if constexpr ((DIAG & 4) != 0) {
+#pragma unroll
+                for (int j = 0; j < 32; ++j) u[j] = make_float2((float)j, seg[lane + j]);
+            } else {
             // ---- 1. load + DFT-32 over r ----
             float2 y[32];
             const float* x = seg + wave * hop + 2 * lane;
@@ -596,7 +603,6 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
                 y[dperm(k)] = cmul(y[dperm(k)], t);
             }
             // ---- 3. transpose in two halves ----
-            float2 u[32];
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
 #pragma unroll
@@ -620,16 +626,17 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
                 const float2 t = cmul(wconst64(j), E1);
                 u[dperm(j)] = h ? csub(E0, t) : cadd(E0, t);
             }
+            }
             // lane holds Z[k1 + 32 (32 h + j)] in u[dperm(j)]
             // ---- 6. real split ----
-            if (h) {
+            if (h && !(DIAG & 8)) {
 #pragma unroll
                 for (int j = 0; j < 32; ++j) wb[k1 + 32 * j] = u[dperm(j)];  // Z[1024 + k1 + 32 j]
             }
             wave_sync();
             // h = 0 lanes: X[k], k = k1 + 32 j < 1024 (bands above NC/2 take the
             // generic kernel, see fe_fast4096)
-            if (!h) {
+            if (!h && !(DIAG & 8)) {
 #pragma unroll
                 for (int j = 0; j < 32; ++j) {
                     const int k = k1 + 32 * j;
@@ -643,12 +650,9 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
                 }
             }
             wave_sync();
-            if (!h) {
+            if (!h) {  // X[0..1023] in natural order (the host keeps 1 <= kmin, kmax <= 1022)
 #pragma unroll
-                for (int j = 0; j < 32; ++j) {
-                    const int k = k1 + 32 * j;
-                    if (k >= xlo && k <= xhi) wb[k - xlo] = u[dperm(j)];
-                }
+                for (int j = 0; j < 32; ++j) wb[k1 + 32 * j] = u[dperm(j)];
             }
             wave_sync();
             // ---- 7. Hann in frequency, |.|^power ----
@@ -656,13 +660,9 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
             float pw[PT];
             const int nb = kmax - kmin + 1;
 #pragma unroll
-            for (int t = 0; t < PT; ++t) {
+            for (int t = 0; t < ((DIAG & 16) ? 0 : PT); ++t) {
                 const int k = min(kmin + lane + 64 * t, kmax);  // clamped: unconditional LDS reads
-                const float2 c0 = wb[k - xlo];
-                float2 cm = wb[max(k - 1, 0) - xlo + (k == 0 ? 1 : 0)];
-                float2 cp = wb[min(k + 1, NC) - xlo - (k == NC ? 1 : 0)];
-                if (k == 0) cm.y = -cm.y;   // X[-1] = conj X[1]
-                if (k == NC) cp.y = -cp.y;  // X[2049] = conj X[2047]
+                const float2 c0 = wb[k], cm = wb[k - 1], cp = wb[k + 1];
                 const float re = 0.5f * c0.x - 0.25f * (cm.x + cp.x);
                 const float im = 0.5f * c0.y - 0.25f * (cm.y + cp.y);
                 pw[t] = pow_mag<PM>(re, im, power);
@@ -670,32 +670,30 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
             wave_sync();
             float* P = reinterpret_cast<float*>(wb);
 #pragma unroll
-            for (int t = 0; t < PT; ++t)
+            for (int t = 0; t < ((DIAG & 16) ? 0 : PT); ++t)
                 if (lane + 64 * t < nb) P[lane + 64 * t] = pw[t];
             wave_sync();
             // ---- 8. mel rows ----
-            for (int m = lane; m < n_mels; m += 64) {
+            // rows of the constant image are zero-padded to whole float4s
+            // (value offsets 16-B aligned); the padding adds exact zeros
+            for (int m = lane; m < ((DIAG & 32) ? 0 : n_mels); m += 64) {
                 const int4 rw = srows[m];
-                const float* wv = svals + rw.z;
+                const float4* wv = reinterpret_cast<const float4*>(svals + rw.z);
                 const float* pv = P + (rw.x - kmin);
                 float s = 0.f;
-                for (int i0 = 0; i0 < rw.y; i0 += 16) {
-                    float a[16], b[16];
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int ii = min(i0 + i, rw.y - 1);
-                        a[i] = (i0 + i < rw.y) ? wv[ii] : 0.f;
-                        b[i] = pv[ii];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) s = fmaf(a[i], b[i], s);
+                for (int i = 0; i < rw.y; i += 4) {
+                    const float4 a = wv[i >> 2];
+                    s = fmaf(a.x, pv[i], s);
+                    s = fmaf(a.y, pv[i + 1], s);
+                    s = fmaf(a.z, pv[i + 2], s);
+                    s = fmaf(a.w, pv[i + 3], s);
                 }
                 melT[m * kFpg + wave] = s;
                 bmax = fmaxf(bmax, s);
             }
         }
         __syncthreads();
-        for (int idx = tid; idx < n_mels * nf; idx += 256) {
+        for (int idx = tid; idx < ((DIAG & 64) ? 0 : n_mels * nf); idx += 256) {
             const int m = idx / nf, f = idx - (idx / nf) * nf;
             melS[((size_t)w * n_mels + m) * T + f0 + f] = melT[m * kFpg + f];
         }
@@ -797,8 +795,10 @@ static int launch_stft(const FePlan& p, const float* pcm, const aa_window* wins,
 // the wave-per-frame kernel covers n_fft 4096 whenever the kept band fits the
 // per-wave buffer (15 bins per lane)
 static bool fe_fast4096(const FePlan& p) {
-    return p.cfg.n_fft == 4096 && p.kmax - p.kmin + 1 <= (kHalf / 64 - 1) * 64 &&
-           p.kmax - p.kmin + 3 <= kHalf && p.kmax + 1 < 1024;
+    // kept band inside X[1..1022] (Hann neighbours in range), padded rows
+    // (+3 bins) inside the 15 x 64 power slots
+    return p.cfg.n_fft == 4096 && p.kmin >= 1 && p.kmax <= 1022 &&
+           p.kmax - p.kmin + 1 + 3 <= (kHalf / 64 - 1) * 64;
 }
 
 static size_t fe_lds_bytes4096(const FePlan& p) {
@@ -910,11 +910,19 @@ extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** 
     if (e == hipSuccess) e = up((void**)&p->d_vals, vals.data(), sizeof(float) * vals.size());
     if (e == hipSuccess && n == 4096) {
         // constant image of the wave-per-frame kernel, byte-identical to its LDS region
-        const size_t raw = kCimgRows + sizeof(int4) * rows.size() + sizeof(float) * vals.size();
+        // CSR rows zero-padded to whole float4s, value offsets 16-B aligned
+        std::vector<int4> prow(rows.size());
+        std::vector<float> pval;
+        for (size_t m = 0; m < rows.size(); ++m) {
+            const int len = (rows[m].y + 3) & ~3;
+            prow[m] = make_int4(rows[m].x, len, (int)pval.size(), 0);
+            for (int i = 0; i < len; ++i) pval.push_back(i < rows[m].y ? vals[rows[m].z + i] : 0.f);
+        }
+        const size_t raw = kCimgRows + sizeof(int4) * prow.size() + sizeof(float) * pval.size();
         std::vector<char> img((raw + 1023) / 1024 * 1024, 0);
         memcpy(img.data(), tw2.data(), sizeof(float2) * 1025);
-        memcpy(img.data() + kCimgRows, rows.data(), sizeof(int4) * rows.size());
-        memcpy(img.data() + kCimgRows + sizeof(int4) * rows.size(), vals.data(), sizeof(float) * vals.size());
+        memcpy(img.data() + kCimgRows, prow.data(), sizeof(int4) * prow.size());
+        memcpy(img.data() + kCimgRows + sizeof(int4) * prow.size(), pval.data(), sizeof(float) * pval.size());
         p->cimg_bytes = (int)img.size();
         e = up((void**)&p->d_cimg, img.data(), img.size());
     }

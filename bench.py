@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bound on the CPU-baseline sample (0 disables)")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="split the step's windows over this many HIP streams (overlaps kernel tails)")
     return ap.parse_args()
 
 
@@ -125,11 +127,41 @@ def main():
     wc = torch.tensor([BATCH_A, BATCH_B], dtype=torch.int32, device=dev)
     tmean = torch.empty((2, model.n_labels), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream()
+    # window chunks, one per stream, each with its own workspaces
+    S = max(1, min(args.streams, n_win))
+    bounds = np.linspace(0, n_win, S + 1).astype(int)
+    chunks = [(int(a), int(b)) for a, b in zip(bounds[:-1], bounds[1:])]
+    streams = [stream] if S == 1 else [torch.cuda.Stream(device=dev) for _ in range(S)]
+    fe_ws = [torch.empty(max(fe.workspace_bytes(b - a), 256), dtype=torch.uint8, device=dev) for a, b in chunks]
+    m_ws = [torch.empty(max(model.workspace_bytes(b - a), 256), dtype=torch.uint8, device=dev) for a, b in chunks]
+
+    def run_chunks(fe_events=None):
+        if S > 1:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        for k, (a, b) in enumerate(chunks):
+            s = streams[k]
+            if S > 1:
+                s.wait_event(ev)
+            e0 = e1 = None
+            if fe_events is not None and k == 0:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+            fe.run(pcm, rows[a:b], out=logmel[a:b], stream=s, workspace=fe_ws[k])
+            if e0 is not None:
+                e1.record(s)
+                fe_events.append((e0, e1, b - a))
+            model.forward(logmel[a:b], logits[a:b], probs[a:b], stream=s, workspace=m_ws[k])
+        if S > 1:
+            for s in streams:
+                done = torch.cuda.Event()
+                done.record(s)
+                stream.wait_event(done)
+        track_mean(probs[None], wb, wc, out=tmean, stream=stream)
 
     def step():
-        fe.run(pcm, rows, out=logmel, stream=stream)
-        model.forward(logmel, logits, probs, stream=stream)
-        track_mean(probs[None], wb, wc, out=tmean, stream=stream)
+        run_chunks()
 
     for _ in range(args.warmup):
         step()
@@ -144,14 +176,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        fe.run(pcm, rows, out=logmel, stream=stream)
-        e1.record(stream)
-        fe_ev.append((e0, e1))
-        model.forward(logmel, logits, probs, stream=stream)
-        track_mean(probs[None], wb, wc, out=tmean, stream=stream)
+        run_chunks(fe_ev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -172,9 +197,11 @@ def main():
     for i in range(model.n_stages()):
         name, flops, byts = model.stage_info(i)
         ms, cnt = model.stage_time(i)
-        stages.append(dict(name=name, flops=flops * n_win, bytes=byts * n_win,
+        # per launch: a launch covers one chunk of the step's windows
+        per = n_win / S
+        stages.append(dict(name=name, flops=flops * per, bytes=byts * per,
                            avg_ms=ms / max(cnt, 1), count=cnt))
-    fe_ms = sum(a.elapsed_time(b) for a, b in fe_ev) / max(len(fe_ev), 1)
+    fe_ms = sum(a.elapsed_time(b) for a, b, _ in fe_ev) / max(len(fe_ev), 1)
     dom = max(stages, key=lambda s: s["avg_ms"])
     achieved = dom["flops"] / (dom["avg_ms"] * 1e-3) / 1e12
     roofline = {"bound": "mfma", "kernel": dom["name"], "achieved": round(achieved, 2),
@@ -195,7 +222,7 @@ def main():
         "config": {"workload": "config2: 64 windows/step (39 of clip A + 25 of clip B, 60 s "
                                "48 kHz mono), htk log-mel n_fft 4096 hop 640 160 mel + model1 CNN",
                    "model": "model1", "global_batch": n_win * world, "seq_len": fe_s.win_len,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "streams": S},
         "roofline": roofline,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -100,7 +100,7 @@ int main() {
 #define AA_ABL(D)                                                                                          \
     printf("abl 9x3 DIAG %2d: %7.1f us\n", D,                                                             \
            time_one<bf16, 9, 3, 64, 4, 2, 5, 4, 3, 9, 33, D, true>(n, H, W, C, in, w, b, out, fc, it));
-        AA_ABL(0) AA_ABL(1) AA_ABL(4) AA_ABL(5) AA_ABL(5 | 32) AA_ABL(5 | 16) AA_ABL(5 | 8) AA_ABL(7) AA_ABL(7 | 32)
+        AA_ABL(0) AA_ABL(1) AA_ABL(4) AA_ABL(5) AA_ABL(5 | 32) AA_ABL(5 | 16) AA_ABL(5 | 8) AA_ABL(7) AA_ABL(7 | 32) AA_ABL(5 | 32 | 128) AA_ABL(5 | 128)
 #undef AA_ABL
     }
     hipError_t e = hipGetLastError();

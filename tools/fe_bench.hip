@@ -1,0 +1,77 @@
+// Diagnostic harness: time fe_stft_mel_4096 with phases ablated (DIAG bits,
+// see the kernel) on the config-2 shape: 64 windows of 144000 samples,
+// n_fft 4096, hop 640, 160 triangular mel bands over bins 5..938.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include
+//   tools/fe_bench.hip audio-analysis_amd/csrc/aa_api.cpp -o tools/fe_bench
+#include "../audio-analysis_amd/csrc/aa_frontend.hip"
+
+#include <cstdio>
+#include <cstdlib>
+
+using namespace aa;
+
+template <int DIAG>
+static float time_diag(const FePlan& p, const float* pcm, const aa_window* wins, int n_win, const float4* stats,
+                       float* melS, float* blkmax, int iters) {
+    const size_t lds = fe_lds_bytes4096(p);
+    (void)hipFuncSetAttribute((const void*)fe_stft_mel_4096<PM_SQUARE, DIAG>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const int n_items = p.nfblk * n_win;
+    auto go = [&]() {
+        hipLaunchKernelGGL((fe_stft_mel_4096<PM_SQUARE, DIAG>), dim3(n_items), dim3(256), lds, 0, pcm, wins, stats,
+                           p.d_tw, p.d_cimg, p.cimg_bytes, p.cfg.win_len, p.cfg.hop, p.T, p.cfg.n_mels, p.kmin,
+                           p.kmax, p.cfg.normalize, p.cfg.power, p.nfblk, n_items, melS, blkmax);
+    };
+    for (int i = 0; i < 3; ++i) go();
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < iters; ++i) go();
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return 1e3f * ms / iters;
+}
+
+int main() {
+    const int n_win = 64, n_mels = 160, nbins = 2049;
+    std::vector<float> fb((size_t)n_mels * nbins, 0.f);
+    for (int m = 0; m < n_mels; ++m) {  // triangles with centres spread over bins 5..938
+        const double a = 5 + 933.0 * m / (n_mels + 1), c = 5 + 933.0 * (m + 1) / (n_mels + 1),
+                     b = 5 + 933.0 * (m + 2) / (n_mels + 1);
+        for (int k = (int)a; k <= (int)b; ++k) {
+            const double v = k < c ? (k - a) / (c - a) : (b - k) / (b - c);
+            if (v > 0) fb[(size_t)m * nbins + k] = (float)v;
+        }
+    }
+    aa_fe_config cfg{144000, 4096, 640, n_mels, 1, 1, 2.f, 1e-10f, 80.f, 0, 1};
+    void* plan = nullptr;
+    if (aa_fe_create(&cfg, fb.data(), &plan) != AA_OK) { printf("create: %s\n", aa_last_error()); return 1; }
+    const FePlan& p = *static_cast<FePlan*>(plan);
+    printf("nnz %d kmin %d kmax %d fast %d lds %zu\n", p.nnz, p.kmin, p.kmax, (int)fe_fast4096(p), fe_lds_bytes4096(p));
+    const size_t n_pcm = 2 * 2880000;
+    std::vector<float> h(n_pcm);
+    for (auto& x : h) x = (rand() % 65536 - 32768) / 32768.f;
+    std::vector<aa_window> hw(n_win);
+    for (int i = 0; i < n_win; ++i) hw[i] = aa_window{(int64_t)(i % 39) * 72000 + (i / 39) * 2880000, 144000, 0};
+    float *pcm, *melS, *blkmax;
+    aa_window* wins;
+    float4* stats;
+    (void)hipMalloc(&pcm, n_pcm * 4);
+    (void)hipMalloc(&wins, n_win * sizeof(aa_window));
+    (void)hipMalloc(&stats, n_win * kStatSplit * sizeof(float4));
+    (void)hipMalloc(&melS, (size_t)n_win * n_mels * p.T * 4);
+    (void)hipMalloc(&blkmax, (size_t)n_win * p.nfblk * 4);
+    (void)hipMemcpy(pcm, h.data(), n_pcm * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(wins, hw.data(), n_win * sizeof(aa_window), hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(fe_stats, dim3(kStatSplit, n_win), dim3(256), 0, 0, pcm, wins, cfg.win_len, stats);
+    const int it = 20;
+#define T_(D) printf("DIAG %3d: %7.1f us\n", D, time_diag<D>(p, pcm, wins, n_win, stats, melS, blkmax, it));
+    T_(0) T_(1) T_(2) T_(3) T_(4) T_(8) T_(16) T_(32) T_(64) T_(4 | 8) T_(4 | 8 | 16) T_(4 | 8 | 16 | 32)
+    T_(127) T_(3 | 32 | 64) T_(1 | 2 | 64)
+#undef T_
+    printf("last error: %s\n", hipGetErrorString(hipGetLastError()));
+    return 0;
+}
