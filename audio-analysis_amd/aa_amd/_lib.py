@@ -69,6 +69,12 @@ _SIGS = {
     "aa_fe_workspace_bytes": (C.c_size_t, [C.c_void_p, C.c_int32]),
     "aa_fe_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p,
                             C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "aa_fe_n_stages": (C.c_int, [C.c_void_p]),
+    "aa_fe_stage_info": (C.c_int, [C.c_void_p, C.c_int32, C.c_char_p, C.c_int32,
+                                   C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "aa_fe_set_timing": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "aa_fe_stage_time": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double),
+                                   C.POINTER(C.c_int64)]),
     "aa_model_create": (C.c_int, [C.POINTER(Layer), C.c_int32, C.c_void_p, C.c_int64, C.c_int32,
                                   C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     "aa_model_destroy": (C.c_int, [C.c_void_p]),
@@ -79,7 +85,7 @@ _SIGS = {
     "aa_model_n_stages": (C.c_int, [C.c_void_p]),
     "aa_model_stage_info": (C.c_int, [C.c_void_p, C.c_int32, C.c_char_p, C.c_int32,
                                       C.POINTER(C.c_double), C.POINTER(C.c_double)]),
-    "aa_model_set_timing": (C.c_int, [C.c_void_p, C.c_int32]),
+    "aa_model_set_timing": (C.c_int, [C.c_void_p, C.c_uint32]),
     "aa_model_stage_time": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double),
                                       C.POINTER(C.c_int64)]),
     "aa_track_mean": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_void_p,
@@ -128,3 +134,37 @@ def dptr(t) -> int:
     if not t.is_contiguous():
         raise AAError("libaa needs contiguous tensors")
     return int(t.data_ptr())
+
+
+class StageTiming:
+    """Per-launch HIP-event timing of a plan/model handle (aa_fe_stage_* /
+    aa_model_stage_*); subclasses set ``_timing_prefix`` and ``_h``."""
+    _timing_prefix = ""
+
+    def _fn(self, what):
+        return getattr(lib(), f"{self._timing_prefix}_{what}")
+
+    def n_stages(self) -> int:
+        return self._fn("n_stages")(self._h)
+
+    def stage_info(self, i: int):
+        """(name, algorithmic flops per window, algorithmic bytes per window)"""
+        name = C.create_string_buffer(96)
+        fl, by = C.c_double(), C.c_double()
+        check(self._fn("stage_info")(self._h, i, name, 96, C.byref(fl), C.byref(by)),
+              f"{self._timing_prefix}_stage_info")
+        return name.value.decode(), fl.value, by.value
+
+    def set_timing(self, on=True, stages=None) -> None:
+        """Time every stage (``on``) or only the stage indices in ``stages``."""
+        mask = 0
+        if on:
+            mask = 0xFFFFFFFF if stages is None else sum(1 << int(i) for i in stages)
+        check(self._fn("set_timing")(self._h, mask), f"{self._timing_prefix}_set_timing")
+
+    def stage_time(self, i: int):
+        """(total ms, launches) recorded for stage i since the last call"""
+        ms, cnt = C.c_double(), C.c_int64()
+        check(self._fn("stage_time")(self._h, i, C.byref(ms), C.byref(cnt)),
+              f"{self._timing_prefix}_stage_time")
+        return ms.value, cnt.value

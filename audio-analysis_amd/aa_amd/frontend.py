@@ -56,7 +56,9 @@ class FeSettings:
         return float(self.power) if self.htk else 2.0
 
 
-class FrontEnd:
+class FrontEnd(_lib.StageTiming):
+    _timing_prefix = "aa_fe"
+
     def __init__(self, s: FeSettings, device=None):
         self.s = s
         self.device = torch.device(device or "cuda")

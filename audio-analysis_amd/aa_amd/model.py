@@ -109,9 +109,10 @@ def layer_table(arch, tensors):
     return arr, blob
 
 
-class Model:
+class Model(_lib.StageTiming):
     """A loaded network on one device.  ``precision``: "f32" (exact-f32 MFMA,
     the parity mode) or "bf16"."""
+    _timing_prefix = "aa_model"
 
     def __init__(self, model_path, in_shape, precision="bf16", device=None, meta=None):
         self.path = Path(model_path)
@@ -170,26 +171,6 @@ class Model:
 
     def predict(self, x: torch.Tensor) -> torch.Tensor:
         return self.forward(x)[1]
-
-    # ---- per-stage timing (bench.py roofline) ----
-    def n_stages(self) -> int:
-        return _lib.lib().aa_model_n_stages(self._h)
-
-    def stage_info(self, i: int):
-        name = C.create_string_buffer(96)
-        fl, by = C.c_double(), C.c_double()
-        _lib.check(_lib.lib().aa_model_stage_info(self._h, i, name, 96, C.byref(fl), C.byref(by)),
-                   "aa_model_stage_info")
-        return name.value.decode(), fl.value, by.value
-
-    def set_timing(self, on: bool) -> None:
-        _lib.check(_lib.lib().aa_model_set_timing(self._h, int(bool(on))), "aa_model_set_timing")
-
-    def stage_time(self, i: int):
-        ms, cnt = C.c_double(), C.c_int64()
-        _lib.check(_lib.lib().aa_model_stage_time(self._h, i, C.byref(ms), C.byref(cnt)),
-                   "aa_model_stage_time")
-        return ms.value, cnt.value
 
 
 def track_mean(probs: torch.Tensor, win_begin: torch.Tensor, win_count: torch.Tensor,

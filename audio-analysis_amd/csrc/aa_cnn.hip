@@ -708,7 +708,6 @@ struct Stage {
     std::string name;
     int skipped = 0;    // first layer computed inside the next stage
     int fused_first = 0;  // this stage computes the previous (first) layer itself
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
 };
 
 struct Model {
@@ -717,8 +716,7 @@ struct Model {
     int L = 0;
     std::vector<Stage> st;
     size_t act_elems[2] = {0, 0};  // per-window elements of the ping-pong buffers
-    int timing = 0;
-    std::vector<hipEvent_t> ev_pool;  // recycled timing events
+    StageTimer timer;  // HIP events around the stages in timer.mask
 };
 
 
@@ -823,14 +821,10 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
 
 static void free_model(Model* m) {
     if (!m) return;
-    for (hipEvent_t e : m->ev_pool) (void)hipEventDestroy(e);
+    m->timer.release();
     for (auto& s : m->st) {
         (void)hipFree(s.d_w);
         (void)hipFree(s.d_b);
-        for (auto& e : s.ev) {
-            (void)hipEventDestroy(e.first);
-            (void)hipEventDestroy(e.second);
-        }
     }
     delete m;
 }
@@ -1074,25 +1068,14 @@ extern "C" int aa_model_forward(void* model, const float* x, int32_t n, float* l
         if (s.skipped) continue;  // computed inside stage k + 1 (reads x directly)
         void* out = buf[k % 2];
         const Stage* first = s.fused_first ? &m->st[k - 1] : nullptr;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (m->timing) {
-            for (hipEvent_t* e : {&e0, &e1}) {
-                if (!m->ev_pool.empty()) {
-                    *e = m->ev_pool.back();
-                    m->ev_pool.pop_back();
-                } else {
-                    AA_HIP(hipEventCreate(e));
-                }
-            }
-            AA_HIP(hipEventRecord(e0, st));
-        }
-        int rc = (m->prec == AA_PREC_BF16) ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st, first)
-                                           : launch_stage<float>(*m, s, in, out, logits, probs, n, st, first);
+        hipEvent_t e0;
+        int rc = m->timer.begin((int)k, st, &e0);
         if (rc != AA_OK) return rc;
-        if (m->timing) {
-            AA_HIP(hipEventRecord(e1, st));
-            s.ev.emplace_back(e0, e1);
-        }
+        rc = (m->prec == AA_PREC_BF16) ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st, first)
+                                       : launch_stage<float>(*m, s, in, out, logits, probs, n, st, first);
+        if (rc != AA_OK) return rc;
+        rc = m->timer.end((int)k, st, e0);
+        if (rc != AA_OK) return rc;
         in = out;
     }
     return AA_OK;
@@ -1113,30 +1096,17 @@ extern "C" int aa_model_stage_info(const void* model, int32_t stage, char* name,
     return AA_OK;
 }
 
-extern "C" int aa_model_set_timing(void* model, int32_t enable) {
+extern "C" int aa_model_set_timing(void* model, uint32_t stage_mask) {
     Model* m = static_cast<Model*>(model);
     AA_CHECK(m, AA_ERR_INVALID, "aa_model_set_timing: null model");
-    m->timing = enable;
+    m->timer.mask = stage_mask;
     return AA_OK;
 }
 
 extern "C" int aa_model_stage_time(void* model, int32_t stage, double* total_ms, int64_t* count) {
     Model* m = static_cast<Model*>(model);
     AA_CHECK(m && stage >= 0 && stage < (int)m->st.size(), AA_ERR_INVALID, "aa_model_stage_time: bad stage");
-    Stage& s = m->st[stage];
-    double tot = 0;
-    for (auto& e : s.ev) {
-        AA_HIP(hipEventSynchronize(e.second));
-        float ms = 0;
-        AA_HIP(hipEventElapsedTime(&ms, e.first, e.second));
-        tot += ms;
-        m->ev_pool.push_back(e.first);
-        m->ev_pool.push_back(e.second);
-    }
-    if (total_ms) *total_ms = tot;
-    if (count) *count = (int64_t)s.ev.size();
-    s.ev.clear();
-    return AA_OK;
+    return m->timer.collect(stage, total_ms, count);
 }
 
 extern "C" int aa_track_mean(const float* probs, int32_t n_models, int64_t model_stride, int32_t n_labels,

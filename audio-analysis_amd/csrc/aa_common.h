@@ -6,6 +6,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../../include/aa.h"
 
@@ -43,6 +45,71 @@ void set_error(const char* fmt, ...);
     } while (0)
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// HIP-event timing of selected launches (bench.py's roofline): a pair of
+// events on the launch stream around each timed launch, recycled through a
+// pool.  Only the stages named in `mask` are timed, so an untimed launch
+// sequence carries no event records between its kernels.
+struct StageTimer {
+    uint32_t mask = 0;
+    std::vector<hipEvent_t> pool;
+    std::vector<std::vector<std::pair<hipEvent_t, hipEvent_t>>> ev;  // per stage
+
+    bool on(int s) const { return s < 32 && (mask >> s) & 1u; }
+    int begin(int s, hipStream_t st, hipEvent_t* e0) {
+        *e0 = nullptr;
+        if (!on(s)) return AA_OK;
+        AA_HIP(take(e0));
+        AA_HIP(hipEventRecord(*e0, st));
+        return AA_OK;
+    }
+    int end(int s, hipStream_t st, hipEvent_t e0) {
+        if (!e0) return AA_OK;
+        hipEvent_t e1;
+        AA_HIP(take(&e1));
+        AA_HIP(hipEventRecord(e1, st));
+        if ((int)ev.size() <= s) ev.resize(s + 1);
+        ev[s].emplace_back(e0, e1);
+        return AA_OK;
+    }
+    // sum and count of the recorded launches of stage s; clears them
+    int collect(int s, double* total_ms, int64_t* count) {
+        double tot = 0;
+        int64_t n = 0;
+        if (s < (int)ev.size()) {
+            for (auto& e : ev[s]) {
+                AA_HIP(hipEventSynchronize(e.second));
+                float ms = 0;
+                AA_HIP(hipEventElapsedTime(&ms, e.first, e.second));
+                tot += ms;
+                ++n;
+                pool.push_back(e.first);
+                pool.push_back(e.second);
+            }
+            ev[s].clear();
+        }
+        if (total_ms) *total_ms = tot;
+        if (count) *count = n;
+        return AA_OK;
+    }
+    void release() {
+        for (auto& v : ev)
+            for (auto& e : v) pool.push_back(e.first), pool.push_back(e.second);
+        ev.clear();
+        for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+        pool.clear();
+    }
+
+  private:
+    hipError_t take(hipEvent_t* e) {
+        if (!pool.empty()) {
+            *e = pool.back();
+            pool.pop_back();
+            return hipSuccess;
+        }
+        return hipEventCreate(e);
+    }
+};
 
 // ---- device helpers -------------------------------------------------------
 __device__ __forceinline__ float wave_max(float v) {

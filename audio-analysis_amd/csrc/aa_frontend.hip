@@ -41,7 +41,10 @@ struct FePlan {
     float* d_vals = nullptr;  // CSR values
     char* d_cimg = nullptr;   // fe_stft_mel_4096 block constants (W4096^k | rows | values), 1-KiB padded
     int cimg_bytes = 0;
+    StageTimer timer;         // HIP events around the launches in timer.mask
 };
+
+enum { FE_STAGE_STATS = 0, FE_STAGE_STFT = 1, FE_STAGE_DB = 2, FE_N_STAGES = 3 };
 
 // ---------------------------------------------------------------------------
 // fe_stats: min / max / non-finite over each virtual window (zeros outside the
@@ -525,7 +528,13 @@ __global__ __launch_bounds__(256) void fe_stft_mel_4096(
 
     const int k1 = lane >> 1, h = lane & 1;
     {
-        const int item = blockIdx.x;
+        // XCD-aware item order: block b runs on XCD b % 8, so XCD x takes the
+        // contiguous item range [x q + min(x, r), ...) (q, r = n_items / 8, % 8).
+        // Consecutive frame groups of a window overlap by 4096 - 4 hop samples
+        // and write the same 128-B lines of melS; keeping them on one XCD lets
+        // its L2 serve the overlap and merge the partial-line stores.
+        const int xcd = blockIdx.x & 7, q = n_items >> 3, r = n_items & 7;
+        const int item = xcd * q + min(xcd, r) + (blockIdx.x >> 3);
         const int w = item / ngrp;
         const int g = item - w * ngrp;
         const int f0 = g * kFpg;
@@ -946,6 +955,7 @@ extern "C" int aa_fe_destroy(void* plan) {
     (void)hipFree(p->d_rows);
     (void)hipFree(p->d_vals);
     (void)hipFree(p->d_cimg);
+    p->timer.release();
     delete p;
     return AA_OK;
 }
@@ -971,11 +981,15 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
     AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE,
              "aa_fe_run: workspace %zu < %zu bytes", workspace_bytes, ws.bytes);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    hipEvent_t e0;
+    int rc = p->timer.begin(FE_STAGE_STATS, st, &e0);
+    if (rc != AA_OK) return rc;
     hipLaunchKernelGGL(fe_stats, dim3(kStatSplit, n_win), dim3(256), 0, st, pcm, windows,
                        p->cfg.win_len, ws.stats);
     AA_LAUNCH_CHECK();
+    if ((rc = p->timer.end(FE_STAGE_STATS, st, e0)) != AA_OK) return rc;
+    if ((rc = p->timer.begin(FE_STAGE_STFT, st, &e0)) != AA_OK) return rc;
     const int pm = p->cfg.power == 2.f ? PM_SQUARE : p->cfg.power == 1.f ? PM_ABS : PM_GENERAL;
-    int rc;
 #define AA_FE_PM(PM)                                                                                    \
     if (fe_fast4096(*p)) {                                                                              \
         rc = launch_stft4096<PM>(*p, pcm, windows, n_win, ws.stats, ws.melS, ws.blkmax, st);            \
@@ -989,10 +1003,53 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
     else { AA_FE_PM(PM_GENERAL) }
 #undef AA_FE_PM
     if (rc != AA_OK) return rc;
+    if ((rc = p->timer.end(FE_STAGE_STFT, st, e0)) != AA_OK) return rc;
+    if ((rc = p->timer.begin(FE_STAGE_DB, st, &e0)) != AA_OK) return rc;
     hipLaunchKernelGGL(fe_db, dim3((p->cfg.n_mels + 3) / 4, n_win), dim3(256), 0, st, ws.melS,
                        ws.blkmax, ws.stats, p->nfblk, p->cfg.n_mels, p->T, p->cfg.db_scale,
                        p->cfg.amin, p->cfg.top_db, p->cfg.mean_sub, p->cfg.channels,
                        p->cfg.normalize, out, win_status);
     AA_LAUNCH_CHECK();
+    return p->timer.end(FE_STAGE_DB, st, e0);
+}
+
+extern "C" int aa_fe_n_stages(const void* plan) { return plan ? FE_N_STAGES : -1; }
+
+// Algorithmic work of one window through each launch:
+//   stft_mel flops = T (2.5 N log2 N + N + 3 (N/2 + 1) + 2 nnz) + 5 L
+//   (real FFT as an N/2 complex FFT + split, window, |.|^p, mel rows; the
+//   normalisation pass), bytes = L f32 PCM in + n_mels T f32 mel power out.
+extern "C" int aa_fe_stage_info(const void* plan, int32_t stage, char* name, int32_t name_len,
+                                double* flops_per_item, double* bytes_per_item) {
+    const FePlan* p = static_cast<const FePlan*>(plan);
+    AA_CHECK(p && stage >= 0 && stage < FE_N_STAGES, AA_ERR_INVALID, "aa_fe_stage_info: bad stage");
+    const double N = p->cfg.n_fft, L = p->cfg.win_len, T = p->T, M = p->cfg.n_mels;
+    double fl = 0, by = 0;
+    const char* nm = "";
+    switch (stage) {
+        case FE_STAGE_STATS: nm = "fe_stats"; fl = 2 * L; by = 4 * L; break;
+        case FE_STAGE_STFT:
+            nm = fe_fast4096(*p) ? "fe_stft_mel_4096" : "fe_stft_mel";
+            fl = T * (2.5 * N * std::log2(N) + N + 3 * (N / 2 + 1) + 2.0 * p->nnz) + 5 * L;
+            by = 4 * L + 4 * M * T;
+            break;
+        default: nm = "fe_db"; fl = 3 * M * T; by = 4 * M * T * (1 + p->cfg.channels); break;
+    }
+    if (name && name_len > 0) snprintf(name, name_len, "%s", nm);
+    if (flops_per_item) *flops_per_item = fl;
+    if (bytes_per_item) *bytes_per_item = by;
     return AA_OK;
+}
+
+extern "C" int aa_fe_set_timing(void* plan, uint32_t stage_mask) {
+    FePlan* p = static_cast<FePlan*>(plan);
+    AA_CHECK(p, AA_ERR_INVALID, "aa_fe_set_timing: null plan");
+    p->timer.mask = stage_mask;
+    return AA_OK;
+}
+
+extern "C" int aa_fe_stage_time(void* plan, int32_t stage, double* total_ms, int64_t* count) {
+    FePlan* p = static_cast<FePlan*>(plan);
+    AA_CHECK(p && stage >= 0 && stage < FE_N_STAGES, AA_ERR_INVALID, "aa_fe_stage_time: bad stage");
+    return p->timer.collect(stage, total_ms, count);
 }

@@ -36,8 +36,11 @@ METRIC = "audio-seconds classified/sec/GPU on 60 s mono; max|delta logit| vs CPU
 WINDOWS_PER_CLIP = 39
 SECONDS_PER_WINDOW = 60.0 / WINDOWS_PER_CLIP
 BATCH_A, BATCH_B = 39, 25
-PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md
+PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s, MI355X_MICROARCH.md
+VALU_F32_PEAK = 157.3                   # FP32 VALU TFLOP/s (fma counted as 2)
 HBM_PEAK_GBS = 8000.0
+WORKLOAD = ("config2: 64 windows/step (39 of clip A + 25 of clip B, 60 s 48 kHz mono), "
+            "htk log-mel n_fft 4096 hop 640 160 mel + model1 CNN")
 
 
 def parse():
@@ -72,13 +75,16 @@ def make_batch(rank, fe_settings):
 
 def cpu_baseline(pcm, views, model_path, fe_cfg, budget_s):
     """Oracle (numpy librosa-0.11 restatement + torch-CPU fp32 CNN) on a bounded
-    sample of the same windows; returns (audio-s/s, windows, seconds, logits)."""
+    sample of the same windows: passes over the step's windows, 8 at a time,
+    until ``budget_s`` seconds of CPU work are done.  Returns (audio-s/s,
+    windows, seconds, threads, logits of the step's first windows)."""
     from oracle import cnn_oracle, fe_oracle
     threads = torch.get_num_threads()
-    done, t0 = [], time.perf_counter()
+    t0 = time.perf_counter()
     logits = []
-    i = 0
-    while i < len(views) and (time.perf_counter() - t0) < budget_s:
+    done = 0
+    while done == 0 or (time.perf_counter() - t0) < budget_s:
+        i = done % len(views)
         chunk = views[i:i + 8]
         mels = []
         for (s, n, p) in chunk:
@@ -86,11 +92,26 @@ def cpu_baseline(pcm, views, model_path, fe_cfg, budget_s):
             w[p:p + n] = pcm[s:s + n]
             mels.append(fe_oracle.window_logmel(w, fe_cfg))
         lg, _ = cnn_oracle.forward(model_path, np.stack(mels))
-        logits.append(lg)
-        done.extend(chunk)
-        i += len(chunk)
+        if done < len(views):
+            logits.append(lg)
+        done += len(chunk)
     dt = time.perf_counter() - t0
-    return len(done) * SECONDS_PER_WINDOW / dt, len(done), dt, threads, np.concatenate(logits)
+    return done * SECONDS_PER_WINDOW / dt, done, dt, threads, np.concatenate(logits)
+
+
+def load_traffic(n_dispatch):
+    """HBM bytes per launch of each kernel of one step, in dispatch order, from
+    the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE summary of this same
+    workload (tools/pmc_traffic.py; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md).  None when no summary of this workload exists."""
+    for path in sorted((ROOT / "profiles").glob("*/pmc_traffic.json"), reverse=True):
+        try:
+            d = json.loads(path.read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == WORKLOAD and len(d.get("kernels", [])) == n_dispatch:
+            return d, path.relative_to(ROOT).as_posix()
+    return None, None
 
 
 def main():
@@ -135,7 +156,7 @@ def main():
     fe_ws = [torch.empty(max(fe.workspace_bytes(b - a), 256), dtype=torch.uint8, device=dev) for a, b in chunks]
     m_ws = [torch.empty(max(model.workspace_bytes(b - a), 256), dtype=torch.uint8, device=dev) for a, b in chunks]
 
-    def run_chunks(fe_events=None):
+    def run_chunks():
         if S > 1:
             ev = torch.cuda.Event()
             ev.record(stream)
@@ -143,15 +164,7 @@ def main():
             s = streams[k]
             if S > 1:
                 s.wait_event(ev)
-            e0 = e1 = None
-            if fe_events is not None and k == 0:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(s)
             fe.run(pcm, rows[a:b], out=logmel[a:b], stream=s, workspace=fe_ws[k])
-            if e0 is not None:
-                e1.record(s)
-                fe_events.append((e0, e1, b - a))
             model.forward(logmel[a:b], logits[a:b], probs[a:b], stream=s, workspace=m_ws[k])
         if S > 1:
             for s in streams:
@@ -160,28 +173,48 @@ def main():
                 stream.wait_event(done)
         track_mean(probs[None], wb, wc, out=tmean, stream=stream)
 
-    def step():
-        run_chunks()
+    # every launch of a step, in dispatch order: (owner, stage index)
+    launches = [(fe, i) for i in range(fe.n_stages())] + [(model, i) for i in range(model.n_stages())]
+
+    def collect(owner_stages):
+        out = []
+        for owner, i in owner_stages:
+            name, flops, byts = owner.stage_info(i)
+            ms, cnt = owner.stage_time(i)
+            per = n_win / S  # a launch covers one chunk of the step's windows
+            out.append(dict(owner=owner, idx=i, name=name, flops=flops * per, bytes=byts * per,
+                            avg_ms=ms / max(cnt, 1), count=cnt))
+        return out
 
     for _ in range(args.warmup):
-        step()
+        run_chunks()
     torch.cuda.synchronize()
-    # drop warmup timings, then time exactly K steps with per-stage events on
+    # calibration (untimed): every launch bracketed by events, to find the
+    # dominant kernel; the timed region then carries events around that one only
+    fe.set_timing(True)
     model.set_timing(True)
-    for i in range(model.n_stages()):
-        model.stage_time(i)
-    fe_ev = []
+    for _ in range(5):
+        run_chunks()
+    torch.cuda.synchronize()
+    calib = [c for c in collect(launches) if c["count"] > 0]  # a fused stage launches nothing
+    launches = [(c["owner"], c["idx"]) for c in calib]
+    fe.set_timing(False)
+    model.set_timing(False)
+    dom = max(calib, key=lambda x: x["avg_ms"])
+    dom["owner"].set_timing(True, stages=[dom["idx"]])
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        run_chunks(fe_ev)
+        run_chunks()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    model.set_timing(False)
+    dom_live = collect([(dom["owner"], dom["idx"])])[0]
+    dom["owner"].set_timing(False)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -193,23 +226,36 @@ def main():
         assert gathered.shape[0] == 2 * world
     elapsed = float(t.item())
 
-    stages = []
-    for i in range(model.n_stages()):
-        name, flops, byts = model.stage_info(i)
-        ms, cnt = model.stage_time(i)
-        # per launch: a launch covers one chunk of the step's windows
-        per = n_win / S
-        stages.append(dict(name=name, flops=flops * per, bytes=byts * per,
-                           avg_ms=ms / max(cnt, 1), count=cnt))
-    fe_ms = sum(a.elapsed_time(b) for a, b, _ in fe_ev) / max(len(fe_ev), 1)
-    dom = max(stages, key=lambda s: s["avg_ms"])
-    achieved = dom["flops"] / (dom["avg_ms"] * 1e-3) / 1e12
-    roofline = {"bound": "mfma", "kernel": dom["name"], "achieved": round(achieved, 2),
-                "peak": PEAK[args.precision], "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK[args.precision], 4), "traffic": None,
-                "avg_ms": round(dom["avg_ms"], 4),
-                "stages_ms": {s["name"]: round(s["avg_ms"], 4) for s in stages},
-                "frontend_ms": round(fe_ms, 4)}
+    is_fe = dom["owner"] is fe
+    if is_fe and dom["name"].startswith("fe_stft"):
+        bound, peak, unit = "valu", VALU_F32_PEAK, "TFLOP/s"
+    elif is_fe:
+        bound, peak, unit = "hbm", HBM_PEAK_GBS, "GB/s"
+    else:
+        bound, peak, unit = "mfma", PEAK[args.precision], "TFLOP/s"
+    avg_s = dom_live["avg_ms"] * 1e-3
+    achieved = (dom["bytes"] / avg_s / 1e9) if unit == "GB/s" else (dom["flops"] / avg_s / 1e12)
+    traffic, traffic_src = None, None
+    tr, tr_path = load_traffic(len(launches) + 1) if S == 1 else (None, None)  # + track_mean
+    if tr is not None:
+        k = tr["kernels"][launches.index((dom["owner"], dom["idx"]))]
+        traffic = k["hbm_bytes"]
+        traffic_src = tr_path
+    roofline = {"bound": bound, "kernel": dom["name"], "achieved": round(achieved, 2), "peak": peak,
+                "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic,
+                "algorithmic_bytes": round(dom["bytes"]),
+                "avg_ms": round(dom_live["avg_ms"], 4), "launches_timed": dom_live["count"],
+                "traffic_source": traffic_src,
+                "stages_ms": {c["name"]: round(c["avg_ms"], 4) for c in calib}}
+    # the CNN's dominant MFMA kernel, reported beside the overall dominant one
+    convs = [c for c in calib if c["owner"] is model]
+    if convs and is_fe:
+        cd = max(convs, key=lambda x: x["avg_ms"])
+        a = cd["flops"] / (cd["avg_ms"] * 1e-3) / 1e12
+        roofline["mfma_kernel"] = {"kernel": cd["name"], "achieved": round(a, 2),
+                                   "peak": PEAK[args.precision], "unit": "TFLOP/s",
+                                   "frac": round(a / PEAK[args.precision], 4),
+                                   "avg_ms": round(cd["avg_ms"], 4), "timed": "calibration pass"}
 
     audio_s = world * args.steps * n_win * SECONDS_PER_WINDOW
     value = audio_s / elapsed
@@ -219,8 +265,7 @@ def main():
         "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
         "data": "synthetic (48 kHz int16-quantised noise+chirps, seeded), seeded random-init model1",
-        "config": {"workload": "config2: 64 windows/step (39 of clip A + 25 of clip B, 60 s "
-                               "48 kHz mono), htk log-mel n_fft 4096 hop 640 160 mel + model1 CNN",
+        "config": {"workload": WORKLOAD,
                    "model": "model1", "global_batch": n_win * world, "seq_len": fe_s.win_len,
                    "parallelism": f"dp{world}", "streams": S},
         "roofline": roofline,
@@ -232,10 +277,10 @@ def main():
         v, nw, dt, thr, ref_logits = cpu_baseline(pcm_np, views, model_path, fe_cfg, args.cpu_seconds)
         out["cpu_baseline"] = {"value": round(v, 2), "unit": "audio-s/s", "cores": thr,
                                "kind": "port",
-                               "sample": f"{nw} of the step's 64 windows (oracle numpy FE + "
+                               "sample": f"{nw} windows (the step's 64, cycled; oracle numpy FE + "
                                          f"torch-CPU fp32 model1), {dt:.1f} s"}
         if not args.no_parity:
-            g = logits[:nw].cpu().numpy()
+            g = logits[:ref_logits.shape[0]].cpu().numpy()
             out["max_abs_dlogit"] = {args.precision: float(np.abs(g - ref_logits).max())}
     if rank == 0:
         print(json.dumps(out))

@@ -90,6 +90,13 @@ size_t aa_fe_workspace_bytes(const void* plan, int32_t max_windows);
 int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa_window* windows,
               int32_t n_win, float* out, int32_t* win_status, void* workspace,
               size_t workspace_bytes, void* stream);
+/* Launch stages of aa_fe_run (0 fe_stats, 1 fe_stft_mel, 2 fe_db) and their
+ * timing, same contract as aa_model_stage_* below. */
+int aa_fe_n_stages(const void* plan);
+int aa_fe_stage_info(const void* plan, int32_t stage, char* name, int32_t name_len,
+                     double* flops_per_item, double* bytes_per_item);
+int aa_fe_set_timing(void* plan, uint32_t stage_mask);
+int aa_fe_stage_time(void* plan, int32_t stage, double* total_ms, int64_t* count);
 
 /* ---------------- CNN: log-mel windows -> logits / probabilities ---------------- */
 typedef enum aa_op {
@@ -131,13 +138,14 @@ size_t aa_model_workspace_bytes(const void* model, int32_t max_batch);
 int aa_model_forward(void* model, const float* x, int32_t n, float* logits, float* probs,
                      void* workspace, size_t workspace_bytes, void* stream);
 
-/* Per-stage timing of aa_model_forward (HIP events around each fused stage,
- * on the launch stream).  Used by bench.py for the roofline of the dominant
- * kernel. */
+/* Per-stage timing of aa_model_forward (HIP events around each stage whose
+ * bit is set in stage_mask, on the launch stream; 0 disables).  Used by
+ * bench.py for the roofline of the dominant kernel.  stage_info reports the
+ * algorithmic flops / HBM bytes of one window (item) through the stage. */
 int aa_model_n_stages(const void* model);
 int aa_model_stage_info(const void* model, int32_t stage, char* name, int32_t name_len,
                         double* flops_per_item, double* bytes_per_item);
-int aa_model_set_timing(void* model, int32_t enable);
+int aa_model_set_timing(void* model, uint32_t stage_mask);
 int aa_model_stage_time(void* model, int32_t stage, double* total_ms, int64_t* count);
 
 /* ---------------- ensemble + window mean ---------------- */
