@@ -14,6 +14,10 @@ INCLUDE = PKG.parent.parent / "include"
 LIB = PKG / "libaa.so"
 SOURCES = ["aa_api.cpp", "aa_frontend.hip", "aa_cnn.hip", "aa_scan.hip"]
 ARCH = os.environ.get("AA_OFFLOAD_ARCH", "gfx950")
+# per-source flags: the FFT front end is written in scalar f32; SLP packing it
+# into v_pk_* ops needs paired SGPR constants and register shuffles that push
+# the wave-per-frame kernel past its 128-VGPR budget (spills)
+EXTRA_FLAGS = {"aa_frontend.hip": ["-fno-slp-vectorize"]}
 
 
 def hipcc() -> str:
@@ -42,7 +46,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
 
     def compile_one(src: str) -> Path:
         obj = objdir / (src.rsplit(".", 1)[0] + ".o")
-        cmd = [cc, *flags, "-c", str(CSRC / src), "-o", str(obj)]
+        cmd = [cc, *flags, *EXTRA_FLAGS.get(src, []), "-c", str(CSRC / src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -39,7 +39,7 @@ struct FePlan {
     float2* d_tw2 = nullptr;  // exp(-2 pi i k / n_fft), k <= Nc
     int4* d_rows = nullptr;   // per band: (first bin, count, value offset, 0)
     float* d_vals = nullptr;  // CSR values
-    char* d_cimg = nullptr;   // fe_stft_mel_4096 block constants (W4096^k | rows | values), 1-KiB padded
+    char* d_cimg = nullptr;   // fe_stft_mel_4096 CSR image (rows | values), 1-KiB padded
     int cimg_bytes = 0;
     StageTimer timer;         // HIP events around the launches in timer.mask
 };
@@ -222,15 +222,19 @@ __device__ __forceinline__ float normalize_sample(float x, float lo, float scale
     return __fmul_rn(y, 2.0f);
 }
 
-// complex64 -> np.abs (hypot) -> ** power.  The power mode is a template
-// parameter: a runtime select between the three forms would make every bin
-// pay for the inlined powf.
+// complex64 -> np.abs -> ** power.  The power mode is a template parameter:
+// a runtime select between the three forms would make every bin pay for the
+// inlined powf.  |X|^2 is formed directly (the reference squares a rounded
+// hypot: the two differ by an ulp, far inside the f32-FFT tolerance), and the
+// other modes use the hardware square root (v_sqrt_f32, 1 ulp) rather than the
+// correctly rounded expansion.
 enum { PM_GENERAL = 0, PM_ABS = 1, PM_SQUARE = 2 };
 template <int PM>
 __device__ __forceinline__ float pow_mag(float re, float im, float power) {
-    const float mag = sqrtf(re * re + im * im);
-    if constexpr (PM == PM_SQUARE) return mag * mag;
-    else if constexpr (PM == PM_ABS) return mag;
+    const float m2 = fmaf(re, re, im * im);
+    if constexpr (PM == PM_SQUARE) return m2;
+    const float mag = __builtin_amdgcn_sqrtf(m2);
+    if constexpr (PM == PM_ABS) return mag;
     else return powf(mag, power);
 }
 
@@ -407,9 +411,9 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
         __syncthreads();  // P / buffers reused by the next frame
     }
     // staged [n_mels][nf] tile -> melS[w][m][f0 .. f0 + nf)
-    for (int idx = tid; idx < n_mels * nf; idx += NT) {
-        const int m = idx / nf, f = idx - (idx / nf) * nf;
-        melS[((size_t)w * n_mels + m) * T + f0 + f] = melT[m * kFpb + f];
+    for (int idx = tid; idx < nf * n_mels; idx += NT) {  // frame-major rows
+        const int f = idx / n_mels, m = idx - f * n_mels;
+        melS[((size_t)w * T + f0 + f) * n_mels + m] = melT[m * kFpb + f];
     }
     // item max -> blkmax[w][fb]
     __shared__ float red[NT / 64];
@@ -424,34 +428,55 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
 }
 
 // ---------------------------------------------------------------------------
-// fe_stft_mel_4096: the n_fft = 4096 path, one WAVE per frame.
+// fe_stft_mel_4096: the n_fft = 4096 path, one WAVE per frame, waves
+// independent of each other (no block-level synchronisation after the
+// prologue).
 //
-// z[n] = x[2n] + i x[2n+1] (2048 complex points), four-step FFT with 64 lanes:
-//   n = c + 64 r (lane c holds r = 0..31 in registers)
+// normalize_data folded into the transform.  It is affine: inside the window
+// y = a (x + beta) with a = 2 / scale, beta = scale (1e-6 - 0.5) - lo
+// (src/identify_tracks.py:203-208), and the centre padding is y = 0.  The
+// transform is linear, so a frame's spectrum is a * FFT(z) with z = x + beta on
+// window samples and 0 on the padding, and |.|^p scales by a^p, applied to the
+// mel sums.  In a frame without centre padding beta * 1 only reaches bin 0 of
+// the unwindowed transform, i.e. bins -1..1 after the Hann convolution (step
+// 7), so interior frames take z = x outright (the host keeps kmin >= 2); edge
+// frames add beta and zero their padding.  The reference rounds y to f32
+// before its f64 STFT; the two agree to f32 rounding (parity tolerance).
+//
+// z[n] = x[2n] + i x[2n+1] (2048 complex points) is loaded straight into
+// registers: lane c holds n = c + 64 r, r = 0..31 (samples 2c + 128 r and +1),
+// through a buffer resource spanning the window's view [src, src + n_valid),
+// so np.pad zeros, centre padding and the ends of the recording all read as 0
+// by the hardware range check (a negative offset wraps past num_records).
 //   1. DFT-32 over r in registers                   -> Y[k1][c]
-//   2. Y[k1][c] *= W2048^(c k1)                     (per-lane register twiddles)
-//   3. transpose through a per-wave LDS buffer (two half passes, rows padded
-//      to 66 float2 so both the row writes and the strided reads are
+//   2. Y[k1][c] *= W2048^(c k1)                     (ladder from two table entries)
+//   3. transpose through the wave's LDS buffer (two half passes, rows padded
+//      to 66 float2 so the row writes and the strided reads are
 //      conflict-free): lane L = 2 k1 + h gets Y[k1][h + 2m], m = 0..31
 //   4. DFT-32 over m in registers -> E_h[k2']
 //   5. radix-2 across the lane pair (DPP quad_perm swap):
 //      Z[k1 + 32 k2'] = E0 + W64^k2' E1, Z[k1 + 32 (k2' + 32)] = E0 - W64^k2' E1
-//   6. real split X[k] = E + W4096^k O from Z[k], conj Z[2048 - k]
+//   6. real split X[k] = E + W4096^k O from Z[k], conj Z[2048 - k], with
+//      W4096^(k1 + 32 j) = W4096^k1 W128^j (one table entry per lane)
 //   7. periodic Hann applied in frequency: Xw[k] = X[k]/2 - (X[k-1] + X[k+1])/4,
 //      |Xw|^power into LDS
-//   8. sparse mel rows (CSR in LDS) -> block staging tile -> melS
-// Block = 4 waves = 4 consecutive frames of one window sharing one normalised
-// PCM segment; 2 blocks per CU.  Only wave-level synchronisation inside a frame.
+//   8. sparse mel rows (CSR in LDS, shared by the block), times a^p ->
+//      melF[w][t][:] (frame-major: one contiguous row per frame) and the frame
+//      maximum -> pmax[w][t]
+// Block = 8 waves sharing one CSR image, 2 blocks per CU (16 waves: VGPRs
+// capped at 128).  Wave g of G takes frames g, g + G, ...; blocks are
+// renumbered so each XCD (block b runs on XCD b % 8) owns a contiguous range of
+// frames: neighbouring frames overlap by 4096 - hop samples and one L2 then
+// serves the overlap.
 // ---------------------------------------------------------------------------
 #include "aa_twiddles.h"
 
-constexpr int kFpg = 4;                 // frames (waves) per block
+#ifndef AA_FE_WPB
+#define AA_FE_WPB 8
+#endif
+constexpr int kWpb = AA_FE_WPB;         // waves per block (2 blocks per CU)
 constexpr int kRow = 66;                // padded transpose row (float2)
 constexpr int kHalf = 16 * kRow;        // per-wave buffer (float2)
-constexpr int kCimgRows = 1026 * 8;     // byte offset of the CSR rows in the constant image
-
-// PCM segment of one block, rounded to whole 64-sample global_load_lds rows
-__host__ __device__ constexpr int fe4096_seg_cap(int hop) { return ((kFpg - 1) * hop + 4096 + 63) & ~63; }
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -461,6 +486,7 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ float2 wconst32(int k) { return make_float2(kW32[k][0], kW32[k][1]); }
 __device__ __forceinline__ float2 wconst64(int k) { return make_float2(kW64[k][0], kW64[k][1]); }
+__device__ __forceinline__ float2 wconst128(int k) { return make_float2(kW128[k][0], kW128[k][1]); }
 
 // 32-point DFT in registers, in place: 4 interleaved DFT-8s, twiddles, DFT-4s.
 // Output X[k] is left in v[dperm(k)], dperm(k) = 4 (k % 8) + k / 8 (a
@@ -488,255 +514,295 @@ __device__ __forceinline__ float swap_pair(float x) {  // value of lane ^ 1
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
 }
 
-// DIAG (tools/fe_bench.hip only): 1 skip the global->LDS staging, 2 the
-// normalisation pass, 4 the FFT (steps 1-5), 8 the real split, 16 Hann and
-// power, 32 the mel rows, 64 the output stores.
+__device__ __forceinline__ float load_view(__amdgpu_buffer_rsrc_t rs, int i) {  // 0 outside the view
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, i * 4, 0, 0));
+}
+
+// DIAG (tools/fe_bench.hip only): 1 skip the PCM loads, 4 the FFT (steps 1-5),
+// 8 the real split, 16 Hann and power, 32 the mel rows, 64 the output stores.
 template <int PM, int DIAG = 0>
-__global__ __launch_bounds__(256) void fe_stft_mel_4096(
+__global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb / 2, kWpb / 2))) void fe_stft_mel_4096(
     const float* __restrict__ pcm, const aa_window* __restrict__ wins, const float4* __restrict__ stats,
-    const float2* __restrict__ tw, const char* __restrict__ cimg, int cimg_bytes, int win_len, int hop, int T,
-    int n_mels, int kmin, int kmax, int normalize, float power, int ngrp, int n_items, float* __restrict__ melS,
-    float* __restrict__ blkmax) {
+    const float2* __restrict__ tw, const float2* __restrict__ tw4096, const char* __restrict__ cimg,
+    int cimg_bytes, int win_len, int hop, int T, int n_mels, int kmin, int kmax, int normalize, float power,
+    int n_frames, float* __restrict__ melF, float* __restrict__ pmax) {
     constexpr int NC = 2048;
     extern __shared__ float lds[];
     const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
-    const int seg_cap = fe4096_seg_cap(hop);
-    float* seg = lds;
-    float2* wb = reinterpret_cast<float2*>(seg + seg_cap) + wave * kHalf;  // this wave's buffer
-    // block constants, one contiguous image (fe4096_cimg): W4096^k | CSR rows | CSR values
-    char* cl = reinterpret_cast<char*>(reinterpret_cast<float2*>(seg + seg_cap) + kFpg * kHalf);
-    const float2* stw2 = reinterpret_cast<const float2*>(cl);
-    const int4* srows = reinterpret_cast<const int4*>(cl + kCimgRows);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    char* cl = reinterpret_cast<char*>(lds);
+    const int4* srows = reinterpret_cast<const int4*>(cl);  // CSR image (fe_cimg4096): rows | values
     const float* svals = reinterpret_cast<const float*>(srows + n_mels);
-    float* melT = reinterpret_cast<float*>(cl + cimg_bytes);  // [n_mels][kFpg]
+    float2* wb = reinterpret_cast<float2*>(cl + cimg_bytes) + wave * kHalf;  // this wave's buffer
 
-    // ---- block prologue: every global read is issued before the first wait.
-    // The constant image and the overlapped PCM segment go global -> LDS by
-    // global_load_lds (no registers, no per-iteration waits); the window
-    // descriptor is the only dependent round trip. ----
-    for (int g = wave; g < ((DIAG & 1) ? 0 : cimg_bytes / 1024); g += kFpg)
+    for (int g = wave; g < cimg_bytes / 1024; g += kWpb)
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(cimg + g * 1024 + lane * 16),
                                          (__attribute__((address_space(3))) void*)(cl + g * 1024), 16, 0, 0);
-    // step-2 twiddles W2048^(c k1) = (W^8c)^(k1/8) (W^c)^(k1%8): two short power
-    // ladders from two table entries (<= 4 roundings per twiddle)
-    float2 p1[8], p8[4];
-    p1[0] = make_float2(1.f, 0.f);
-    p1[1] = tw[lane];
-    p8[0] = make_float2(1.f, 0.f);
-    p8[1] = tw[(8 * lane) & (NC - 1)];
-
     const int k1 = lane >> 1, h = lane & 1;
-    {
-        // XCD-aware item order: block b runs on XCD b % 8, so XCD x takes the
-        // contiguous item range [x q + min(x, r), ...) (q, r = n_items / 8, % 8).
-        // Consecutive frame groups of a window overlap by 4096 - 4 hop samples
-        // and write the same 128-B lines of melS; keeping them on one XCD lets
-        // its L2 serve the overlap and merge the partial-line stores.
-        const int xcd = blockIdx.x & 7, q = n_items >> 3, r = n_items & 7;
-        const int item = xcd * q + min(xcd, r) + (blockIdx.x >> 3);
-        const int w = item / ngrp;
-        const int g = item - w * ngrp;
-        const int f0 = g * kFpg;
-        const int nf = min(kFpg, T - f0);
-        const int seg_len = (nf - 1) * hop + 4096;
+    float2 t1 = tw[lane];                // W2048^c
+    float2 t8 = tw[(8 * lane) & (NC - 1)];  // W2048^(8c)
+    const float2 wk1 = tw4096[k1];       // W4096^k1
+    // (cos, sin) of 2 pi n / 4096 at the lane's first even / odd sample n = 2c, 2c + 1
+    const float2 te = tw4096[2 * lane], to = tw4096[2 * lane + 1];
+    const float2 hwe = make_float2(te.x, -te.y), hwo = make_float2(to.x, -to.y);
+    __syncthreads();                     // vmcnt(0): the CSR image has landed
+
+    const int nb = gridDim.x;  // a multiple of 8 (host)
+    const int blk = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
+    const int G = nb * kWpb;
+    for (int fi = blk * kWpb + wave; fi < n_frames; fi += G) {
+        const int w = fi / T;
+        const int t = fi - w * T;
         const aa_window d = wins[w];
-        const int base = f0 * hop - 2048;
-        const long long safe = d.n_valid > 0 ? d.src : 0;
-        // raw segment: lane q of wave-instruction gg loads sample base + q (a
-        // clamped in-bounds address where the window has no sample; the
-        // normalisation pass below rewrites those)
-        for (int gg = wave; gg * 64 < ((DIAG & 1) ? 0 : seg_len); gg += kFpg) {
-            const int q = gg * 64 + lane;
-            const int i = base + q;
-            const int rel = i - d.pad_left;
-            const bool ok = q < seg_len && i >= 0 && i < win_len && rel >= 0 && rel < d.n_valid;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(pcm + (ok ? d.src + rel : safe)),
-                                             (__attribute__((address_space(3))) void*)(seg + gg * 64), 4, 0, 0);
-        }
-        float lo = INFINITY, hi = -INFINITY;
+        float apow = 1.f, beta = 0.f;
+        if (normalize) {
+            float lo = INFINITY, hi = -INFINITY;
 #pragma unroll
-        for (int s = 0; s < kStatSplit; ++s) {
-            const float4 st = stats[w * kStatSplit + s];
-            lo = fminf(lo, st.x);
-            hi = fmaxf(hi, st.y);
+            for (int s = 0; s < kStatSplit; ++s) {
+                const float4 st = stats[w * kStatSplit + s];
+                lo = fminf(lo, st.x);
+                hi = fmaxf(hi, st.y);
+            }
+            const float scale = __fsub_rn(hi, lo);  // == max(x - min) (monotone rounding)
+            const float a = __fdiv_rn(2.f, scale);
+            apow = PM == PM_SQUARE ? a * a : PM == PM_ABS ? a : powf(a, power);
+            beta = fmaf(scale, 0.000001f - 0.5f, -lo);
         }
-        const float scale = __fsub_rn(hi, lo);
-        const float inv = __fdiv_rn(1.f, scale);
-#pragma unroll
-        for (int i = 2; i < 8; ++i) p1[i] = cmul(p1[i - 1], p1[1]);
-        p8[2] = cmul(p8[1], p8[1]);
-        p8[3] = cmul(p8[2], p8[1]);
-        __syncthreads();  // vmcnt(0): segment and constants have landed
-        // ---- normalise in place (np.pad zeros, centre padding stays 0) ----
+        const int i0 = t * hop - 2048;  // window index of the frame's first sample
+        // per-lane sample index, opaque to the optimiser: otherwise it hoists the
+        // 64 loop-invariant load offsets and edge masks out of the frame loop
+        // and spills them
+        int l2 = 2 * lane;
+        __asm__ volatile("" : "+v"(l2));
+        float2 wk = wk1;  // per frame, or W4096^k1 W128^j gets hoisted as 32 live twiddles
+        __asm__ volatile("" : "+v"(wk.x), "+v"(wk.y));
+        float2 u[32];
         {
-            constexpr int U = 8;
-            for (int q0 = 0; q0 < ((DIAG & 2) ? 0 : seg_len); q0 += U * 256) {
-                float v[U];
+            // ---- load (steps 0) ----
+            float2 y[32];
+            if constexpr ((DIAG & 1) != 0) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) v[u] = seg[min(q0 + u * 256 + tid, seg_cap - 1)];
+                for (int r = 0; r < 32; ++r) y[r] = make_float2((float)(lane + r), (float)(t - r));
+            } else {
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)(pcm + d.src), 0, d.n_valid * 4, 0x00020000);
+                // even and odd samples through two address registers: the
+                // backend must not fuse a pair into one 8-byte load, whose range
+                // check would not zero the two samples independently
+                const int offe = i0 - d.pad_left + l2;
+                int offo = offe + 1;
+                __asm__ volatile("" : "+v"(offo));
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int q = q0 + u * 256 + tid;
-                    const int i = base + q;
-                    const int rel = i - d.pad_left;
-                    if (q < seg_len) {
-                        float x = 0.f;
-                        if (i >= 0 && i < win_len) {
-                            x = (rel >= 0 && rel < d.n_valid) ? v[u] : 0.f;
-                            if (normalize) x = normalize_sample(x, lo, scale, inv);
-                        }
-                        seg[q] = x;
-                    }
+                for (int r = 0; r < 32; ++r) y[r] = make_float2(load_view(rs, offe + 128 * r), load_view(rs, offo + 128 * r));
+            }
+            if (normalize && (i0 < 0 || i0 + 4096 > win_len)) {  // edge frame: + beta, centre padding 0
+#pragma unroll
+                for (int r = 0; r < 32; ++r) {
+                    const int i = i0 + l2 + 128 * r;
+                    y[r].x = (i >= 0 && i < win_len) ? y[r].x + beta : 0.f;
+                    y[r].y = (i + 1 >= 0 && i + 1 < win_len) ? y[r].y + beta : 0.f;
                 }
             }
-        }
-        __syncthreads();
-        float bmax = 0.f;
-        if (wave < nf) {
-            float2 u[32];
+            // periodic Hann, w[n] = 1/2 - cos(2 pi n / 4096) / 2 at n = 2c + 128 r
+            // (+1): cos(a + 2 pi r / 32) by angle addition from the lane's
+            // cos/sin of a (table values; opaque per frame so the 64 products
+            // are not hoisted into live registers)
+            // The upper half-wave's (-1)^r input modulation of step 1 is folded
+            // in as the sign of the odd-r weights: +-1/2 per lane.
+            float2 he = hwe, ho = hwo;
+            float hs = lane >= 32 ? -0.5f : 0.5f;
+            __asm__ volatile("" : "+v"(he.x), "+v"(he.y), "+v"(ho.x), "+v"(ho.y), "+v"(hs));
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                const float cr = kW32[r][0], sr = -kW32[r][1];  // cos, sin of 2 pi r / 32
+                const float ce = fmaf(he.x, cr, -he.y * sr), co = fmaf(ho.x, cr, -ho.y * sr);
+                const float a = (r & 1) ? hs : 0.5f;  // w = a (1 - cos)
+                y[r].x *= fmaf(-a, ce, a);
+                y[r].y *= fmaf(-a, co, a);
+            }
             if constexpr ((DIAG & 4) != 0) {
 #pragma unroll
-                for (int j = 0; j < 32; ++j) u[j] = make_float2((float)j, seg[lane + j]);
+                for (int j = 0; j < 32; ++j) u[j] = y[j];
             } else {
-            // ---- 1. load + DFT-32 over r ----
-            float2 y[32];
-            const float* x = seg + wave * hop + 2 * lane;
+                // The transpose (step 3) runs in two passes of 16 registers per
+                // lane, each pass freeing 16 registers before it fills 16, so the
+                // data never occupies more than 64 VGPRs.  For that, the upper
+                // half-wave (columns c >= 32) works with its rows rotated by 16:
+                // (-1)^r on the input gives DFT output X[(k + 16) % 32] in
+                // register k (step 1), its twiddle ladder is rotated to match
+                // (step 2), it reads its columns rotated by 16 (step 3), and
+                // undoes that rotation of the second DFT by (-1)^k on the odd
+                // outputs (step 4).
+                const unsigned up = lane >= 32 ? 0x80000000u : 0u;  // sign mask of the upper half
+                auto flip = [up](float2 v) {
+                    return make_float2(__uint_as_float(__float_as_uint(v.x) ^ up),
+                                       __uint_as_float(__float_as_uint(v.y) ^ up));
+                };
+                // ---- 1. DFT-32 over r ----
+                // (the (-1)^r of the upper half rides on its Hann weights, above)
+                dft32(y);
+                // ---- 2. twiddle W2048^(c row) = (W^8c)^(row/8) (W^c)^(row%8),
+                // row = k (+16 mod 32 in the upper half); ladders rebuilt per frame
+                // (<= 4 roundings per twiddle; not kept live across the loop) ----
+                __asm__ volatile("" : "+v"(t1.x), "+v"(t1.y), "+v"(t8.x), "+v"(t8.y));
+                float2 p1[8], p8[4];
+                p1[0] = make_float2(1.f, 0.f);
+                p1[1] = t1;
 #pragma unroll
-            for (int r = 0; r < 32; ++r) y[r] = make_float2(x[128 * r], x[128 * r + 1]);
-            dft32(y);
-            // ---- 2. twiddle ----
-#pragma unroll
-            for (int k = 1; k < 32; ++k) {
-                const float2 t = (k & 7) == 0 ? p8[k >> 3] : (k < 8 ? p1[k] : cmul(p8[k >> 3], p1[k & 7]));
-                y[dperm(k)] = cmul(y[dperm(k)], t);
-            }
-            // ---- 3. transpose in two halves ----
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) wb[k * kRow + lane] = y[dperm(half * 16 + k)];
-                wave_sync();
-                if ((lane >> 5) == half) {
-                    const float2* src = wb + (k1 - 16 * half) * kRow + h;
-#pragma unroll
-                    for (int m = 0; m < 32; ++m) u[m] = src[2 * m];
+                for (int i = 2; i < 8; ++i) p1[i] = cmul(p1[i - 1], t1);
+                {
+                    const float2 q1 = t8, q2 = cmul(t8, t8), q3 = cmul(q2, t8);
+                    const bool hi = lane >= 32;
+                    p8[0] = hi ? q2 : make_float2(1.f, 0.f);
+                    p8[1] = hi ? q3 : q1;
+                    p8[2] = hi ? make_float2(1.f, 0.f) : q2;
+                    p8[3] = hi ? q1 : q3;
                 }
-                wave_sync();
-            }
-            // ---- 4. DFT-32 over m ----
-            dft32(u);
-            // ---- 5. radix-2 across the lane pair ----
 #pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                const float2 e = u[dperm(j)];
-                const float2 o = make_float2(swap_pair(e.x), swap_pair(e.y));
-                const float2 E0 = h ? o : e, E1 = h ? e : o;
-                const float2 t = cmul(wconst64(j), E1);
-                u[dperm(j)] = h ? csub(E0, t) : cadd(E0, t);
-            }
-            }
-            // lane holds Z[k1 + 32 (32 h + j)] in u[dperm(j)]
-            // ---- 6. real split ----
-            if (h && !(DIAG & 8)) {
+                for (int k = 0; k < 32; ++k) {
+                    const float2 tk = (k & 7) == 0 ? p8[k >> 3] : cmul(p8[k >> 3], p1[k & 7]);
+                    y[dperm(k)] = cmul(y[dperm(k)], tk);
+                }
+                // ---- 3. transpose in two passes: pass p moves registers
+                // 16p..16p+15 (rows (16p + 16 [c >= 32]) % 32 + 0..15 of column
+                // c) and lane (k1, h) takes columns h + 2m, m in the 16-range
+                // 16 ((k1 / 16) ^ p) of row k1, into u[16p ..] ----
 #pragma unroll
-                for (int j = 0; j < 32; ++j) wb[k1 + 32 * j] = u[dperm(j)];  // Z[1024 + k1 + 32 j]
-            }
-            wave_sync();
-            // h = 0 lanes: X[k], k = k1 + 32 j < 1024 (bands above NC/2 take the
-            // generic kernel, see fe_fast4096)
-            if (!h && !(DIAG & 8)) {
+                for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) wb[k * kRow + lane] = y[dperm(16 * pass + k)];
+                    wave_sync();
+                    const float2* src = wb + (k1 & 15) * kRow + h + 32 * (((k1 >> 4) ^ pass) & 1);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) u[16 * pass + i] = src[2 * i];
+                    wave_sync();
+                }
+                // ---- 4. DFT-32 over m (input rotated by 16 in the upper half:
+                // output k times (-1)^k) ----
+                dft32(u);
+#pragma unroll
+                for (int k = 1; k < 32; k += 2) u[dperm(k)] = flip(u[dperm(k)]);
+                // ---- 5. radix-2 across the lane pair: lane h = 1 sends
+                // W64^j E1, lane h = 0 sends E0; then Z = E0 + W E1 (h = 0) and
+                // E0 - W E1 (h = 1) are recv +- own ----
+                const float sg = h ? -1.f : 1.f;
 #pragma unroll
                 for (int j = 0; j < 32; ++j) {
-                    const int k = k1 + 32 * j;
-                    const float2 a = u[dperm(j)];
-                    const float2 zb = wb[k == 0 ? 0 : 1024 - k];
-                    const float2 b = (k == 0) ? a : zb;  // Z[NC - k]
-                    const float2 E = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
-                    const float2 O = make_float2(0.5f * (a.y + b.y), -0.5f * (a.x - b.x));
-                    const float2 t = cmul(stw2[k], O);
-                    u[dperm(j)] = cadd(E, t);
+                    const float2 e = u[dperm(j)];
+                    const float2 wj = wconst64(j);
+                    const float2 g = h ? cmul(wj, e) : e;
+                    const float2 rv = make_float2(swap_pair(g.x), swap_pair(g.y));
+                    u[dperm(j)] = make_float2(fmaf(sg, g.x, rv.x), fmaf(sg, g.y, rv.y));
                 }
             }
-            wave_sync();
-            if (!h) {  // X[0..1023] in natural order (the host keeps 1 <= kmin, kmax <= 1022)
+        }
+        // lane holds Z[k1 + 32 (32 h + j)] in u[dperm(j)]
+        // ---- 6. real split and |X|^power ----
+        if (h && !(DIAG & 8)) {
 #pragma unroll
-                for (int j = 0; j < 32; ++j) wb[k1 + 32 * j] = u[dperm(j)];
-            }
-            wave_sync();
-            // ---- 7. Hann in frequency, |.|^power ----
-            constexpr int PT = kHalf / 64 - 1;  // 15 bins per lane: nb <= 960 (host-checked)
-            float pw[PT];
-            const int nb = kmax - kmin + 1;
+            for (int j = 0; j < 32; ++j) wb[k1 + 32 * j] = u[dperm(j)];  // Z[1024 + k1 + 32 j]
+        }
+        wave_sync();
+        // h = 0 lanes: X[k], k = k1 + 32 j < 1024 (bands above NC/2 take the
+        // generic kernel, see fe_fast4096), |X|^p straight into the band
+        // buffer, stored reversed from the top of the wave's buffer: bin k at
+        // float Pt[-k], Pt = float 2 kHalf - 1.  Step j writes bins
+        // [32 j, 32 j + 32), at or above float2 kHalf - 16 - 16 j, while later
+        // steps still read mirrors below float2 1024 - 32 j - 32: the two never
+        // meet, so the split needs no extra registers, no buffer and no guard.
+        float* Pt = reinterpret_cast<float*>(wb) + (2 * kHalf - 1);
+        if (!h && !(DIAG & 8)) {
+            // Z[2048 - k] sits at wb[1024 - k1 - 32 j] = mb[32 (31 - j)]: one base
+            // register and non-negative immediate offsets (wb[1024], read for
+            // k = 0, is in the buffer and unused)
+            const float2* mb = wb + (32 - k1);
+            float* pk = Pt - k1 - 32 * 31;  // bin k1 + 32 j at pk[32 (31 - j)] = Pt[-k]
 #pragma unroll
-            for (int t = 0; t < ((DIAG & 16) ? 0 : PT); ++t) {
-                const int k = min(kmin + lane + 64 * t, kmax);  // clamped: unconditional LDS reads
-                const float2 c0 = wb[k], cm = wb[k - 1], cp = wb[k + 1];
-                const float re = 0.5f * c0.x - 0.25f * (cm.x + cp.x);
-                const float im = 0.5f * c0.y - 0.25f * (cm.y + cp.y);
-                pw[t] = pow_mag<PM>(re, im, power);
-            }
-            wave_sync();
-            float* P = reinterpret_cast<float*>(wb);
-#pragma unroll
-            for (int t = 0; t < ((DIAG & 16) ? 0 : PT); ++t)
-                if (lane + 64 * t < nb) P[lane + 64 * t] = pw[t];
-            wave_sync();
-            // ---- 8. mel rows ----
-            // rows of the constant image are zero-padded to whole float4s
-            // (value offsets 16-B aligned); the padding adds exact zeros
-            for (int m = lane; m < ((DIAG & 32) ? 0 : n_mels); m += 64) {
-                const int4 rw = srows[m];
-                const float4* wv = reinterpret_cast<const float4*>(svals + rw.z);
-                const float* pv = P + (rw.x - kmin);
-                float s = 0.f;
-                for (int i = 0; i < rw.y; i += 4) {
-                    const float4 a = wv[i >> 2];
-                    s = fmaf(a.x, pv[i], s);
-                    s = fmaf(a.y, pv[i + 1], s);
-                    s = fmaf(a.z, pv[i + 2], s);
-                    s = fmaf(a.w, pv[i + 3], s);
-                }
-                melT[m * kFpg + wave] = s;
-                bmax = fmaxf(bmax, s);
+            for (int j = 0; j < 32; ++j) {
+                const float2 a = u[dperm(j)];
+                const float2 zb = mb[32 * (31 - j)];
+                const float2 b = (j == 0 && k1 == 0) ? a : zb;  // Z[NC - k]; Z[0] for k = 0
+                const float2 E = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+                const float2 O = make_float2(0.5f * (a.y + b.y), -0.5f * (a.x - b.x));
+                float2 wj = cmul(wk, wconst128(j));  // W4096^k
+                __asm__ volatile("" : "+v"(wj.x), "+v"(wj.y));  // formed here, not hoisted
+                const float2 X = cadd(E, cmul(wj, O));
+                if (!(DIAG & 16)) pk[32 * (31 - j)] = pow_mag<PM>(X.x, X.y, power);
             }
         }
-        __syncthreads();
-        for (int idx = tid; idx < ((DIAG & 64) ? 0 : n_mels * nf); idx += 256) {
-            const int m = idx / nf, f = idx - (idx / nf) * nf;
-            melS[((size_t)w * n_mels + m) * T + f0 + f] = melT[m * kFpg + f];
+        wave_sync();
+        // ---- 8. mel rows ----
+        // rows of the CSR image are zero-padded to whole float4s (value
+        // offsets 16-B aligned); the padding adds exact zeros
+        float fmx = 0.f;
+        float* orow = melF + (size_t)fi * n_mels;  // fi = w T + t
+        for (int m = lane; m < ((DIAG & 32) ? 0 : n_mels); m += 64) {
+            // row m covers bins [x, x + L): its values are stored reversed and
+            // front-padded to L4 = roundup(L, 4) (fe_cimg4096), so with P
+            // reversed the row is an ascending run pv[0 .. L4)
+            const int4 rw = srows[m];
+            const float4* wv = reinterpret_cast<const float4*>(svals + rw.z);
+            const float* pv = Pt - rw.x - (rw.y - 1);  // bins x + L4 - 1 down to x
+            float s = 0.f;
+            for (int i = 0; i < rw.y; i += 4) {
+                const float4 a = wv[i >> 2];
+                s = fmaf(a.x, pv[i], s);
+                s = fmaf(a.y, pv[i + 1], s);
+                s = fmaf(a.z, pv[i + 2], s);
+                s = fmaf(a.w, pv[i + 3], s);
+            }
+            s *= apow;
+            if (!(DIAG & 64)) orow[m] = s;
+            fmx = fmaxf(fmx, s);
         }
-        __shared__ float red[kFpg];
-        bmax = wave_max(bmax);
-        if (lane == 0) red[wave] = bmax;
-        __syncthreads();
-        if (tid == 0) {
-            for (int k = 1; k < kFpg; ++k) bmax = fmaxf(bmax, red[k]);
-            blkmax[w * ngrp + g] = bmax;
-        }
+        fmx = wave_max(fmx);
+        if (lane == 0 && !(DIAG & 64)) pmax[fi] = fmx;
+        wave_sync();  // the buffer is rewritten by the next frame
     }
 }
 
 // ---------------------------------------------------------------------------
-// fe_db: power_to_db(ref=max), clamp at -top_db, mean_sub, channel repeat.
-// One wave per mel band row.
+// fe_db: power_to_db(ref=max), clamp at -top_db, mean_sub, channel repeat,
+// and the frame-major -> band-major transpose of the stft kernels' output.
+// Block = (tile of `tile_t` frames, window): coalesced rows of melF in,
+// dB in registers, transpose through LDS, contiguous band rows out.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melS, const float* __restrict__ blkmax,
-                                             const float4* __restrict__ stats, int nfblk, int n_mels, int T,
-                                             int db_scale, float amin, float top_db, int mean_sub,
-                                             int channels, int normalize, float* __restrict__ out,
-                                             int* __restrict__ status) {
+__device__ __forceinline__ float db_value(float v, float ref_db, int db_scale, float amin, float top_db) {
+    if (db_scale) {
+        v = __fsub_rn(__fmul_rn(10.0f, log10f(fmaxf(amin, v))), ref_db);
+        v = fmaxf(v, -top_db);  // log_spec.max() == 0 exactly
+    }
+    return v;
+}
+
+// block-wide max of the window's partial maxima -> 10 log10(max(amin, S.max()))
+__device__ __forceinline__ float window_ref_db(const float* __restrict__ pmax, int nparts, float amin, float* red) {
+    float mx = 0.f;
+    for (int i = threadIdx.x; i < nparts; i += blockDim.x) mx = fmaxf(mx, pmax[i]);
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    mx = red[0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) mx = fmaxf(mx, red[k]);
+    return __fmul_rn(10.0f, log10f(fmaxf(amin, mx)));
+}
+
+__global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melF, const float* __restrict__ pmax,
+                                             int nparts, const float4* __restrict__ stats,
+                                             const float* __restrict__ band_mean, int n_mels, int T, int tile_t,
+                                             int db_scale, float amin, float top_db, int channels, int normalize,
+                                             float* __restrict__ out, int* __restrict__ status) {
+    extern __shared__ float tile[];  // [tile_t][n_mels + 1]
+    __shared__ float red[4];
     const int w = blockIdx.y;
-    float smax = 0.f;
-    for (int i = 0; i < nfblk; ++i) smax = fmaxf(smax, blkmax[w * nfblk + i]);
-    const float ref_db = __fmul_rn(10.0f, log10f(fmaxf(amin, smax)));
-    const int lane = threadIdx.x & 63;
-    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int t0 = blockIdx.x * tile_t;
+    const int nt = min(tile_t, T - t0);
+    const float ref_db = window_ref_db(pmax + (size_t)w * nparts, nparts, amin, red);
     if (blockIdx.x == 0 && threadIdx.x == 0 && status) {
         float lo = INFINITY, hi = -INFINITY;
         int bad = 0;
         for (int s = 0; s < kStatSplit; ++s) {
-            float4 st = stats[w * kStatSplit + s];
+            const float4 st = stats[w * kStatSplit + s];
             lo = fminf(lo, st.x);
             hi = fmaxf(hi, st.y);
             bad |= st.z != 0.f;
@@ -745,26 +811,36 @@ __global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melS, con
         if (normalize && !(hi - lo > 0.f)) bad = 1;
         status[w] = bad ? AA_WIN_NONFINITE : AA_WIN_OK;
     }
-    if (m >= n_mels) return;
-    const float* row = melS + ((size_t)w * n_mels + m) * T;
-    auto val = [&](int t) {
-        float v = row[t];
-        if (db_scale) {
-            v = __fsub_rn(__fmul_rn(10.0f, log10f(fmaxf(amin, v))), ref_db);
-            v = fmaxf(v, -top_db);  // log_spec.max() == 0 exactly
-        }
-        return v;
-    };
-    float mean = 0.f;
-    if (mean_sub) {
-        float s = 0.f;
-        for (int t = lane; t < T; t += 64) s += val(t);
-        mean = wave_sum(s) / (float)T;
+    const int ld = n_mels + 1;
+    const float* src = melF + ((size_t)w * T + t0) * n_mels;  // nt contiguous frame rows
+    for (int idx = threadIdx.x; idx < nt * n_mels; idx += 256) {
+        const int tt = idx / n_mels, m = idx - tt * n_mels;
+        tile[tt * ld + m] = db_value(src[idx], ref_db, db_scale, amin, top_db);
     }
-    float* o = out + ((size_t)w * n_mels + m) * T * channels;
-    for (int t = lane; t < T; t += 64) {
-        const float v = val(t) - mean;
-        for (int c = 0; c < channels; ++c) o[t * channels + c] = v;
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < n_mels * tile_t; idx += 256) {
+        const int m = idx / tile_t, tt = idx - m * tile_t;
+        if (tt < nt) {
+            float v = tile[tt * ld + m];
+            if (band_mean) v -= band_mean[(size_t)w * n_mels + m];
+            float* o = out + (((size_t)w * n_mels + m) * T + t0 + tt) * channels;
+            for (int c = 0; c < channels; ++c) o[c] = v;
+        }
+    }
+}
+
+// mean_sub: per-band mean over time of the dB values, one block per window
+__global__ __launch_bounds__(256) void fe_band_mean(const float* __restrict__ melF, const float* __restrict__ pmax,
+                                                    int nparts, int n_mels, int T, int db_scale, float amin,
+                                                    float top_db, float* __restrict__ band_mean) {
+    __shared__ float red[4];
+    const int w = blockIdx.x;
+    const float ref_db = window_ref_db(pmax + (size_t)w * nparts, nparts, amin, red);
+    const float* src = melF + (size_t)w * T * n_mels;
+    for (int m = threadIdx.x; m < n_mels; m += 256) {
+        float s = 0.f;
+        for (int t = 0; t < T; ++t) s += db_value(src[(size_t)t * n_mels + m], ref_db, db_scale, amin, top_db);
+        band_mean[(size_t)w * n_mels + m] = s / (float)T;
     }
 }
 
@@ -804,41 +880,46 @@ static int launch_stft(const FePlan& p, const float* pcm, const aa_window* wins,
 // the wave-per-frame kernel covers n_fft 4096 whenever the kept band fits the
 // per-wave buffer (15 bins per lane)
 static bool fe_fast4096(const FePlan& p) {
-    // kept band inside X[1..1022] (Hann neighbours in range), padded rows
+    // kept band inside X[2..1022]: Hann neighbours in range and clear of the
+    // bins -1..1 that the folded normalisation offset touches; padded rows
     // (+3 bins) inside the 15 x 64 power slots
-    return p.cfg.n_fft == 4096 && p.kmin >= 1 && p.kmax <= 1022 &&
+    return p.cfg.n_fft == 4096 && p.kmin >= 2 && p.kmax <= 1022 && p.kmin + 64 * (kHalf / 64 - 1) < kHalf &&
            p.kmax - p.kmin + 1 + 3 <= (kHalf / 64 - 1) * 64;
 }
 
 static size_t fe_lds_bytes4096(const FePlan& p) {
-    return sizeof(float) * (size_t)fe4096_seg_cap(p.cfg.hop) + sizeof(float2) * (size_t)kFpg * kHalf +
-           (size_t)p.cimg_bytes + sizeof(float) * (size_t)p.cfg.n_mels * kFpg;
+    return (size_t)p.cimg_bytes + sizeof(float2) * (size_t)kWpb * kHalf;
 }
 
 template <int PM>
 static int launch_stft4096(const FePlan& p, const float* pcm, const aa_window* wins, int n_win,
-                           const float4* stats, float* melS, float* blkmax, hipStream_t st) {
+                           const float4* stats, float* melS, float* pmax, hipStream_t st) {
     const size_t lds = fe_lds_bytes4096(p);
-    AA_CHECK(lds <= 150 * 1024, AA_ERR_UNSUPPORTED, "fe4096: hop %d needs %zu B of LDS", p.cfg.hop, lds);
+    AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "fe4096: %zu B of LDS", lds);
     static size_t attr_set = 0;
     if (lds > attr_set) {
         AA_HIP(hipFuncSetAttribute((const void*)fe_stft_mel_4096<PM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds));
         attr_set = lds;
     }
-    const int ngrp = p.nfblk;
-    const int n_items = ngrp * n_win;
-    hipLaunchKernelGGL(fe_stft_mel_4096<PM>, dim3(n_items), dim3(256), lds, st, pcm, wins, stats, p.d_tw, p.d_cimg,
-                       p.cimg_bytes, p.cfg.win_len, p.cfg.hop, p.T, p.cfg.n_mels, p.kmin, p.kmax,
-                       p.cfg.normalize, p.cfg.power, ngrp, n_items, melS, blkmax);
+    const int n_frames = p.T * n_win;
+    // persistent grid: blocks resident together (LDS-limited, 2 per CU at the
+    // CFG filterbank), a multiple of 8 for the XCD renumbering
+    const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
+    int grid = std::min((n_frames + kWpb - 1) / kWpb, 256 * per_cu);
+    grid = (grid + 7) & ~7;
+    hipLaunchKernelGGL(fe_stft_mel_4096<PM>, dim3(grid), dim3(64 * kWpb), lds, st, pcm, wins, stats, p.d_tw,
+                       p.d_tw2, p.d_cimg, p.cimg_bytes, p.cfg.win_len, p.cfg.hop, p.T, p.cfg.n_mels, p.kmin,
+                       p.kmax, p.cfg.normalize, p.cfg.power, n_frames, melS, pmax);
     AA_LAUNCH_CHECK();
     return AA_OK;
 }
 
 struct FeWs {
     float4* stats;
-    float* melS;
-    float* blkmax;
+    float* melS;       // frame-major mel power [n_win][T][n_mels]
+    float* blkmax;     // partial maxima [n_win][nparts]
+    float* band_mean;  // mean_sub: [n_win][n_mels]
     size_t bytes;
 };
 
@@ -851,6 +932,8 @@ static FeWs fe_ws_layout(const FePlan& p, int n_win, char* base) {
     off = align_up(off + sizeof(float) * (size_t)n_win * p.cfg.n_mels * p.T, 256);
     w.blkmax = reinterpret_cast<float*>(base + off);
     off = align_up(off + sizeof(float) * (size_t)n_win * p.nfblk, 256);
+    w.band_mean = reinterpret_cast<float*>(base + off);
+    if (p.cfg.mean_sub) off = align_up(off + sizeof(float) * (size_t)n_win * p.cfg.n_mels, 256);
     w.bytes = off;
     return w;
 }
@@ -892,7 +975,7 @@ extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** 
     p->kmax = kmax;
     p->nnz = (int)vals.size();
     // per-window partial maxima: one per frame block of whichever kernel runs
-    p->nfblk = fe_fast4096(*p) ? (p->T + kFpg - 1) / kFpg : (p->T + kFpb - 1) / kFpb;
+    p->nfblk = fe_fast4096(*p) ? p->T : (p->T + kFpb - 1) / kFpb;
     if (vals.empty()) vals.push_back(0.f);
     const int nc = n / 2;
     std::vector<float> win(n);
@@ -918,20 +1001,22 @@ extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** 
     if (e == hipSuccess) e = up((void**)&p->d_rows, rows.data(), sizeof(int4) * rows.size());
     if (e == hipSuccess) e = up((void**)&p->d_vals, vals.data(), sizeof(float) * vals.size());
     if (e == hipSuccess && n == 4096) {
-        // constant image of the wave-per-frame kernel, byte-identical to its LDS region
-        // CSR rows zero-padded to whole float4s, value offsets 16-B aligned
+        // CSR image of the wave-per-frame kernel, byte-identical to its LDS
+        // region: rows (first bin, padded length, value offset) | values, each
+        // row zero-padded to whole float4s (value offsets 16-B aligned)
         std::vector<int4> prow(rows.size());
         std::vector<float> pval;
+        // (the kernel keeps the band power reversed: values are stored last
+        // bin first, zero-padded at the front, so a row reads one ascending run)
         for (size_t m = 0; m < rows.size(); ++m) {
-            const int len = (rows[m].y + 3) & ~3;
+            const int len = (rows[m].y + 3) & ~3, pad = len - rows[m].y;
             prow[m] = make_int4(rows[m].x, len, (int)pval.size(), 0);
-            for (int i = 0; i < len; ++i) pval.push_back(i < rows[m].y ? vals[rows[m].z + i] : 0.f);
+            for (int i = 0; i < len; ++i) pval.push_back(i < pad ? 0.f : vals[rows[m].z + rows[m].y - 1 - (i - pad)]);
         }
-        const size_t raw = kCimgRows + sizeof(int4) * prow.size() + sizeof(float) * pval.size();
+        const size_t raw = sizeof(int4) * prow.size() + sizeof(float) * pval.size();
         std::vector<char> img((raw + 1023) / 1024 * 1024, 0);
-        memcpy(img.data(), tw2.data(), sizeof(float2) * 1025);
-        memcpy(img.data() + kCimgRows, prow.data(), sizeof(int4) * prow.size());
-        memcpy(img.data() + kCimgRows + sizeof(int4) * prow.size(), pval.data(), sizeof(float) * pval.size());
+        memcpy(img.data(), prow.data(), sizeof(int4) * prow.size());
+        memcpy(img.data() + sizeof(int4) * prow.size(), pval.data(), sizeof(float) * pval.size());
         p->cimg_bytes = (int)img.size();
         e = up((void**)&p->d_cimg, img.data(), img.size());
     }
@@ -1005,10 +1090,17 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
     if (rc != AA_OK) return rc;
     if ((rc = p->timer.end(FE_STAGE_STFT, st, e0)) != AA_OK) return rc;
     if ((rc = p->timer.begin(FE_STAGE_DB, st, &e0)) != AA_OK) return rc;
-    hipLaunchKernelGGL(fe_db, dim3((p->cfg.n_mels + 3) / 4, n_win), dim3(256), 0, st, ws.melS,
-                       ws.blkmax, ws.stats, p->nfblk, p->cfg.n_mels, p->T, p->cfg.db_scale,
-                       p->cfg.amin, p->cfg.top_db, p->cfg.mean_sub, p->cfg.channels,
-                       p->cfg.normalize, out, win_status);
+    if (p->cfg.mean_sub) {
+        hipLaunchKernelGGL(fe_band_mean, dim3(n_win), dim3(256), 0, st, ws.melS, ws.blkmax, p->nfblk,
+                           p->cfg.n_mels, p->T, p->cfg.db_scale, p->cfg.amin, p->cfg.top_db, ws.band_mean);
+        AA_LAUNCH_CHECK();
+    }
+    int tile_t = 64;  // frames per fe_db block: the [tile_t][n_mels + 1] tile within 64 KiB
+    while (tile_t > 1 && (size_t)tile_t * (p->cfg.n_mels + 1) * 4 > 65536) tile_t >>= 1;
+    hipLaunchKernelGGL(fe_db, dim3((p->T + tile_t - 1) / tile_t, n_win), dim3(256),
+                       (size_t)tile_t * (p->cfg.n_mels + 1) * 4, st, ws.melS, ws.blkmax, p->nfblk, ws.stats,
+                       p->cfg.mean_sub ? ws.band_mean : nullptr, p->cfg.n_mels, p->T, tile_t, p->cfg.db_scale,
+                       p->cfg.amin, p->cfg.top_db, p->cfg.channels, p->cfg.normalize, out, win_status);
     AA_LAUNCH_CHECK();
     return p->timer.end(FE_STAGE_DB, st, e0);
 }
