@@ -1,6 +1,6 @@
 // Diagnostic harness: time conv_mfma variants (phases ablated) on random
 // bf16 data.  Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include
-//   tools/conv_bench.hip -o /tmp/conv_bench ; run on the GPU box.
+//   tools/conv_bench.hip audio-analysis_amd/csrc/aa_api.cpp -o tools/conv_bench ; run on the GPU box.
 #include "../audio-analysis_amd/csrc/aa_cnn.hip"
 
 #include <cstdio>
@@ -38,7 +38,8 @@ static float time_one(int n, int Hin, int Win, int cout, void* in, void* w, floa
     return 1e3f * ms / iters;
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool pmc = argc > 1;  // PMC runs: the model's configurations once each, no ablations
     const int n = 64;
     std::vector<uint16_t> h(200u << 20);  // 400 MB: larger than every layer's input
     for (auto& x : h) x = 0x3c00 + (rand() & 0x3ff);  // bf16 ~1..2 with random mantissa
@@ -52,7 +53,7 @@ int main() {
     (void)hipMemcpy(w, h.data(), 8u << 20, hipMemcpyHostToDevice);
     (void)hipMemset(b, 0, 4096);
     FirstConv fc{};
-    const int it = 20;
+    const int it = pmc ? 1 : 20;
     // layer dims of model1 at T = 226 (hop 640)
     auto dims = [](int kh, int kw, int cin, int pool, int& H, int& W, int& C) {
         if (kh == 3 && cin == 32 && pool == 3) { H = 158; W = 224; C = 32; }
@@ -67,7 +68,7 @@ int main() {
         dims(KH, KW, CIN, POOL, H, W, C);                                                                 \
         const float full = time_one<T_, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, 0, EB>(n, H, W, C, in, w, b, \
                                                                                           out, fc, it);   \
-        const float mf = time_one<T_, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, 5, EB>(n, H, W, C, in, w, b,   \
+        const float mf = pmc ? 0.f : time_one<T_, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, 5, EB>(n, H, W, C, in, w, b, \
                                                                                         out, fc, it);     \
         const double fl = 2.0 * n * (H - KH + 1) * (W - KW + 1) * KH * KW * CIN * C;                      \
         printf("%-6s %dx%d cin %3d pool %d  WM%d WN%d MF%d NF%d %2dx%2d  full %7.1f us (%6.1f TF)  only-mfma %7.1f us\n", \
@@ -75,6 +76,16 @@ int main() {
                fl / full * 1e-6, mf);                                                                     \
     }
     AA_CONV_CFGS(AA_BENCH)
+    if (!pmc && argc == 1) {  // candidate tilings of the 9x3 layer
+#define AA_TRY(X)                                          \
+        X(bf16, 9, 3, 64, 3, 4, 2, 7, 4, 12, 33, true)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 15, 24, true)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 4, 4, 6, 33, true)      \
+        X(bf16, 9, 3, 64, 3, 4, 1, 5, 8, 9, 33, true)      \
+        X(bf16, 9, 3, 64, 3, 2, 2, 10, 4, 9, 33, true)
+        AA_TRY(AA_BENCH)
+#undef AA_TRY
+    }
     // first conv (1 -> 32, VALU) fused into the 3x3/32 pool-3 stage, on a
     // 160 x 226 log-mel input
     {
@@ -90,7 +101,9 @@ int main() {
 #define AA_FUSED(D)                                                                                        \
     printf("fused c1+c2 DIAG %2d: %7.1f us\n", D,                                                         \
            time_one<bf16, 3, 3, 32, 4, 1, 9, 2, 3, 12, 48, D, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
-        AA_FUSED(0) AA_FUSED(2) AA_FUSED(4) AA_FUSED(6)
+        AA_FUSED(0)
+        if (pmc) return 0;
+        AA_FUSED(2) AA_FUSED(4) AA_FUSED(6)
 #undef AA_FUSED
     }
     // ablations of the 9x3 layer: staging / MFMA / stores / weight stream
