@@ -476,7 +476,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
 #pragma unroll
                 for (int i = 0; i < MF; ++i)
 #pragma unroll
-                    for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(fa[i], fb[j], acc[i][j]);
+                    for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(fb[j], fa[i], acc[i][j]);
             }
             continue;
         }
@@ -492,7 +492,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
 #pragma unroll
             for (int i = 0; i < MF; ++i)
 #pragma unroll
-                for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(fa[i], fb[j], acc[i][j]);
+                for (int j = 0; j < NF; ++j) acc[i][j] = mfma_chunk(fb[j], fa[i], acc[i][j]);
 #pragma unroll
             for (int i = 0; i < MF; ++i) fa[i] = na[i];
             if (cc + 1 < CPC) {
@@ -506,17 +506,31 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
 #undef AA_GLDS
     __syncthreads();  // patch no longer needed: reuse LDS for the f32 tile
 
+    // The MFMAs compute D = W X^T (weights as the A operand): lane holds
+    // output channels c0 .. c0 + 3 of pixel p, stored as one 8-byte (bf16) /
+    // 16-byte (f32) vector per fragment
     ET* E = reinterpret_cast<ET*>(smem);
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
-        const int col = wn * NF * 16 + j * 16 + (lane & 15);
-        const float bj = EBF16 ? bias[blockIdx.y * BN + col] : 0.f;
+        const int c0 = wn * NF * 16 + j * 16 + 4 * (lane >> 4);
+        float bj[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bj[r] = EBF16 ? bias[blockIdx.y * BN + c0 + r] : 0.f;
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
-            const int prow = (wm * MF + i) * 16 + 4 * (lane >> 4);
+            const int p = (wm * MF + i) * 16 + (lane & 15);
+            if (p < TP) {
+                ET* e = E + p * ESTR + c0;
+                if constexpr (EBF16) {
+                    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                    bf16x4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (prow + r < TP) E[(prow + r) * ESTR + col] = (ET)(acc[i][j][r] + bj);
+                    for (int r = 0; r < 4; ++r) v[r] = (bf16)(acc[i][j][r] + bj[r]);
+                    *reinterpret_cast<bf16x4*>(e) = v;
+                } else {
+                    *reinterpret_cast<float4*>(e) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+                }
+            }
         }
     }
     __syncthreads();
@@ -757,7 +771,7 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     X(bf16, 3, 3, 32, 3, 4, 1, 9, 2, 12, 48, true)          \
     X(bf16, 3, 3, 32, 1, 4, 1, 4, 4, 8, 32, true)           \
     X(bf16, 3, 3, 64, 1, 4, 1, 4, 4, 8, 32, true)           \
-    X(bf16, 9, 3, 64, 3, 4, 2, 5, 4, 9, 33, true)           \
+    X(bf16, 9, 3, 64, 3, 4, 2, 7, 4, 12, 33, true)          \
     X(bf16, 1, 3, 128, 1, 1, 4, 9, 2, 6, 24, false)         \
     X(float, 3, 3, 32, 3, 2, 2, 9, 1, 6, 48, false)         \
     X(float, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false)         \
