@@ -12,12 +12,12 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG.parent / "csrc"
 INCLUDE = PKG.parent.parent / "include"
 LIB = PKG / "libaa.so"
-SOURCES = ["aa_api.cpp", "aa_frontend.hip", "aa_cnn.hip", "aa_scan.hip"]
+SOURCES = ["aa_api.cpp", "aa_frontend.hip", "aa_cnn.hip", "aa_scan.hip", "aa_signal.hip"]
 ARCH = os.environ.get("AA_OFFLOAD_ARCH", "gfx950")
 # per-source flags: the FFT front end is written in scalar f32; SLP packing it
 # into v_pk_* ops needs paired SGPR constants and register shuffles that push
 # the wave-per-frame kernel past its 128-VGPR budget (spills)
-EXTRA_FLAGS = {"aa_frontend.hip": ["-fno-slp-vectorize"]}
+EXTRA_FLAGS = {"aa_frontend.hip": ["-fno-slp-vectorize"], "aa_signal.hip": ["-fno-slp-vectorize"]}
 
 
 def hipcc() -> str:

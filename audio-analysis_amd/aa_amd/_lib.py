@@ -33,6 +33,9 @@ AA_OP = {
 AA_WIN_OK = 0
 AA_WIN_NONFINITE = 1
 
+AA_SN_NONFINITE = 1
+AA_SN_RUN_OVERFLOW = 2
+
 
 class AAError(RuntimeError):
     pass
@@ -56,6 +59,16 @@ class Layer(C.Structure):
         ("op", C.c_int32), ("kh", C.c_int32), ("kw", C.c_int32), ("filters", C.c_int32),
         ("alpha", C.c_float), ("eps", C.c_float), ("off", C.c_int64 * 4),
     ]
+
+
+class SnConfig(C.Structure):
+    _fields_ = [("sr", C.c_int32), ("n_fft", C.c_int32), ("hop_length", C.c_int32),
+                ("signal_width", C.c_double), ("freq_range", C.c_double)]
+
+
+class SnComponent(C.Structure):
+    _fields_ = [("left", C.c_int32), ("top", C.c_int32), ("width", C.c_int32), ("height", C.c_int32),
+                ("area", C.c_int32), ("order", C.c_int32)]
 
 
 _lib = None
@@ -92,6 +105,15 @@ _SIGS = {
                                 C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "aa_span_nonzero": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p,
                                   C.c_void_p]),
+    "aa_sn_create": (C.c_int, [C.POINTER(SnConfig), C.POINTER(C.c_void_p)]),
+    "aa_sn_destroy": (C.c_int, [C.c_void_p]),
+    "aa_sn_geometry": (C.c_int, [C.POINTER(SnConfig), C.POINTER(C.c_int32)]),
+    "aa_sn_n_frames": (C.c_int64, [C.c_void_p, C.c_int64]),
+    "aa_sn_workspace_bytes": (C.c_size_t, [C.c_void_p, C.c_int64]),
+    "aa_sn_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.c_void_p,
+                            C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "aa_sn_components_from_mask": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t,
+                                             C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -5,11 +5,13 @@ Surface kept from the reference (src/identify_tracks.py):
       -> (tracks, length, signals, raw_length, bird_labels)        :416-573
   Signal (:915-1033), ModelResult (:869-912), Prediction (:845-866),
   get_master_tag (:580-647), load_recording (:49-62), get_end (:387-413),
+  signal_noise (:650-706), merge_signals / get_tracks_from_signals (:725-842),
   segment_overlap / mel_freq (:709-718), NON_BIRD / DEFAULT_* constants.
 
 What runs where: decode on the host; the window schedule on the host
 (integers only, aa_amd.windows); log-mel front end, CNN ensemble, per-track
-mean and the end-of-recording scan on the GPU through libaa.so.  The JSON-facing
+mean, the end-of-recording scan and the signal detector on the GPU through
+libaa.so; the track builder (merging a few dozen signals) on the host.  The JSON-facing
 objects below are plain host bookkeeping, identical in content to the
 reference's.
 """
@@ -223,7 +225,7 @@ def load_recording(file, resample=48000):
         raise Exception(f"Could not load {file}")
 
 
-def get_end(frames, sr, device=None):
+def get_end(frames, sr, device=None, pcm_dev=None):
     """Reference get_end (:387-413): the start (whole seconds) of the first
     170-frame chunk of the 4800/281 STFT whose 120-band mel block is constant,
     else the recording length.  A block is constant exactly when every frame
@@ -231,7 +233,105 @@ def get_end(frames, sr, device=None):
     spectrum), so the GPU scans sample spans for nonzero values instead of
     computing the STFT."""
     from . import gpu_ops
-    return gpu_ops.get_end(frames, sr, device=device)
+    return gpu_ops.get_end(frames, sr, device=device, pcm_dev=pcm_dev)
+
+
+# ---------------------------------------------------------------------------
+# signals and the track builder
+# ---------------------------------------------------------------------------
+def signal_noise(frames, sr, hop_length=281, device=None, pcm_dev=None):
+    """Reference signal_noise (:650-706): the recording's spectral blobs as
+    Signals, computed on the GPU (aa_amd.signals / aa_signal.hip)."""
+    from .signals import detector
+    det = detector(sr, hop_length, device)
+    return [Signal(*t) for t in det.signal_noise(frames, pcm=pcm_dev)]
+
+
+def merge_signals(signals):
+    """One merge sweep (:725-792): signals sorted by start (ties: higher
+    mel_freq_end first); each absorbs the first other signal on the same side
+    of 1500 mel that overlaps it enough in time and mel frequency, or lies
+    within 2 s with a similar mel range.  Absorbed signals are dropped."""
+    to_delete = []
+    something_merged = False
+    signals = sorted(signals, key=lambda s: s.mel_freq_end, reverse=True)
+    signals = sorted(signals, key=lambda s: s.start)
+    for s in signals:
+        if s in to_delete:
+            continue
+        merged = False
+        for u in signals:
+            if u in to_delete or u == s:
+                continue
+            same_side = (u.mel_freq_end < 1500 and s.mel_freq_end < 1500) or (
+                u.mel_freq_end > 1500 and s.mel_freq_end > 1500)
+            if not same_side:
+                continue
+            overlap = s.time_overlap(u)
+            freq_overlap_time = 0.5 if (s.mel_freq_start > 1000 and u.mel_freq_start > 1000) else 0.75
+            time_diff = s.start - u.end if s.start > u.end else u.start - s.end
+            mel_overlap = s.mel_freq_overlap(u)
+            if overlap > u.length * 0.75 and mel_overlap > -20:
+                s.merge(u)
+                merged = True
+                break
+            elif overlap > 0 and mel_overlap > u.mel_freq_range * freq_overlap_time:
+                s.merge(u)
+                merged = True
+                break
+            elif mel_overlap > u.mel_freq_range * freq_overlap_time and time_diff <= 2:
+                # (sic) the reference compares u's mel end with s's mel range
+                if u.mel_freq_end > s.mel_freq_range:
+                    range_overlap = s.mel_freq_range / u.mel_freq_range
+                else:
+                    range_overlap = u.mel_freq_range / s.mel_freq_range
+                if range_overlap < 0.75:
+                    continue
+                s.merge(u)
+                merged = True
+                break
+        if merged:
+            something_merged = True
+            to_delete.append(u)
+    for s in to_delete:
+        signals.remove(s)
+    return signals, something_merged
+
+
+def get_tracks_from_signals(signals, end):
+    """Tracks from signals (:795-842): merge until stable, drop signals
+    shorter than the running ``min_length`` (0.35 s, then rebound by the
+    overlap test as in the reference), enlarge by 1.4 (at least 0.7 s, clipped
+    to ``end``), absorb signals overlapping > 70 % of the shorter one, drop
+    tracks narrower than 50 mel."""
+    merged = True
+    while merged:
+        signals, merged = merge_signals(signals)
+    to_delete = []
+    min_length = 0.35
+    min_track_length = 0.7
+    for s in signals:
+        if s in to_delete:
+            continue
+        if s.length < min_length:
+            to_delete.append(s)
+            continue
+        s.enlarge(1.4, min_track_length=min_track_length)
+        s.end = min(end, s.end)
+        for s2 in signals:
+            if s2 in to_delete or s == s2:
+                continue
+            overlap = s.time_overlap(s2)
+            min_length = min(s.length, s2.length)
+            if overlap > 0.7 * min_length:
+                s.merge(s2)
+                to_delete.append(s2)
+    for s in to_delete:
+        signals.remove(s)
+    narrow = [s for s in signals if s.mel_freq_range < 50]
+    for s in narrow:
+        signals.remove(s)
+    return signals
 
 
 # ---------------------------------------------------------------------------
@@ -250,26 +350,32 @@ def _group_models(models):
 
 
 def classify(file, models, analyse_tracks, meta_data=None, precision=None, device=None):
+    """Reference classify (:416-573): decode, get_end, signal_noise on every
+    recording; tracks from the metadata (analyse_tracks) or built from the
+    signals; the model groups over every track's windows."""
+    import torch
     from .pipeline import Classifier
     frames, sr = load_recording(file)
     raw_length = len(frames) / sr
-    length = get_end(frames, sr, device=device)
-    if not analyse_tracks:
-        raise NotImplementedError(
-            "signal detection + track building (src/identify_tracks.py:650-842) is not on the "
-            "MI355X path yet; run with --analyse-tracks and metadata tracks")
-    signals = []  # only consumed by the analyse_tracks=False JSON branch (src/analyse.py:157)
-    if meta_data is None:
-        return None
-    tracks = []
-    for t in meta_data["Tracks"]:
-        s = Signal(t["start"], t["end"], t.get("minFreq", 0), t.get("maxFreq", MAX_FRQUENCY))
-        s.track_id = t["id"]
-        tracks.append(s)
+    dev = torch.device(device or "cuda")
+    pcm = torch.from_numpy(np.ascontiguousarray(frames, dtype=np.float32)).to(dev)  # uploaded once
+    length = get_end(frames, sr, device=dev, pcm_dev=pcm)
+    n_sig = int(sr * length)
+    signals = signal_noise(frames[:n_sig], sr, 281, device=dev, pcm_dev=pcm[:n_sig])
+    if analyse_tracks:
+        if meta_data is None:
+            return None
+        tracks = []
+        for t in meta_data["Tracks"]:
+            s = Signal(t["start"], t["end"], t.get("minFreq", 0), t.get("maxFreq", MAX_FRQUENCY))
+            s.track_id = t["id"]
+            tracks.append(s)
+    else:
+        tracks = get_tracks_from_signals([s.copy() for s in signals], length)
     if len(tracks) == 0:
         return [], length, [], raw_length, []
-    clf = Classifier.shared(precision=precision, device=device)
-    bird_labels = clf.classify_tracks(frames, sr, tracks, _group_models(models))
+    clf = Classifier.shared(precision=precision, device=dev)
+    bird_labels = clf.classify_tracks(frames, sr, tracks, _group_models(models), pcm=pcm)
     if bird_labels is None:
         return [], length, [], raw_length, []
     return tracks, length, signals, raw_length, list(bird_labels)

@@ -78,10 +78,11 @@ class Classifier:
                                       meta=meta)
         return self._models[key]
 
-    def classify_tracks(self, frames, sr, tracks, groups):
+    def classify_tracks(self, frames, sr, tracks, groups, pcm=None):
         from .identify_tracks import DEFAULT_BIRDS
         dev = self.device
-        pcm = torch.from_numpy(np.ascontiguousarray(frames, dtype=np.float32)).to(dev)
+        if pcm is None:
+            pcm = torch.from_numpy(np.ascontiguousarray(frames, dtype=np.float32)).to(dev)
         views = None
         logmel = None
         bird_labels = set()

@@ -17,6 +17,7 @@
 //               on the sparse mel filterbank (CSR rows, contiguous bins).
 //   fe_db       per-window max -> power_to_db, clamp, mean_sub, layout/channels.
 #include "aa_common.h"
+#include "aa_wavefft.h"
 
 #include <cmath>
 #include <cstring>
@@ -106,49 +107,6 @@ __global__ __launch_bounds__(256) void fe_stats(const float* __restrict__ pcm,
         }
         stats[w * kStatSplit + blockIdx.x] = make_float4(mn, mx, (float)bad, 0.f);
     }
-}
-
-// ---------------------------------------------------------------------------
-// radix building blocks (forward transform, W = exp(-2 pi i / n))
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 mul_negi(float2 a) { return make_float2(a.y, -a.x); }  // a * (-i)
-
-__device__ __forceinline__ void dft2(float2& a, float2& b) {
-    float2 t = csub(a, b);
-    a = cadd(a, b);
-    b = t;
-}
-// in: a,b,c,d = x0..x3 ; out in natural order X0..X3
-__device__ __forceinline__ void dft4(float2& a, float2& b, float2& c, float2& d) {
-    float2 t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = mul_negi(csub(b, d));
-    a = cadd(t0, t2);
-    c = csub(t0, t2);
-    b = cadd(t1, t3);
-    d = csub(t1, t3);
-}
-__device__ __forceinline__ void dft8(float2* v) {
-    const float r = 0.70710678118654752440f;
-    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
-    float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
-    dft4(e0, e1, e2, e3);
-    dft4(o0, o1, o2, o3);
-    // twiddles W8^k, k = 0..3
-    float2 w1 = make_float2(r * (o1.x + o1.y), r * (o1.y - o1.x));   // * (r, -r)
-    float2 w2 = mul_negi(o2);                                       // * (0, -1)
-    float2 w3 = make_float2(r * (o3.y - o3.x), -r * (o3.x + o3.y));  // * (-r, -r)
-    v[0] = cadd(e0, o0);
-    v[4] = csub(e0, o0);
-    v[1] = cadd(e1, w1);
-    v[5] = csub(e1, w1);
-    v[2] = cadd(e2, w2);
-    v[6] = csub(e2, w2);
-    v[3] = cadd(e3, w3);
-    v[7] = csub(e3, w3);
 }
 
 // LDS index of complex point i: one float2 of padding per 8 keeps the radix-8
@@ -458,8 +416,8 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
 //      Z[k1 + 32 k2'] = E0 + W64^k2' E1, Z[k1 + 32 (k2' + 32)] = E0 - W64^k2' E1
 //   6. real split X[k] = E + W4096^k O from Z[k], conj Z[2048 - k], with
 //      W4096^(k1 + 32 j) = W4096^k1 W128^j (one table entry per lane)
-//   7. periodic Hann applied in frequency: Xw[k] = X[k]/2 - (X[k-1] + X[k+1])/4,
-//      |Xw|^power into LDS
+//   7. |X|^power into the wave's LDS buffer (the periodic Hann was applied to
+//      the samples before step 1, by angle addition from two table values)
 //   8. sparse mel rows (CSR in LDS, shared by the block), times a^p ->
 //      melF[w][t][:] (frame-major: one contiguous row per frame) and the frame
 //      maximum -> pmax[w][t]
@@ -469,54 +427,10 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
 // frames: neighbouring frames overlap by 4096 - hop samples and one L2 then
 // serves the overlap.
 // ---------------------------------------------------------------------------
-#include "aa_twiddles.h"
-
 #ifndef AA_FE_WPB
 #define AA_FE_WPB 8
 #endif
 constexpr int kWpb = AA_FE_WPB;         // waves per block (2 blocks per CU)
-constexpr int kRow = 66;                // padded transpose row (float2)
-constexpr int kHalf = 16 * kRow;        // per-wave buffer (float2)
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ float2 wconst32(int k) { return make_float2(kW32[k][0], kW32[k][1]); }
-__device__ __forceinline__ float2 wconst64(int k) { return make_float2(kW64[k][0], kW64[k][1]); }
-__device__ __forceinline__ float2 wconst128(int k) { return make_float2(kW128[k][0], kW128[k][1]); }
-
-// 32-point DFT in registers, in place: 4 interleaved DFT-8s, twiddles, DFT-4s.
-// Output X[k] is left in v[dperm(k)], dperm(k) = 4 (k % 8) + k / 8 (a
-// compile-time permutation, so no data moves).
-__device__ __forceinline__ constexpr int dperm(int k) { return 4 * (k & 7) + (k >> 3); }
-__device__ __forceinline__ void dft32(float2* v) {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        float2 t[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) t[m] = v[4 * m + p];
-        dft8(t);
-#pragma unroll
-        for (int m = 0; m < 8; ++m) v[4 * m + p] = t[m];
-    }
-#pragma unroll
-    for (int p = 1; p < 4; ++p)
-#pragma unroll
-        for (int k = 1; k < 8; ++k) v[4 * k + p] = cmul(v[4 * k + p], wconst32(p * k));
-#pragma unroll
-    for (int k = 0; k < 8; ++k) dft4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-}
-
-__device__ __forceinline__ float swap_pair(float x) {  // value of lane ^ 1
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
-}
-
-__device__ __forceinline__ float load_view(__amdgpu_buffer_rsrc_t rs, int i) {  // 0 outside the view
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, i * 4, 0, 0));
-}
 
 // DIAG (tools/fe_bench.hip only): 1 skip the PCM loads, 4 the FFT (steps 1-5),
 // 8 the real split, 16 Hann and power, 32 the mel rows, 64 the output stores.
@@ -624,6 +538,9 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
 #pragma unroll
                 for (int j = 0; j < 32; ++j) u[j] = y[j];
             } else {
+                // (the same steps as aa_wavefft.h's wave_hann + wave_fft_core,
+                // kept inline here: called as functions, the register
+                // allocation of this kernel spills 11 VGPRs)
                 // The transpose (step 3) runs in two passes of 16 registers per
                 // lane, each pass freeing 16 registers before it fills 16, so the
                 // data never occupies more than 64 VGPRs.  For that, the upper

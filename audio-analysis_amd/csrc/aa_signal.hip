@@ -1,0 +1,792 @@
+// Signal detector of classify() for gfx950: signal_noise
+// (reference src/identify_tracks.py:650-706), run on every recording (:420).
+//
+// Launches (one stream, no host synchronisation inside aa_sn_run):
+//   sn_stft       |STFT| of the recording (n_fft 4096, centre zero padding,
+//                 periodic Hann), one wave per frame through the front end's
+//                 wave FFT (aa_wavefft.h).  The real split yields every bin:
+//                 the lane holding Z[k] and its mirror Z[2048 - k] forms
+//                 X[k] = E + W^k O and X[2048 - k] = conj(E - W^k O).  Writes
+//                 the frame-major magnitude S[f][0..2048], the frame's median
+//                 over bins (radix select on the f32 bit patterns, values in
+//                 registers, an LDS histogram per wave) and the maximum.
+//   sn_transpose  S -> ST[bin][frame] (64 x 64 tiles through LDS)
+//   sn_select     per-bin median over frames: radix select over the contiguous
+//                 (L2-resident) ST row, both middle elements for an even count
+//   sn_mask       (S/a > 3 colmed/a) & (S/a > 3 rowmed/a) in numpy's f32
+//                 arithmetic (:656-669), bit-packed along time by ballot
+//   sn_morph_h/v  cv2 erode / dilate with rectangles (:670-684), separable,
+//                 64 frames per 64-bit word
+//   sn_runs, sn_unite, sn_stats, sn_emit
+//                 8-connected components over row runs (:686): union-find with
+//                 atomicMin hooking, bounding box, area and OpenCV's label-order
+//                 key per root, the size filter (:689-691), a compact list of
+//                 kept components for the host (a few entries per recording).
+#include "aa_common.h"
+#include "aa_wavefft.h"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+
+namespace aa {
+
+constexpr int kSnWpb = 8;      // waves per sn_stft block (1 block per CU: 2 waves per SIMD)
+constexpr int kSnBins = 2049;  // n_fft / 2 + 1
+constexpr int kSnLd = 2080;    // S row stride in floats (128-B aligned rows)
+constexpr int kSnHist = 256;   // radix-select buckets (8 bits per pass)
+constexpr int kSnFields = 10;  // run table: x0 x1 y parent left right top bottom area key
+enum { R_X0 = 0, R_X1, R_Y, R_P, R_LEFT, R_RIGHT, R_TOP, R_BOT, R_AREA, R_KEY };
+
+struct SnPlan {
+    aa_sn_config cfg;
+    int kh_d = 0, kw_d = 0;  // cv2.dilate(ones((height, width))) (:683)
+    int kh_e = 0, kw_e = 0;  // cv2.erode(ones((height // 10, width))) (:684)
+    int wmin = 0, hmin = 0;  // kept: width >= wmin, height >= hmin (:689-691)
+    float2* d_tw = nullptr;      // exp(-2 pi i m / 2048), m < 2048
+    float2* d_tw4096 = nullptr;  // exp(-2 pi i k / 4096), k <= 2048
+};
+
+__device__ __forceinline__ float mag(float re, float im) { return __builtin_amdgcn_sqrtf(fmaf(re, re, im * im)); }
+
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// The bucket of a 256-bucket histogram that holds `rank` (0-based), found by
+// one wave (lane owns buckets 4 lane .. 4 lane + 3).  *below: elements in
+// lower buckets; *cnt: elements in the bucket.
+__device__ __forceinline__ unsigned hist_pick(const unsigned* hist, unsigned rank, int lane, unsigned* below,
+                                              unsigned* cnt) {
+    const uint4 c = reinterpret_cast<const uint4*>(hist)[lane];
+    const unsigned s = c.x + c.y + c.z + c.w;
+    const unsigned incl = wave_incl_scan(s, lane);
+    const unsigned excl = incl - s;
+    const bool mine = excl <= rank && rank < incl;
+    unsigned dig = 0, bl = 0, cn = 0;
+    if (mine) {
+        const unsigned r = rank - excl;
+        if (r < c.x) { dig = 0; bl = 0; cn = c.x; }
+        else if (r < c.x + c.y) { dig = 1; bl = c.x; cn = c.y; }
+        else if (r < c.x + c.y + c.z) { dig = 2; bl = c.x + c.y; cn = c.z; }
+        else { dig = 3; bl = c.x + c.y + c.z; cn = c.w; }
+        dig += 4 * lane;
+        bl += excl;
+    }
+    const int src = __builtin_ctzll(__ballot(mine));
+    *below = __shfl(bl, src, 64);
+    *cnt = __shfl(cn, src, 64);
+    return __shfl(dig, src, 64);
+}
+
+// ---------------------------------------------------------------------------
+// sn_stft: one wave per frame, persistent over frames (XCD-contiguous ranges
+// of frames like fe_stft_mel_4096: neighbouring frames share 4096 - hop
+// samples through one L2).  Register budget 256 (2 waves per SIMD): the wave
+// FFT, the 2-bin split and the 33-value select need ~180 VGPRs; at the
+// 128-VGPR budget of 4 waves per SIMD they spill.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(2, 2))) void sn_stft(
+    const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const float2* __restrict__ tw,
+    const float2* __restrict__ tw4096, float* __restrict__ S, unsigned* __restrict__ colmed,
+    unsigned* __restrict__ gmax) {
+    extern __shared__ float lds[];
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    float2* wb = reinterpret_cast<float2*>(lds) + wave * kHalf;
+    unsigned* hist = reinterpret_cast<unsigned*>(reinterpret_cast<float2*>(lds) + kSnWpb * kHalf) + wave * kSnHist;
+    const int k1 = lane >> 1, h = lane & 1;
+    float2 t1 = tw[lane];                 // W2048^c
+    float2 t8 = tw[(8 * lane) & 2047];    // W2048^(8c)
+    const float2 wk1 = tw4096[k1];        // W4096^k1
+    const float2 te = tw4096[2 * lane], to = tw4096[2 * lane + 1];
+    const float2 hwe = make_float2(te.x, -te.y), hwo = make_float2(to.x, -to.y);
+    // the recording as a buffer view: centre padding and the ends read as 0
+    // (a negative offset wraps past num_records)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)pcm, 0, n_samples * 4, 0x00020000);
+
+    const int nb = gridDim.x;  // a multiple of 8 (host)
+    const int blk = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
+    const int G = nb * kSnWpb;
+    unsigned wmax = 0;
+    for (int fi = blk * kSnWpb + wave; fi < n_frames; fi += G) {
+        int l2 = 2 * lane;  // opaque: keeps the 64 load offsets from being hoisted
+        __asm__ volatile("" : "+v"(l2));
+        float2 wk = wk1;
+        __asm__ volatile("" : "+v"(wk.x), "+v"(wk.y));
+        float2 u[32];
+        {
+            float2 y[32];
+            const int offe = fi * hop - 2048 + l2;
+            int offo = offe + 1;  // separate register: no merged 8-byte loads
+            __asm__ volatile("" : "+v"(offo));
+#pragma unroll
+            for (int r = 0; r < 32; ++r) y[r] = make_float2(load_view(rs, offe + 128 * r), load_view(rs, offo + 128 * r));
+            wave_hann(y, hwe, hwo, lane);
+            wave_fft_core(y, u, wb, lane, t1, t8);
+        }
+        // ---- real split, every bin: lane (k1, 0) holds Z[k], k = k1 + 32 j <
+        // 1024, reads the mirror Z[2048 - k] the h = 1 lanes stored, and forms
+        // |X[k]| and |X[2048 - k]|.  The magnitudes stream into the same buffer
+        // from the top down as the mirrors below are consumed: step j writes
+        // |X[k]| at float 2111 - 64 j - k1 and |X[2048 - k]| at 2079 - 64 j - k1,
+        // above every mirror a later step reads (float2 <= 1024 - 32 (j + 1)).
+        // |X[1024]| = |Z[1024]| (lane 1) goes to float 31. ----
+        const float mid = mag(u[dperm(0)].x, u[dperm(0)].y);
+        if (h) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) wb[k1 + 32 * j] = u[dperm(j)];  // Z[1024 + k1 + 32 j]
+        }
+        wave_sync();
+        float* P = reinterpret_cast<float*>(wb);
+        if (!h) {
+            const float2* mb = wb + (32 - k1);  // Z[2048 - k] at mb[32 (31 - j)]
+            float* pb = P + (95 - k1);          // |X[2048 - k]| at pb[64 (31 - j)], |X[k]| 32 above
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                const float2 a = u[dperm(j)];
+                const float2 zb = mb[32 * (31 - j)];
+                const float2 b = (j == 0 && k1 == 0) ? a : zb;  // Z[0] is its own mirror
+                const float2 E = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+                const float2 O = make_float2(0.5f * (a.y + b.y), -0.5f * (a.x - b.x));
+                float2 wj = cmul(wk, wconst128(j));  // W4096^k
+                __asm__ volatile("" : "+v"(wj.x), "+v"(wj.y));
+                const float2 q = cmul(wj, O);
+                pb[64 * (31 - j) + 32] = mag(E.x + q.x, E.y + q.y);
+                pb[64 * (31 - j)] = mag(E.x - q.x, E.y - q.y);
+            }
+        }
+        wave_sync();
+        if (lane == 1) P[31] = mid;
+        wave_sync();
+        // ---- the frame's row of S, its maximum and its median over bins ----
+        // bin lane + 64 i sits at float lb - 128 i (i < 16) / hb + 128 i (i >= 16)
+        unsigned v[33];  // v[32] = bin 2048 (counted by lane 0)
+        {
+            const int lb = 2111 - 64 * (lane >> 5) - (lane & 31);
+            const int hb = -1889 - 64 * ((64 - lane) >> 5) - ((64 - lane) & 31);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = __float_as_uint(P[lb - 128 * i]);
+#pragma unroll
+            for (int i = 16; i < 32; ++i) v[i] = __float_as_uint(P[hb + 128 * i]);
+            v[32] = __float_as_uint(P[2079]);
+        }
+        float* srow = S + (size_t)fi * kSnLd;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) srow[lane + 64 * i] = __uint_as_float(v[i]);
+        if (lane == 0) srow[2048] = __uint_as_float(v[32]);
+        // bit patterns of non-negative floats order like the values (NaN and
+        // inf above every finite value: the host reads that as non-finite input)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) wmax = max(wmax, v[i]);
+        wmax = max(wmax, v[32]);
+        unsigned prefix = 0, pmask = 0, rank = kSnBins / 2;
+#pragma unroll 1
+        for (int shift = 24; shift >= 0; shift -= 8) {
+            reinterpret_cast<uint4*>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
+            wave_sync();
+#pragma unroll
+            for (int i = 0; i < 33; ++i)
+                if ((i < 32 || lane == 0) && (v[i] & pmask) == prefix) atomicAdd(&hist[(v[i] >> shift) & 255u], 1u);
+            wave_sync();
+            unsigned below, cnt;
+            const unsigned dig = hist_pick(hist, rank, lane, &below, &cnt);
+            prefix |= dig << shift;
+            pmask |= 255u << shift;
+            rank -= below;
+            wave_sync();
+        }
+        if (lane == 0) colmed[fi] = prefix;
+        wave_sync();  // the buffer is rewritten by the next frame
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (unsigned)__shfl_xor((int)wmax, o, 64));
+    if (lane == 0 && wmax) atomicMax(gmax, wmax);
+}
+
+// ---------------------------------------------------------------------------
+// sn_transpose: S[f][b] (stride kSnLd) -> ST[b][f] (stride ldt)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sn_transpose(const float* __restrict__ S, int n_frames, int ldt,
+                                                    float* __restrict__ ST) {
+    __shared__ float tile[64][65];
+    const int b0 = blockIdx.x * 64, f0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+    for (int r = ty; r < 64; r += 4) {
+        const int f = f0 + r, b = b0 + tx;
+        tile[r][tx] = (f < n_frames && b < kSnBins) ? S[(size_t)f * kSnLd + b] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int r = ty; r < 64; r += 4) {
+        const int b = b0 + r;
+        if (b < kSnBins) ST[(size_t)b * ldt + f0 + tx] = tile[tx][r];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// sn_select: numpy median of each row of X ([rows][ld], first n entries,
+// non-negative f32) as bit patterns: lo = element of rank (n - 1) / 2, hi =
+// element of rank n / 2 (equal for odd n).  One block per row; every pass
+// re-reads the row (L2-resident after the first).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, int ld, int n, unsigned* __restrict__ lo,
+                                                 unsigned* __restrict__ hi) {
+    __shared__ unsigned hist[kSnHist];
+    __shared__ unsigned pick[3];
+    __shared__ unsigned red[4];
+    const unsigned* row = reinterpret_cast<const unsigned*>(X) + (size_t)blockIdx.x * ld;
+    const int tid = threadIdx.x, lane = tid & 63;
+    unsigned prefix = 0, pmask = 0, rank = (unsigned)(n - 1) / 2, cnt = 0;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        hist[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < n; i += 256) {
+            const unsigned v = row[i];
+            if ((v & pmask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) {
+            unsigned below, c;
+            const unsigned dig = hist_pick(hist, rank, lane, &below, &c);
+            if (lane == 0) { pick[0] = dig; pick[1] = below; pick[2] = c; }
+        }
+        __syncthreads();
+        prefix |= pick[0] << shift;
+        pmask |= 255u << shift;
+        rank -= pick[1];
+        cnt = pick[2];
+    }
+    // prefix is the rank-(n-1)/2 element, `rank` its place among the cnt equal ones
+    unsigned second = prefix;
+    if ((n & 1) == 0 && rank + 1 >= cnt) {  // block-uniform: rank n/2 is the next larger value
+        unsigned mn = 0xFFFFFFFFu;
+        for (int i = tid; i < n; i += 256) {
+            const unsigned v = row[i];
+            if (v > prefix) mn = min(mn, v);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+        if (lane == 0) red[tid >> 6] = mn;
+        __syncthreads();
+        second = min(min(red[0], red[1]), min(red[2], red[3]));
+    }
+    if (tid == 0) {
+        lo[blockIdx.x] = prefix;
+        hi[blockIdx.x] = second;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// sn_mask: bit f % 64 of word (b, f / 64) = S[b][f]/a > 3 colmed[f]/a and
+// S[b][f]/a > 3 rowmed[b], with a = max(S) and numpy's float32 rounding of
+// every step (:656-667; division is monotone, so the medians of S/a are the
+// quotients of S's middle elements, the even-count mean taken on quotients).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sn_mask(const float* __restrict__ ST, int ldt, int n_frames, int words,
+                                               const unsigned* __restrict__ gmax, const unsigned* __restrict__ colmed,
+                                               const unsigned* __restrict__ rlo, const unsigned* __restrict__ rhi,
+                                               unsigned long long* __restrict__ M) {
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    if (w >= words) return;
+    const float a = __uint_as_float(*gmax);
+    float dr = __fdiv_rn(__uint_as_float(rlo[b]), a);
+    if ((n_frames & 1) == 0) dr = __fmul_rn(__fadd_rn(dr, __fdiv_rn(__uint_as_float(rhi[b]), a)), 0.5f);
+    const float r3 = __fmul_rn(3.f, dr);
+    const int f = 64 * w + lane;
+    bool bit = false;
+    if (f < n_frames) {
+        const float d = __fdiv_rn(ST[(size_t)b * ldt + f], a);
+        const float c3 = __fmul_rn(3.f, __fdiv_rn(__uint_as_float(colmed[f]), a));
+        bit = d > c3 && d > r3;  // false throughout when a == 0 (NaN quotients), like numpy
+    }
+    const unsigned long long m = __ballot(bit);
+    if (lane == 0) M[(size_t)b * words + w] = m;
+}
+
+// ---------------------------------------------------------------------------
+// Morphology on the bit image (row = bin, bit = frame).  cv2's erode/dilate
+// with a rectangle of ones and the default anchor (kw / 2, kh / 2): out(x, y)
+// = min / max over the kernel of in(x + i - ax, y + j - ay), taps outside the
+// image ignored.  Separable: sn_morph_h along time (offsets lo..hi, |d| < 64,
+// from the word and its two neighbours), sn_morph_v across bins.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sn_morph_h(const unsigned long long* __restrict__ src,
+                                                  unsigned long long* __restrict__ dst, int words, int n_frames,
+                                                  int lo, int hi, int erode) {
+    const int w = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y;
+    if (w >= words) return;
+    const unsigned long long ident = erode ? ~0ull : 0ull;
+    const unsigned long long* r = src + (size_t)y * words;
+    auto word = [&](int i) -> unsigned long long {  // bits past the image read as the identity
+        if (i < 0 || i >= words) return ident;
+        const unsigned long long v = r[i];
+        const int valid = n_frames - 64 * i;
+        if (valid >= 64) return v;
+        const unsigned long long keep = (1ull << valid) - 1;
+        return (v & keep) | (ident & ~keep);
+    };
+    const unsigned long long wm = word(w - 1), w0 = word(w), wp = word(w + 1);
+    unsigned long long acc = ident;
+    for (int d = lo; d <= hi; ++d) {
+        unsigned long long s;  // bit i = in(64 w + i + d)
+        if (d == 0) s = w0;
+        else if (d > 0) s = (w0 >> d) | (wp << (64 - d));
+        else s = (w0 << -d) | (wm >> (64 + d));
+        acc = erode ? (acc & s) : (acc | s);
+    }
+    const int valid = n_frames - 64 * w;
+    if (valid < 64) acc &= (1ull << valid) - 1;
+    dst[(size_t)y * words + w] = acc;
+}
+
+__global__ __launch_bounds__(256) void sn_morph_v(const unsigned long long* __restrict__ src,
+                                                  unsigned long long* __restrict__ dst, int rows, int words, int lo,
+                                                  int hi, int erode) {
+    const int w = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y;
+    if (w >= words) return;
+    unsigned long long acc = erode ? ~0ull : 0ull;
+    const int y0 = max(0, y + lo), y1 = min(rows - 1, y + hi);
+    for (int yy = y0; yy <= y1; ++yy) {
+        const unsigned long long v = src[(size_t)yy * words + w];
+        acc = erode ? (acc & v) : (acc | v);
+    }
+    dst[(size_t)y * words + w] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// Connected components (8-connectivity) over row runs.
+// Run table R (SoA, kSnFields arrays of max_runs ints).  sn_runs: one wave per
+// row lists its runs [x0, x1] in order into one atomically allocated range,
+// and initialises parents and statistics.  sn_unite: each run joins every run
+// of the row above that touches it (x ranges within one frame).  sn_stats:
+// bounding box, area and OpenCV's label-order key (the first 2x2 block of the
+// component in block-raster order) accumulated on the root.  sn_emit: roots
+// that pass the size filter.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int uf_load(const int* P, int i) {
+    return __hip_atomic_load(P + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int uf_find(const int* P, int i) {
+    int p = uf_load(P, i);
+    while (p != i) {
+        i = p;
+        p = uf_load(P, i);
+    }
+    return i;
+}
+// Parents only ever decrease (atomicMin hooking of the larger root under the
+// smaller), so every find terminates and the final root of a component is its
+// smallest run index.
+__device__ __forceinline__ void uf_union(int* P, int a, int b) {
+    a = uf_find(P, a);
+    b = uf_find(P, b);
+    while (a != b) {
+        if (a > b) { const int t = a; a = b; b = t; }
+        const int old = atomicMin(P + b, a);
+        if (old == b) return;  // b was still a root: hooked
+        b = uf_find(P, old);   // b was hooked meanwhile: join a with b's new tree
+        a = uf_find(P, a);
+    }
+}
+
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void sn_runs(const unsigned long long* __restrict__ M, int rows, int words,
+                                               int* __restrict__ R, int max_runs, int* __restrict__ row_off,
+                                               int* __restrict__ row_cnt, int* __restrict__ counters) {
+    const int lane = threadIdx.x & 63;
+    const int y = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (y >= rows) return;
+    const unsigned long long* r = M + (size_t)y * words;
+    auto starts_of = [&](int w) -> unsigned long long {
+        const unsigned long long v = r[w], prev = w > 0 ? r[w - 1] : 0ull;
+        return v & ~((v << 1) | (prev >> 63));
+    };
+    auto ends_of = [&](int w) -> unsigned long long {
+        const unsigned long long v = r[w], next = w + 1 < words ? r[w + 1] : 0ull;
+        return v & ~((v >> 1) | (next << 63));
+    };
+    int total = 0;
+    for (int w0 = 0; w0 < words; w0 += 64) {
+        const int w = w0 + lane;
+        total += wave_sum_int(w < words ? __popcll(starts_of(w)) : 0);
+    }
+    int base = 0;
+    if (lane == 0 && total > 0) base = atomicAdd(counters, total);
+    base = __shfl(base, 0, 64);
+    if (base + total > max_runs) {  // cannot happen within the host's bound; flagged, row dropped
+        if (lane == 0) atomicOr(counters + 1, AA_SN_RUN_OVERFLOW);
+        total = 0;
+    }
+    if (lane == 0) {
+        row_off[y] = base;
+        row_cnt[y] = total;
+    }
+    if (total == 0) return;
+    int* X0 = R + (size_t)R_X0 * max_runs;
+    int* X1 = R + (size_t)R_X1 * max_runs;
+    int* Y = R + (size_t)R_Y * max_runs;
+    int* P = R + (size_t)R_P * max_runs;
+    int ks0 = base, ke0 = base;
+    for (int w0 = 0; w0 < words; w0 += 64) {
+        const int w = w0 + lane;
+        unsigned long long s = w < words ? starts_of(w) : 0ull;
+        unsigned long long e = w < words ? ends_of(w) : 0ull;
+        const unsigned cs = __popcll(s), ce = __popcll(e);
+        const unsigned is = wave_incl_scan(cs, lane), ie = wave_incl_scan(ce, lane);
+        int ks = ks0 + (int)(is - cs), ke = ke0 + (int)(ie - ce);
+        while (s) {  // the k-th start and the k-th end of a row bound run k
+            const int i = ks++;
+            X0[i] = 64 * w + __builtin_ctzll(s);
+            Y[i] = y;
+            P[i] = i;
+            R[(size_t)R_LEFT * max_runs + i] = INT_MAX;
+            R[(size_t)R_RIGHT * max_runs + i] = -1;
+            R[(size_t)R_TOP * max_runs + i] = INT_MAX;
+            R[(size_t)R_BOT * max_runs + i] = -1;
+            R[(size_t)R_AREA * max_runs + i] = 0;
+            R[(size_t)R_KEY * max_runs + i] = INT_MAX;
+            s &= s - 1;
+        }
+        while (e) {
+            X1[ke++] = 64 * w + __builtin_ctzll(e);
+            e &= e - 1;
+        }
+        ks0 += (int)__shfl(is, 63, 64);
+        ke0 += (int)__shfl(ie, 63, 64);
+    }
+}
+
+__global__ __launch_bounds__(256) void sn_unite(int* __restrict__ R, int max_runs, const int* __restrict__ row_off,
+                                                const int* __restrict__ row_cnt, const int* __restrict__ counters,
+                                                int rows) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= min(counters[0], max_runs)) return;
+    const int* X0 = R + (size_t)R_X0 * max_runs;
+    const int* X1 = R + (size_t)R_X1 * max_runs;
+    const int y = R[(size_t)R_Y * max_runs + i];
+    if (y <= 0 || y >= rows) return;  // row 0, or a slot of a dropped row (y = -1)
+    int* P = R + (size_t)R_P * max_runs;
+    const int a = X0[i] - 1, b = X1[i] + 1;  // 8-connectivity: diagonal neighbours touch
+    const int first = row_off[y - 1], end = first + row_cnt[y - 1];
+    int lo = first, hi = end;  // first run above that ends at or after a
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (X1[m] < a) lo = m + 1;
+        else hi = m;
+    }
+    for (int j = lo; j < end && X0[j] <= b; ++j) uf_union(P, i, j);
+}
+
+__global__ __launch_bounds__(256) void sn_stats(int* __restrict__ R, int max_runs, int kx,
+                                                const int* __restrict__ counters) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= min(counters[0], max_runs)) return;
+    const int y = R[(size_t)R_Y * max_runs + i];
+    if (y < 0) return;
+    const int root = uf_find(R + (size_t)R_P * max_runs, i);
+    const int x0 = R[(size_t)R_X0 * max_runs + i], x1 = R[(size_t)R_X1 * max_runs + i];
+    atomicMin(R + (size_t)R_LEFT * max_runs + root, x0);
+    atomicMax(R + (size_t)R_RIGHT * max_runs + root, x1);
+    atomicMin(R + (size_t)R_TOP * max_runs + root, y);
+    atomicMax(R + (size_t)R_BOT * max_runs + root, y);
+    atomicAdd(R + (size_t)R_AREA * max_runs + root, x1 - x0 + 1);
+    atomicMin(R + (size_t)R_KEY * max_runs + root, (y >> 1) * kx + (x0 >> 1));
+}
+
+__global__ __launch_bounds__(256) void sn_emit(const int* __restrict__ R, int max_runs, int wmin, int hmin,
+                                               const int* __restrict__ counters, const unsigned* __restrict__ gmax,
+                                               aa_sn_component* __restrict__ out, int max_out,
+                                               int32_t* __restrict__ n_out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) {
+        int st = counters[1];
+        if (gmax && (*gmax & 0x7FFFFFFFu) >= 0x7F800000u) st |= AA_SN_NONFINITE;
+        n_out[1] = st;
+    }
+    if (i >= min(counters[0], max_runs)) return;
+    if (R[(size_t)R_Y * max_runs + i] < 0 || R[(size_t)R_P * max_runs + i] != i) return;
+    const int left = R[(size_t)R_LEFT * max_runs + i], top = R[(size_t)R_TOP * max_runs + i];
+    const int w = R[(size_t)R_RIGHT * max_runs + i] - left + 1;
+    const int hgt = R[(size_t)R_BOT * max_runs + i] - top + 1;
+    if (w < wmin || hgt < hmin) return;
+    const int k = atomicAdd(n_out, 1);
+    if (k < max_out) {
+        aa_sn_component c;
+        c.left = left;
+        c.top = top;
+        c.width = w;
+        c.height = hgt;
+        c.area = R[(size_t)R_AREA * max_runs + i];
+        c.order = R[(size_t)R_KEY * max_runs + i];
+        out[k] = c;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct SnWs {
+    float* S;
+    float* ST;
+    unsigned* colmed;
+    unsigned* rlo;
+    unsigned* rhi;
+    unsigned* gmax;
+    int* counters;  // [0] runs allocated, [1] status flags
+    unsigned long long* M0;
+    unsigned long long* M1;
+    int* row_off;
+    int* row_cnt;
+    int* R;
+    int max_runs;
+    size_t bytes;
+};
+
+static int sn_frames(const SnPlan& p, int64_t n) { return 1 + (int)(n / p.cfg.hop_length); }
+
+// After the final horizontal erosion of a horizontal dilation of the same
+// width kw (and the row-wise AND of the vertical erosion), the runs of a row
+// are separated by >= kw clear frames: at most (F + kw) / (kw + 1) per row.
+static int sn_max_runs(const SnPlan& p, int F) {
+    const long long per = (p.kw_e == p.kw_d && p.kw_e > 1) ? (F + p.kw_e) / (p.kw_e + 1) + 1 : F / 2 + 1;
+    return (int)std::min<long long>(per * kSnBins, INT_MAX / kSnFields);
+}
+
+static SnWs sn_ws_layout(const SnPlan& p, int F, char* base) {
+    SnWs w{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> char* {
+        char* q = base ? base + off : nullptr;
+        off = align_up(off + bytes, 256);
+        return q;
+    };
+    const int words = (F + 63) / 64, ldt = words * 64;
+    w.S = reinterpret_cast<float*>(take(sizeof(float) * (size_t)F * kSnLd));
+    w.ST = reinterpret_cast<float*>(take(sizeof(float) * (size_t)kSnBins * ldt));
+    w.colmed = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * (size_t)F));
+    w.rlo = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * kSnBins));
+    w.rhi = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * kSnBins));
+    w.gmax = reinterpret_cast<unsigned*>(take(64));
+    w.counters = reinterpret_cast<int*>(take(64));
+    w.M0 = reinterpret_cast<unsigned long long*>(take(8 * (size_t)kSnBins * words));
+    w.M1 = reinterpret_cast<unsigned long long*>(take(8 * (size_t)kSnBins * words));
+    w.row_off = reinterpret_cast<int*>(take(sizeof(int) * kSnBins));
+    w.row_cnt = reinterpret_cast<int*>(take(sizeof(int) * kSnBins));
+    w.max_runs = sn_max_runs(p, F);
+    w.R = reinterpret_cast<int*>(take(sizeof(int) * (size_t)kSnFields * w.max_runs));
+    w.bytes = off;
+    return w;
+}
+
+// morphology (:670-684), components (:686) and the size filter (:689-691)
+// from the mask in ws.M0
+static int sn_components(const SnPlan& p, const SnWs& ws, int F, const unsigned* gmax, aa_sn_component* out,
+                         int max_out, int32_t* n_out, hipStream_t st) {
+    const int words = (F + 63) / 64;
+    const dim3 gm((words + 255) / 256, kSnBins);
+    unsigned long long* a = ws.M0;
+    unsigned long long* b = ws.M1;
+    auto horiz = [&](int kw, int erode) -> int {
+        const int ax = kw / 2;
+        hipLaunchKernelGGL(sn_morph_h, gm, dim3(256), 0, st, a, b, words, F, -ax, kw - 1 - ax, erode);
+        AA_LAUNCH_CHECK();
+        std::swap(a, b);
+        return AA_OK;
+    };
+    auto vert = [&](int kh, int erode) -> int {
+        const int ay = kh / 2;
+        hipLaunchKernelGGL(sn_morph_v, gm, dim3(256), 0, st, a, b, kSnBins, words, -ay, kh - 1 - ay, erode);
+        AA_LAUNCH_CHECK();
+        std::swap(a, b);
+        return AA_OK;
+    };
+    int rc = AA_OK;
+    // MORPH_OPEN with ones(4, 4): erode, then dilate
+    if ((rc = horiz(4, 1)) || (rc = vert(4, 1)) || (rc = horiz(4, 0)) || (rc = vert(4, 0))) return rc;
+    if ((rc = horiz(p.kw_d, 0)) || (rc = vert(p.kh_d, 0))) return rc;
+    if ((rc = horiz(p.kw_e, 1)) || (rc = vert(p.kh_e, 1))) return rc;
+    AA_HIP(hipMemsetAsync(ws.counters, 0, 64, st));
+    AA_HIP(hipMemsetAsync(ws.R + (size_t)R_Y * ws.max_runs, 0xFF, sizeof(int) * (size_t)ws.max_runs, st));
+    hipLaunchKernelGGL(sn_runs, dim3((kSnBins + 3) / 4), dim3(256), 0, st, a, kSnBins, words, ws.R, ws.max_runs,
+                       ws.row_off, ws.row_cnt, ws.counters);
+    AA_LAUNCH_CHECK();
+    const int gr = (ws.max_runs + 255) / 256;
+    hipLaunchKernelGGL(sn_unite, dim3(gr), dim3(256), 0, st, ws.R, ws.max_runs, ws.row_off, ws.row_cnt, ws.counters,
+                       kSnBins);
+    AA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sn_stats, dim3(gr), dim3(256), 0, st, ws.R, ws.max_runs, (F + 1) / 2, ws.counters);
+    AA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sn_emit, dim3(gr), dim3(256), 0, st, ws.R, ws.max_runs, p.wmin, p.hmin, ws.counters, gmax, out,
+                       max_out, n_out);
+    AA_LAUNCH_CHECK();
+    return AA_OK;
+}
+
+}  // namespace aa
+
+using namespace aa;
+
+// cv2: an empty structuring element means a 3x3 rectangle
+static void sn_kernel_dims(int kh, int kw, int* oh, int* ow) {
+    if (kh <= 0 || kw <= 0) kh = kw = 3;
+    *oh = kh;
+    *ow = kw;
+}
+
+// kernel sizes and filter thresholds of src/identify_tracks.py:673-691, in
+// the reference's arithmetic (host only)
+static int sn_plan_geometry(const aa_sn_config& cfg, SnPlan* p) {
+    AA_CHECK(cfg.n_fft == 4096, AA_ERR_UNSUPPORTED, "aa_sn: n_fft %d (signal_noise uses 4096)", cfg.n_fft);
+    AA_CHECK(cfg.sr > 0 && cfg.hop_length > 0 && cfg.signal_width >= 0, AA_ERR_INVALID, "aa_sn: bad sizes");
+    p->cfg = cfg;
+    const int width = (int)(cfg.signal_width * cfg.sr / cfg.hop_length);
+    const double bin_hz = 1.0 / (cfg.n_fft * (1.0 / cfg.sr));  // np.fft.rfftfreq: k / (n d)
+    int height = 0;
+    for (int k = 0; k <= cfg.n_fft / 2; ++k)
+        if (k * bin_hz > cfg.freq_range) {
+            height = k + 1;
+            break;
+        }
+    sn_kernel_dims(height, width, &p->kh_d, &p->kw_d);
+    sn_kernel_dims(height / 10, width, &p->kh_e, &p->kw_e);
+    p->wmin = (int)std::floor(0.65 * width) + 1;  // s[2] > 0.65 * width
+    p->hmin = height - height / 10 + 1;            // s[3] > height - height // 10
+    AA_CHECK(p->kw_d <= 127 && p->kw_e <= 127, AA_ERR_UNSUPPORTED,
+             "aa_sn: signal width %d frames exceeds the 127-frame morphology window", width);
+    return AA_OK;
+}
+
+extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
+    AA_CHECK(cfg && plan, AA_ERR_INVALID, "aa_sn_create: null argument");
+    SnPlan* p = new SnPlan();
+    const int rc = sn_plan_geometry(*cfg, p);
+    if (rc != AA_OK) {
+        delete p;
+        return rc;
+    }
+    std::vector<float2> tw(2048), tw2(2049);
+    for (int m = 0; m < 2048; ++m) {
+        const double a = -2.0 * M_PI * m / 2048;
+        tw[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    for (int k = 0; k <= 2048; ++k) {
+        const double a = -2.0 * M_PI * k / 4096;
+        tw2[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    hipError_t e = hipMalloc((void**)&p->d_tw, sizeof(float2) * tw.size());
+    if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(float2) * tw.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc((void**)&p->d_tw4096, sizeof(float2) * tw2.size());
+    if (e == hipSuccess) e = hipMemcpy(p->d_tw4096, tw2.data(), sizeof(float2) * tw2.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        set_error("aa_sn_create: %s", hipGetErrorString(e));
+        aa_sn_destroy(p);
+        return AA_ERR_HIP;
+    }
+    *plan = p;
+    return AA_OK;
+}
+
+extern "C" int aa_sn_destroy(void* plan) {
+    SnPlan* p = static_cast<SnPlan*>(plan);
+    if (!p) return AA_OK;
+    (void)hipFree(p->d_tw);
+    (void)hipFree(p->d_tw4096);
+    delete p;
+    return AA_OK;
+}
+
+extern "C" int aa_sn_geometry(const aa_sn_config* cfg, int32_t* out6) {
+    AA_CHECK(cfg && out6, AA_ERR_INVALID, "aa_sn_geometry: null argument");
+    SnPlan p;
+    const int rc = sn_plan_geometry(*cfg, &p);
+    if (rc != AA_OK) return rc;
+    out6[0] = p.kh_d;
+    out6[1] = p.kw_d;
+    out6[2] = p.kh_e;
+    out6[3] = p.kw_e;
+    out6[4] = p.wmin;
+    out6[5] = p.hmin;
+    return AA_OK;
+}
+
+extern "C" int64_t aa_sn_n_frames(const void* plan, int64_t n_samples) {
+    const SnPlan* p = static_cast<const SnPlan*>(plan);
+    if (!p || n_samples < 0) return -1;
+    return sn_frames(*p, n_samples);
+}
+
+extern "C" size_t aa_sn_workspace_bytes(const void* plan, int64_t max_samples) {
+    const SnPlan* p = static_cast<const SnPlan*>(plan);
+    if (!p || max_samples < 0) return 0;
+    return sn_ws_layout(*p, sn_frames(*p, max_samples), nullptr).bytes;
+}
+
+extern "C" int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* workspace, size_t workspace_bytes,
+                         aa_sn_component* out, int32_t max_out, int32_t* n_out, uint64_t* mask_out, void* stream) {
+    SnPlan* p = static_cast<SnPlan*>(plan);
+    AA_CHECK(p && out && n_out && (pcm || n_samples == 0), AA_ERR_INVALID, "aa_sn_run: null argument");
+    AA_CHECK(n_samples >= 0 && n_samples <= (int64_t(1) << 29), AA_ERR_UNSUPPORTED,
+             "aa_sn_run: %lld samples (at most 2^29)", (long long)n_samples);
+    const int F = sn_frames(*p, n_samples);
+    const SnWs ws = sn_ws_layout(*p, F, static_cast<char*>(workspace));
+    AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE, "aa_sn_run: workspace %zu < %zu bytes",
+             workspace_bytes, ws.bytes);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    AA_HIP(hipMemsetAsync(ws.gmax, 0, 64, st));
+    AA_HIP(hipMemsetAsync(n_out, 0, 2 * sizeof(int32_t), st));
+    const size_t lds = sizeof(float2) * kSnWpb * kHalf + sizeof(unsigned) * kSnWpb * kSnHist;
+    static bool attr_set = false;
+    if (!attr_set) {
+        AA_HIP(hipFuncSetAttribute((const void*)sn_stft, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_set = true;
+    }
+    int grid = std::min((F + kSnWpb - 1) / kSnWpb, 256);  // persistent: 1 block per CU
+    grid = (grid + 7) & ~7;
+    hipLaunchKernelGGL(sn_stft, dim3(grid), dim3(64 * kSnWpb), lds, st, pcm, (int)n_samples, p->cfg.hop_length, F,
+                       p->d_tw, p->d_tw4096, ws.S, ws.colmed, ws.gmax);
+    AA_LAUNCH_CHECK();
+    const int words = (F + 63) / 64, ldt = words * 64;
+    hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST);
+    AA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sn_select, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, ws.rlo, ws.rhi);
+    AA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sn_mask, dim3((words + 3) / 4, kSnBins), dim3(256), 0, st, ws.ST, ldt, F, words, ws.gmax,
+                       ws.colmed, ws.rlo, ws.rhi, ws.M0);
+    AA_LAUNCH_CHECK();
+    if (mask_out)
+        AA_HIP(hipMemcpyAsync(mask_out, ws.M0, 8 * (size_t)kSnBins * words, hipMemcpyDeviceToDevice, st));
+    return sn_components(*p, ws, F, ws.gmax, out, max_out, n_out, st);
+}
+
+extern "C" int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int64_t n_frames, void* workspace,
+                                          size_t workspace_bytes, aa_sn_component* out, int32_t max_out,
+                                          int32_t* n_out, void* stream) {
+    SnPlan* p = static_cast<SnPlan*>(plan);
+    AA_CHECK(p && mask && out && n_out, AA_ERR_INVALID, "aa_sn_components_from_mask: null argument");
+    AA_CHECK(n_frames >= 1 && n_frames <= (int64_t(1) << 28), AA_ERR_INVALID,
+             "aa_sn_components_from_mask: %lld frames", (long long)n_frames);
+    const int F = (int)n_frames;
+    const SnWs ws = sn_ws_layout(*p, F, static_cast<char*>(workspace));
+    AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE,
+             "aa_sn_components_from_mask: workspace %zu < %zu bytes", workspace_bytes, ws.bytes);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    AA_HIP(hipMemsetAsync(n_out, 0, 2 * sizeof(int32_t), st));
+    AA_HIP(hipMemcpyAsync(ws.M0, mask, 8 * (size_t)kSnBins * ((F + 63) / 64), hipMemcpyDeviceToDevice, st));
+    return sn_components(*p, ws, F, nullptr, out, max_out, n_out, st);
+}

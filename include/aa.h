@@ -19,6 +19,8 @@
  *                model.predict(np.array(d))         src/identify_tracks.py:544
  *                MagTransform.call                  src/magtransformv2.py:19-21
  *   aa_track_mean  np.mean over models, windows     src/identify_tracks.py:547-551
+ *   aa_span_nonzero  get_end                        src/identify_tracks.py:387-413
+ *   aa_sn_*      signal_noise                       src/identify_tracks.py:650-706
  *
  * Return values: AA_OK (0) or an aa_status code; aa_last_error() gives a
  * thread-local message for the last failing call on this thread.
@@ -164,6 +166,48 @@ int aa_track_mean(const float* probs, int32_t n_models, int64_t model_stride, in
  * a constant mel block exactly when every sample its frames cover is zero. */
 int aa_span_nonzero(const float* pcm, int64_t n, const int64_t* spans, int32_t n_spans,
                     int32_t* flags, void* stream);
+
+/* ---------------------------------------------------------------- signal detector */
+/* signal_noise (src/identify_tracks.py:650-706): |STFT| (n_fft 4096) of the
+ * recording, the 3x row/column-median mask, cv2 morphology, 8-connected
+ * components and the size filter, all on the device. */
+typedef struct aa_sn_config {
+    int32_t sr;          /* sample rate of the PCM (48000 after load_recording) */
+    int32_t n_fft;       /* 4096 (:652) */
+    int32_t hop_length;  /* 281 (:420) */
+    double signal_width; /* SIGNAL_WIDTH seconds (:21, :673) */
+    double freq_range;   /* Hz; the first bin above it sets the kernel height (:675-681) */
+} aa_sn_config;
+
+/* One kept component: the cv2 stats row (x = frame, y = frequency bin) and
+ * OpenCV's label-order key, which orders components that tie on `left` in the
+ * reference's stable sort (:688). */
+typedef struct aa_sn_component {
+    int32_t left, top, width, height, area, order;
+} aa_sn_component;
+
+#define AA_SN_NONFINITE 1    /* status: non-finite PCM (librosa valid_audio would raise) */
+#define AA_SN_RUN_OVERFLOW 2 /* status: run table bound exceeded (internal error) */
+
+int aa_sn_create(const aa_sn_config* cfg, void** plan);
+int aa_sn_destroy(void* plan);
+/* {dilate height, dilate width, erode height, erode width, min width, min
+ * height} as derived from cfg (:673-691); host only */
+int aa_sn_geometry(const aa_sn_config* cfg, int32_t* out6);
+/* STFT frames of n_samples: 1 + n_samples / hop_length */
+int64_t aa_sn_n_frames(const void* plan, int64_t n_samples);
+size_t aa_sn_workspace_bytes(const void* plan, int64_t max_samples);
+/* pcm: device f32 [n_samples] (frames[: int(sr * length)], :420).
+ * out: device aa_sn_component[max_out], unordered; n_out: device int32[2] =
+ * {components kept (may exceed max_out), AA_SN_* status}.
+ * mask_out (may be NULL): device uint64 [2049][ceil(F / 64)], the thresholded
+ * mask before morphology; bit f % 64 of word f / 64 is frame f. */
+int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* workspace, size_t workspace_bytes,
+              aa_sn_component* out, int32_t max_out, int32_t* n_out, uint64_t* mask_out, void* stream);
+/* Morphology, components and filter of a given mask (mask_out's layout). */
+int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int64_t n_frames, void* workspace,
+                               size_t workspace_bytes, aa_sn_component* out, int32_t max_out,
+                               int32_t* n_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -27,6 +27,8 @@ Outputs (all small, committed):
                          detection and model.predict stubbed
 * ebird_subset.json      the reference's region species lists restricted to
                          the ebird codes the build's label sets use (data)
+* tracks.json            get_tracks_from_signals (:795-842) on seeded random
+                         signal sets (the track builder of analyse_tracks=False)
 """
 from __future__ import annotations
 
@@ -173,6 +175,17 @@ POSTPROC_CASES = [
      [(3, 1.0, 7.0, None, None), (4, 8.0, 16.0, None, None)], 13),
 ]
 
+# analyse_tracks=False: tracks built from these signals (start, end, f0, f1) by
+# the reference's get_tracks_from_signals; the JSON carries chirps/signals
+SIGNAL_CASES = [
+    ("signals_nz", None, True,
+     [(1.0, 1.6, 1500.0, 3000.0), (1.5, 2.2, 1600.0, 3200.0), (10.0, 10.4, 800.0, 900.0),
+      (20.0, 21.5, 4000.0, 6000.0), (20.2, 21.0, 4100.0, 5500.0), (40.0, 43.0, 300.0, 2500.0),
+      (55.0, 55.2, 100.0, 9000.0)], 21),
+    ("signals_auckland", {"lat": -36.85, "lng": 174.76}, True,
+     [(0.5, 1.5, 2000.0, 2600.0), (3.0, 5.0, 900.0, 4000.0), (30.0, 31.0, 6000.0, 9000.0)], 22),
+]
+
 
 def _model_metas():
     sys.path.insert(0, str(OUT.parents[1]))
@@ -201,7 +214,8 @@ def gen_postproc():
     import analyse
     metas = _model_metas()
     out_json, arrays = {}, {}
-    for name, location, species_file, tracks, seed in POSTPROC_CASES:
+    cases = [(c, None) for c in POSTPROC_CASES] + [((n, l, sf, [], sd), sig) for (n, l, sf, sig, sd) in SIGNAL_CASES]
+    for (name, location, species_file, tracks, seed), signals in cases:
         calls = {"n": 0}
         class FakeModel:
             def __init__(self, mname):
@@ -213,7 +227,7 @@ def gen_postproc():
                 return probs
         it.load_recording = lambda f, resample=48000: (np.ones(60 * 48000, np.float32) * 0.01, 48000)
         it.get_end = lambda frames, sr: 60.0
-        it.signal_noise = lambda frames, sr, hop=281: []
+        it.signal_noise = (lambda frames, sr, hop=281, _s=signals: [it.Signal(*x) for x in (_s or [])])
         it.load_model_meta = lambda p: metas[Path(p).parent.name]
         it.load_model = lambda p, meta: FakeModel(Path(p).parent.name)
         it.get_spect = lambda data, *a, **k: np.zeros((1,), np.float32)
@@ -235,10 +249,11 @@ def gen_postproc():
             os.chdir(str(REF.parent) if species_file else d)
             try:
                 np.random.seed(seed)
-                res = analyse.species_identify(str(rec), models, True)
+                res = analyse.species_identify(str(rec), models, signals is None)
             finally:
                 os.chdir(cwd)
         out_json[name] = {"meta": meta, "models": ["model1", "model2", "premodel"], "seed": seed,
+                          "signals": signals,
                           "species_file": species_file, "n_calls": calls["n"],
                           "result": json.loads(json.dumps(res, sort_keys=True))}
     with open(OUT / "postproc.json", "w") as f:
@@ -254,12 +269,42 @@ def gen_postproc():
         json.dump(subset, f, indent=1, sort_keys=True)
 
 
+def gen_tracks():
+    import identify_tracks as it
+    freqs = np.fft.rfftfreq(n=4096, d=1.0 / 48000)
+    cases = []
+    for seed in range(40):
+        rng = np.random.default_rng(1000 + seed)
+        n = int(rng.integers(0, 30))
+        end = float(rng.choice([60.0, 59.7, 30.0]))
+        sigs = []
+        for _ in range(n):
+            left = int(rng.integers(0, int(end * 48000 / 281)))
+            width = int(rng.integers(28, 600))
+            top = int(rng.integers(0, 1200))
+            height = int(rng.integers(10, 400))
+            if rng.random() < 0.3 and sigs:  # near-duplicates exercise the merge rules
+                b = sigs[int(rng.integers(0, len(sigs)))]
+                left, top = b[0] + int(rng.integers(-40, 40)), max(0, b[1] + int(rng.integers(-20, 20)))
+                left = max(0, left)
+            sigs.append((left, top, width, height))
+        inp = [[l * 281 / 48000, (l + w) * 281 / 48000, float(freqs[t]), float(freqs[min(2048, t + h)])]
+               for (l, t, w, h) in sigs]
+        tr = it.get_tracks_from_signals([it.Signal(*a) for a in inp], end)
+        cases.append({"end": end, "signals": inp,
+                      "tracks": [[float(x.start), float(x.end), float(x.freq_start), float(x.freq_end)]
+                                 for x in tr]})
+    with open(OUT / "tracks.json", "w") as f:
+        json.dump(cases, f, indent=1)
+
+
 def main():
     install_shims()
     gen_mel()
     gen_normalize()
     gen_windows()
     gen_postproc()
+    gen_tracks()
     print("wrote", sorted(p.name for p in OUT.glob("*.npz")) + sorted(p.name for p in OUT.glob("*.json")))
 
 

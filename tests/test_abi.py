@@ -13,7 +13,7 @@ HEADER = Path(__file__).resolve().parent.parent / "include" / "aa.h"
 
 def declared():
     text = HEADER.read_text()
-    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(aa_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|size_t|const char\*)\s+(aa_\w+)\s*\(", text, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -30,6 +30,7 @@ def test_abi_version_and_struct_sizes():
     assert C.sizeof(_lib.Window) == 16
     assert C.sizeof(_lib.Layer) == 6 * 4 + 4 * 8
     assert C.sizeof(_lib.FeConfig) == 11 * 4
+    assert C.sizeof(_lib.SnConfig) == 32 and C.sizeof(_lib.SnComponent) == 24
 
 
 def test_invalid_arguments_fail_without_gpu():
@@ -42,3 +43,21 @@ def test_invalid_arguments_fail_without_gpu():
     assert rc == 3 and b"n_fft" in L.aa_last_error()
     assert L.aa_model_create(None, 0, None, 0, 1, 1, 1, 0, C.byref(h)) == 1
     assert L.aa_fe_run(None, None, 0, None, 0, None, None, None, 0, None) == 1
+    sc = _lib.SnConfig(sr=48000, n_fft=2048, hop_length=281, signal_width=0.25, freq_range=100.0)
+    assert L.aa_sn_create(C.byref(sc), C.byref(h)) == 3 and b"n_fft" in L.aa_last_error()
+    assert L.aa_sn_run(None, None, 0, None, 0, None, 0, None, None, None) == 1
+
+
+def test_signal_geometry_matches_reference_arithmetic():
+    """width / height / filter thresholds of src/identify_tracks.py:673-691
+    (host-side plan values; no GPU call)."""
+    from oracle.signal_oracle import signal_geometry
+    L = _lib.lib()
+    for sr, hop in [(48000, 281), (44100, 281), (16000, 281), (96000, 281), (48000, 640)]:
+        sc = _lib.SnConfig(sr=sr, n_fft=4096, hop_length=hop, signal_width=0.25, freq_range=100.0)
+        g = (C.c_int32 * 6)()
+        assert L.aa_sn_geometry(C.byref(sc), g) == 0
+        width, height, _ = signal_geometry(sr, hop)
+        dh, dw = (height, width) if height and width else (3, 3)
+        eh, ew = (height // 10, width) if height // 10 and width else (3, 3)
+        assert tuple(g) == (dh, dw, eh, ew, int(0.65 * width) + 1, height - height // 10 + 1)

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from aa_amd import analyse, pipeline
-from aa_amd.identify_tracks import MAX_FRQUENCY, Signal
+from aa_amd.identify_tracks import MAX_FRQUENCY, Signal, get_tracks_from_signals
 from aa_amd.windows import schedule
 
 G = Path(__file__).parent / "golden"
@@ -26,11 +26,15 @@ PROBS = np.load(G / "postproc_probs.npz")
 
 def _classify_from_golden(name, case, metas):
     def fake(file_name, bird_models, analyse_tracks, meta_data=None):
-        tracks = []
-        for t in meta_data["Tracks"]:
-            s = Signal(t["start"], t["end"], t.get("minFreq", 0), t.get("maxFreq", MAX_FRQUENCY))
-            s.track_id = t["id"]
-            tracks.append(s)
+        signals = [Signal(*x) for x in (case.get("signals") or [])]
+        if analyse_tracks:
+            tracks = []
+            for t in meta_data["Tracks"]:
+                s = Signal(t["start"], t["end"], t.get("minFreq", 0), t.get("maxFreq", MAX_FRQUENCY))
+                s.track_id = t["id"]
+                tracks.append(s)
+        else:  # built from the signals exactly as classify() does (:434-437)
+            tracks = get_tracks_from_signals([s.copy() for s in signals], 60.0)
         groups = [[metas[m] for m in case["models"] if not metas[m]["pre_model"]],
                   [metas[m] for m in case["models"] if metas[m]["pre_model"]]]
         np.random.seed(case["seed"])
@@ -51,7 +55,7 @@ def _classify_from_golden(name, case, metas):
                 rows.append(np.mean(np.mean(per_model, axis=0), axis=0))
             pipeline.apply_group_scores(tracks, sel, np.asarray(rows, np.float32), g[0])
         assert call == case["n_calls"]
-        return tracks, 60.0, [], 60.0, ["bird", "kiwi", "whistler", "morepork"]
+        return tracks, 60.0, signals, 60.0, ["bird", "kiwi", "whistler", "morepork"]
     return fake
 
 
@@ -65,7 +69,7 @@ def test_species_identify_json_matches_reference(name, tmp_path, monkeypatch):
     monkeypatch.setenv("AA_EBIRD_SPECIES", str(G / "ebird_subset.json") if case["species_file"]
                        else str(tmp_path / "absent.json"))
     monkeypatch.setattr(analyse, "classify", _classify_from_golden(name, case, metas))
-    got = analyse.species_identify(str(rec), ["m1", "m2", "m3"], True)
+    got = analyse.species_identify(str(rec), ["m1", "m2", "m3"], case.get("signals") is None)
     assert json.dumps(got, sort_keys=True) == json.dumps(case["result"], sort_keys=True)
 
 
