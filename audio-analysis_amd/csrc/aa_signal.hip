@@ -11,10 +11,11 @@
 //                 over bins (radix select on the f32 bit patterns, values in
 //                 registers, an LDS histogram per wave) and the maximum.
 //   sn_transpose  S -> ST[bin][frame] (64 x 64 tiles through LDS)
-//   sn_select     per-bin median over frames: radix select over the contiguous
-//                 (L2-resident) ST row, both middle elements for an even count
-//   sn_mask       (S/a > 3 colmed/a) & (S/a > 3 rowmed/a) in numpy's f32
-//                 arithmetic (:656-669), bit-packed along time by ballot
+//   sn_select     per-bin median over frames: radix select over the ST row
+//                 (staged in LDS), both middle elements for an even count
+//   sn_thresholds 3 colmed/a per frame, 3 rowmed/a per bin (numpy's f32 steps)
+//   sn_mask       (S/a > 3 colmed/a) & (S/a > 3 rowmed/a) (:656-669),
+//                 bit-packed along time by ballot
 //   sn_morph_h/v  cv2 erode / dilate with rectangles (:670-684), separable,
 //                 64 frames per 64-bit word
 //   sn_runs, sn_unite, sn_stats, sn_emit
@@ -233,47 +234,84 @@ __global__ __launch_bounds__(256) void sn_transpose(const float* __restrict__ S,
 // ---------------------------------------------------------------------------
 // sn_select: numpy median of each row of X ([rows][ld], first n entries,
 // non-negative f32) as bit patterns: lo = element of rank (n - 1) / 2, hi =
-// element of rank n / 2 (equal for odd n).  One block per row; every pass
-// re-reads the row (L2-resident after the first).
+// element of rank n / 2 (equal for odd n).  One block per row.  The row is
+// staged in LDS when it fits (STAGE; otherwise every pass re-reads it from
+// L2).  Radix select on the bit patterns: the bits above the highest bit where
+// the row's min and max differ are common to every element, so the 8-bit
+// digits start there (fewer passes, and the first digit spreads over the
+// exponents actually present); one histogram per wave keeps the LDS atomics
+// of different waves off each other's counters.
 // ---------------------------------------------------------------------------
+constexpr int kSnStageMax = 12288;  // values staged in LDS (48 KiB)
+
+template <bool STAGE>
 __global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, int ld, int n, unsigned* __restrict__ lo,
                                                  unsigned* __restrict__ hi) {
-    __shared__ unsigned hist[kSnHist];
+    extern __shared__ unsigned srow[];
+    __shared__ unsigned hist[4][kSnHist];
     __shared__ unsigned pick[3];
-    __shared__ unsigned red[4];
-    const unsigned* row = reinterpret_cast<const unsigned*>(X) + (size_t)blockIdx.x * ld;
-    const int tid = threadIdx.x, lane = tid & 63;
-    unsigned prefix = 0, pmask = 0, rank = (unsigned)(n - 1) / 2, cnt = 0;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-        hist[tid] = 0;
+    __shared__ unsigned red[8];
+    const unsigned* grow = reinterpret_cast<const unsigned*>(X) + (size_t)blockIdx.x * ld;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    unsigned mn = 0xFFFFFFFFu, mx = 0;
+    for (int i = tid; i < n; i += 256) {
+        const unsigned v = grow[i];
+        if (STAGE) srow[i] = v;
+        mn = min(mn, v);
+        mx = max(mx, v);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if (lane == 0) { red[wv] = mn; red[4 + wv] = mx; }
+    __syncthreads();
+    mn = min(min(red[0], red[1]), min(red[2], red[3]));
+    mx = max(max(red[4], red[5]), max(red[6], red[7]));
+    const unsigned* row = STAGE ? srow : grow;
+    if (mn == mx) {  // block-uniform: a constant row
+        if (tid == 0) { lo[blockIdx.x] = mn; hi[blockIdx.x] = mn; }
+        return;
+    }
+    const int hb = 31 - __clz(mn ^ mx);  // highest bit that differs
+    unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
+    unsigned prefix = mn & pmask, rank = (unsigned)(n - 1) / 2, cnt = 0;
+    for (int s = hb - 7;; s -= 8) {
+        const int shift = max(s, 0);  // a last digit may repeat known prefix bits: harmless
+        reinterpret_cast<uint4*>(&hist[0][0])[tid] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
         for (int i = tid; i < n; i += 256) {
             const unsigned v = row[i];
-            if ((v & pmask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+            if ((v & pmask) == prefix) atomicAdd(&hist[wv][(v >> shift) & 255u], 1u);
         }
+        __syncthreads();
+        hist[0][tid] += hist[1][tid] + hist[2][tid] + hist[3][tid];
         __syncthreads();
         if (tid < 64) {
             unsigned below, c;
-            const unsigned dig = hist_pick(hist, rank, lane, &below, &c);
+            const unsigned dig = hist_pick(&hist[0][0], rank, lane, &below, &c);
             if (lane == 0) { pick[0] = dig; pick[1] = below; pick[2] = c; }
         }
         __syncthreads();
-        prefix |= pick[0] << shift;
+        prefix = (prefix & ~(255u << shift)) | (pick[0] << shift);
         pmask |= 255u << shift;
         rank -= pick[1];
         cnt = pick[2];
+        if (shift == 0) break;
     }
     // prefix is the rank-(n-1)/2 element, `rank` its place among the cnt equal ones
     unsigned second = prefix;
     if ((n & 1) == 0 && rank + 1 >= cnt) {  // block-uniform: rank n/2 is the next larger value
-        unsigned mn = 0xFFFFFFFFu;
+        unsigned m2 = 0xFFFFFFFFu;
         for (int i = tid; i < n; i += 256) {
             const unsigned v = row[i];
-            if (v > prefix) mn = min(mn, v);
+            if (v > prefix) m2 = min(m2, v);
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
-        if (lane == 0) red[tid >> 6] = mn;
+        for (int o = 32; o > 0; o >>= 1) m2 = min(m2, (unsigned)__shfl_xor((int)m2, o, 64));
+        __syncthreads();  // red[] reuse
+        if (lane == 0) red[wv] = m2;
         __syncthreads();
         second = min(min(red[0], red[1]), min(red[2], red[3]));
     }
@@ -284,32 +322,50 @@ __global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, in
 }
 
 // ---------------------------------------------------------------------------
-// sn_mask: bit f % 64 of word (b, f / 64) = S[b][f]/a > 3 colmed[f]/a and
-// S[b][f]/a > 3 rowmed[b], with a = max(S) and numpy's float32 rounding of
-// every step (:656-667; division is monotone, so the medians of S/a are the
-// quotients of S's middle elements, the even-count mean taken on quotients).
+// sn_thresholds: c3[f] = 3 * (colmed[f] / a) per frame and r3[b] = 3 *
+// rowmed_b per bin, in numpy's float32 rounding (:656-667).  Division is
+// monotone, so the medians of S / a are the quotients of S's middle elements;
+// an even count takes numpy's f32 mean of the two middle quotients.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sn_thresholds(const unsigned* __restrict__ gmax,
+                                                     const unsigned* __restrict__ colmed, int n_frames,
+                                                     const unsigned* __restrict__ rlo,
+                                                     const unsigned* __restrict__ rhi, float* __restrict__ c3,
+                                                     float* __restrict__ r3) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const float a = __uint_as_float(*gmax);
+    if (i < n_frames) c3[i] = __fmul_rn(3.f, __fdiv_rn(__uint_as_float(colmed[i]), a));
+    if (i < kSnBins) {
+        float dr = __fdiv_rn(__uint_as_float(rlo[i]), a);
+        if ((n_frames & 1) == 0) dr = __fmul_rn(__fadd_rn(dr, __fdiv_rn(__uint_as_float(rhi[i]), a)), 0.5f);
+        r3[i] = __fmul_rn(3.f, dr);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// sn_mask: bit f % 64 of word (b, f / 64) = S[b][f] / a > c3[f] and
+// S[b][f] / a > r3[b] (false throughout when a == 0: NaN quotients, like
+// numpy).  One block per bin row, each wave a run of 64-frame words, packed by
+// ballot.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void sn_mask(const float* __restrict__ ST, int ldt, int n_frames, int words,
-                                               const unsigned* __restrict__ gmax, const unsigned* __restrict__ colmed,
-                                               const unsigned* __restrict__ rlo, const unsigned* __restrict__ rhi,
-                                               unsigned long long* __restrict__ M) {
-    const int lane = threadIdx.x & 63;
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int b = blockIdx.y;
-    if (w >= words) return;
+                                               const unsigned* __restrict__ gmax, const float* __restrict__ c3,
+                                               const float* __restrict__ r3, unsigned long long* __restrict__ M) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b = blockIdx.x;
     const float a = __uint_as_float(*gmax);
-    float dr = __fdiv_rn(__uint_as_float(rlo[b]), a);
-    if ((n_frames & 1) == 0) dr = __fmul_rn(__fadd_rn(dr, __fdiv_rn(__uint_as_float(rhi[b]), a)), 0.5f);
-    const float r3 = __fmul_rn(3.f, dr);
-    const int f = 64 * w + lane;
-    bool bit = false;
-    if (f < n_frames) {
-        const float d = __fdiv_rn(ST[(size_t)b * ldt + f], a);
-        const float c3 = __fmul_rn(3.f, __fdiv_rn(__uint_as_float(colmed[f]), a));
-        bit = d > c3 && d > r3;  // false throughout when a == 0 (NaN quotients), like numpy
+    const float rb = r3[b];
+    const float* row = ST + (size_t)b * ldt;
+    for (int w = wv; w < words; w += 4) {
+        const int f = 64 * w + lane;
+        bool bit = false;
+        if (f < n_frames) {
+            const float d = __fdiv_rn(row[f], a);
+            bit = d > c3[f] && d > rb;
+        }
+        const unsigned long long m = __ballot(bit);
+        if (lane == 0) M[(size_t)b * words + w] = m;
     }
-    const unsigned long long m = __ballot(bit);
-    if (lane == 0) M[(size_t)b * words + w] = m;
 }
 
 // ---------------------------------------------------------------------------
@@ -547,6 +603,8 @@ struct SnWs {
     unsigned* colmed;
     unsigned* rlo;
     unsigned* rhi;
+    float* c3;
+    float* r3;
     unsigned* gmax;
     int* counters;  // [0] runs allocated, [1] status flags
     unsigned long long* M0;
@@ -582,6 +640,8 @@ static SnWs sn_ws_layout(const SnPlan& p, int F, char* base) {
     w.colmed = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * (size_t)F));
     w.rlo = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * kSnBins));
     w.rhi = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * kSnBins));
+    w.c3 = reinterpret_cast<float*>(take(sizeof(float) * (size_t)F));
+    w.r3 = reinterpret_cast<float*>(take(sizeof(float) * kSnBins));
     w.gmax = reinterpret_cast<unsigned*>(take(64));
     w.counters = reinterpret_cast<int*>(take(64));
     w.M0 = reinterpret_cast<unsigned long long*>(take(8 * (size_t)kSnBins * words));
@@ -764,10 +824,16 @@ extern "C" int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* 
     const int words = (F + 63) / 64, ldt = words * 64;
     hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST);
     AA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sn_select, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, ws.rlo, ws.rhi);
+    if (F <= kSnStageMax)
+        hipLaunchKernelGGL(sn_select<true>, dim3(kSnBins), dim3(256), sizeof(unsigned) * F, st, ws.ST, ldt, F, ws.rlo,
+                           ws.rhi);
+    else
+        hipLaunchKernelGGL(sn_select<false>, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, ws.rlo, ws.rhi);
     AA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sn_mask, dim3((words + 3) / 4, kSnBins), dim3(256), 0, st, ws.ST, ldt, F, words, ws.gmax,
-                       ws.colmed, ws.rlo, ws.rhi, ws.M0);
+    hipLaunchKernelGGL(sn_thresholds, dim3((std::max(F, kSnBins) + 255) / 256), dim3(256), 0, st, ws.gmax, ws.colmed, F,
+                       ws.rlo, ws.rhi, ws.c3, ws.r3);
+    AA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sn_mask, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, words, ws.gmax, ws.c3, ws.r3, ws.M0);
     AA_LAUNCH_CHECK();
     if (mask_out)
         AA_HIP(hipMemcpyAsync(mask_out, ws.M0, 8 * (size_t)kSnBins * words, hipMemcpyDeviceToDevice, st));
