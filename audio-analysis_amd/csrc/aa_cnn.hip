@@ -1034,7 +1034,11 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         m->st[0].skipped = 1;
         m->st[1].fused_first = 1;
         m->st[1].flops += m->st[0].flops;
-        m->st[1].bytes = 4.0 * m->st[0].Hin * m->st[0].Win + m->st[1].bytes - 0.0;
+        // the fused pair reads the first conv's f32 input and writes the
+        // second's output; the first conv's activations never reach HBM
+        const double es1 = (precision == AA_PREC_BF16) ? 2.0 : 4.0;
+        m->st[1].bytes = 4.0 * m->st[0].Hin * m->st[0].Win * m->st[0].cin +
+                         (m->st[1].bytes - es1 * m->st[1].Hin * m->st[1].Win * m->st[1].cin);
         m->st[1].name = m->st[0].name + "+" + m->st[1].name;
     }
     // ping-pong activation buffers: stage s writes buffer s % 2
