@@ -85,6 +85,26 @@ int main(int argc, char** argv) {
         X(bf16, 9, 3, 64, 3, 2, 2, 10, 4, 9, 33, true)
         AA_TRY(AA_BENCH)
 #undef AA_TRY
+        // candidate tilings of the small-K layers (c3: 3x3 32->64, c4: 3x3
+        // 64->64, c6: 1x3 128->256)
+#define AA_TRY2(X)                                         \
+        X(bf16, 3, 3, 32, 1, 4, 1, 2, 4, 8, 16, true)      \
+        X(bf16, 3, 3, 32, 1, 8, 1, 2, 4, 8, 32, true)      \
+        X(bf16, 3, 3, 32, 1, 4, 2, 4, 2, 8, 32, true)      \
+        X(bf16, 3, 3, 32, 1, 4, 1, 6, 4, 12, 32, true)     \
+        X(bf16, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true)      \
+        X(bf16, 3, 3, 64, 1, 4, 1, 2, 4, 8, 16, true)      \
+        X(bf16, 3, 3, 64, 1, 8, 1, 2, 4, 8, 32, true)      \
+        X(bf16, 3, 3, 64, 1, 4, 2, 4, 2, 8, 32, true)      \
+        X(bf16, 3, 3, 64, 1, 4, 1, 6, 4, 12, 32, true)     \
+        X(bf16, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)      \
+        X(bf16, 3, 3, 64, 1, 4, 1, 3, 4, 6, 32, true)      \
+        X(bf16, 1, 3, 128, 1, 1, 4, 9, 2, 6, 24, true)     \
+        X(bf16, 1, 3, 128, 1, 2, 2, 9, 2, 13, 20, true)    \
+        X(bf16, 1, 3, 128, 1, 1, 4, 5, 2, 4, 20, false)    \
+        X(bf16, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)
+        AA_TRY2(AA_BENCH)
+#undef AA_TRY2
     }
     // first conv (1 -> 32, VALU) fused into the 3x3/32 pool-3 stage, on a
     // 160 x 226 log-mel input
