@@ -105,6 +105,12 @@ int main(int argc, char** argv) {
         X(bf16, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)
         AA_TRY2(AA_BENCH)
 #undef AA_TRY2
+        {  // the 3x3/32 layer with the weight ring instead of register-resident weights
+            int H, W, C;
+            dims(3, 3, 32, 1, H, W, C);
+            printf("3x3/32 WREG off: %7.1f us\n",
+                   time_one<bf16, 3, 3, 32, 2, 2, 4, 2, 1, 8, 16, 256, true>(n, H, W, C, in, w, b, out, fc, it));
+        }
     }
     // first conv (1 -> 32, VALU) fused into the 3x3/32 pool-3 stage, on a
     // 160 x 226 log-mel input
@@ -123,8 +129,13 @@ int main(int argc, char** argv) {
            time_one<bf16, 3, 3, 32, 4, 1, 9, 2, 3, 12, 48, D, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
         AA_FUSED(0)
         if (pmc) return 0;
-        AA_FUSED(2) AA_FUSED(4) AA_FUSED(6)
+        AA_FUSED(2) AA_FUSED(4) AA_FUSED(6) AA_FUSED(256)
 #undef AA_FUSED
+#define AA_FT(MF, TH, TW)                                                                                  \
+    printf("fused c1+c2 MF%2d %2dx%2d: %7.1f us\n", MF, TH, TW,                                            \
+           time_one<bf16, 3, 3, 32, 4, 1, MF, 2, 3, TH, TW, 0, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
+        AA_FT(9, 12, 45) AA_FT(6, 6, 60) AA_FT(9, 9, 60) AA_FT(7, 9, 48) AA_FT(5, 6, 48) AA_FT(11, 12, 57)
+#undef AA_FT
     }
     // ablations of the 9x3 layer: staging / MFMA / stores / weight stream
     {
