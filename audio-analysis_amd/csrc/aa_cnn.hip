@@ -674,29 +674,24 @@ __global__ void track_mean(const float* __restrict__ probs, int n_models, long l
     const int t = blockIdx.x;
     const int c = threadIdx.x;
     if (c >= L) return;
-    constexpr int U = 16;  // loads in flight; the adds stay in numpy's order
+    constexpr int U = 40;  // loads in flight (a 60 s track has 39 windows); the adds stay in numpy's order
     float acc = 0.f;
     const int n = wc[t];
     const float* base = probs + (size_t)wb[t] * L + c;
     for (int w0 = 0; w0 < n; w0 += U) {
-        float v[U][4];
+        float m[U];  // per window: ((0 + p_0) + p_1) + ..., numpy's axis-0 sum over models
+#pragma unroll
+        for (int u = 0; u < U; ++u) m[u] = 0.f;
+        for (int k = 0; k < n_models; ++k) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = base[k * model_stride + (size_t)min(w0 + u, n - 1) * L];
+#pragma unroll
+            for (int u = 0; u < U; ++u) m[u] = __fadd_rn(m[u], v[u]);
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                v[u][k] = base[min(k, n_models - 1) * model_stride + (size_t)min(w0 + u, n - 1) * L];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (w0 + u < n) {
-                float m = 0.f;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (k < n_models) m = __fadd_rn(m, v[u][k]);
-                for (int k = 4; k < n_models; ++k)
-                    m = __fadd_rn(m, base[k * model_stride + (size_t)(w0 + u) * L]);
-                acc = __fadd_rn(acc, __fdiv_rn(m, (float)n_models));
-            }
-        }
+            if (w0 + u < n) acc = __fadd_rn(acc, __fdiv_rn(m[u], (float)n_models));
     }
     out[(size_t)t * L + c] = n > 0 ? __fdiv_rn(acc, (float)n) : NAN;
 }

@@ -730,9 +730,20 @@ __global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melF, con
     }
     const int ld = n_mels + 1;
     const float* src = melF + ((size_t)w * T + t0) * n_mels;  // nt contiguous frame rows
-    for (int idx = threadIdx.x; idx < nt * n_mels; idx += 256) {
-        const int tt = idx / n_mels, m = idx - tt * n_mels;
-        tile[tt * ld + m] = db_value(src[idx], ref_db, db_scale, amin, top_db);
+    const int total = nt * n_mels;
+    constexpr int U = 8;  // loads in flight per thread before any is consumed
+    for (int i0 = 0; i0 < total; i0 += U * 256) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[min(i0 + u * 256 + (int)threadIdx.x, total - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int idx = i0 + u * 256 + threadIdx.x;
+            if (idx < total) {
+                const int tt = idx / n_mels, m = idx - tt * n_mels;
+                tile[tt * ld + m] = db_value(v[u], ref_db, db_scale, amin, top_db);
+            }
+        }
     }
     __syncthreads();
     for (int idx = threadIdx.x; idx < n_mels * tile_t; idx += 256) {
@@ -1012,7 +1023,7 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
                            p->cfg.n_mels, p->T, p->cfg.db_scale, p->cfg.amin, p->cfg.top_db, ws.band_mean);
         AA_LAUNCH_CHECK();
     }
-    int tile_t = 64;  // frames per fe_db block: the [tile_t][n_mels + 1] tile within 64 KiB
+    int tile_t = 32;  // frames per fe_db block (the [tile_t][n_mels + 1] tile within 64 KiB)
     while (tile_t > 1 && (size_t)tile_t * (p->cfg.n_mels + 1) * 4 > 65536) tile_t >>= 1;
     hipLaunchKernelGGL(fe_db, dim3((p->T + tile_t - 1) / tile_t, n_win), dim3(256),
                        (size_t)tile_t * (p->cfg.n_mels + 1) * 4, st, ws.melS, ws.blkmax, p->nfblk, ws.stats,
