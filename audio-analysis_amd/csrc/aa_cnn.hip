@@ -599,7 +599,8 @@ template <typename T, int CIN, int MF, int NF>
 __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int HW,
                                                  const T* __restrict__ wt, const float* __restrict__ bias,
                                                  int L, int act, float alpha, int sigmoid,
-                                                 float* __restrict__ logits, float* __restrict__ probs) {
+                                                 float* __restrict__ logits, float* __restrict__ probs,
+                                                 float* __restrict__ part) {
     const int n = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q8 = 8 * (lane >> 4);
@@ -611,7 +612,7 @@ __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int H
 #pragma unroll
     for (int j = 0; j < NF; ++j) rmax[j] = -INFINITY;
     constexpr int CHUNK = 4 * MF * 16;
-    for (int p0 = 0; p0 < HW; p0 += CHUNK) {
+    for (int p0 = blockIdx.y * CHUNK; p0 < HW; p0 += CHUNK * gridDim.y) {
         f32x4 acc[MF][NF];
 #pragma unroll
         for (int i = 0; i < MF; ++i)
@@ -655,6 +656,12 @@ __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int H
         if (lane < 16) red[wave][j * 16 + lane] = v;
     }
     __syncthreads();
+    if (part) {  // one of gridDim.y pixel ranges: its column maxima, finished by head_final
+        if (threadIdx.x < 16 * NF)
+            part[((size_t)n * gridDim.y + blockIdx.y) * 16 * NF + threadIdx.x] =
+                fmaxf(fmaxf(red[0][threadIdx.x], red[1][threadIdx.x]), fmaxf(red[2][threadIdx.x], red[3][threadIdx.x]));
+        return;
+    }
     if (threadIdx.x < 16 * NF && (int)threadIdx.x < L) {
         const int c = threadIdx.x;
         float v = fmaxf(fmaxf(red[0][c], red[1][c]), fmaxf(red[2][c], red[3][c]));
@@ -662,6 +669,21 @@ __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int H
         logits[(size_t)n * L + c] = v;
         if (probs) probs[(size_t)n * L + c] = sigmoid ? 1.f / (1.f + expf(-v)) : v;
     }
+}
+
+// global max over the head's pixel ranges, bias, activation, sigmoid
+__global__ __launch_bounds__(64) void head_final(const float* __restrict__ part, int nparts, int width,
+                                                 const float* __restrict__ bias, int L, int act, float alpha,
+                                                 int sigmoid, float* __restrict__ logits,
+                                                 float* __restrict__ probs) {
+    const int n = blockIdx.x, c = threadIdx.x;
+    if (c >= L) return;
+    const float* p = part + (size_t)n * nparts * width + c;
+    float v = p[0];
+    for (int k = 1; k < nparts; ++k) v = fmaxf(v, p[(size_t)k * width]);
+    v = apply_act(v + bias[c], act, alpha);
+    logits[(size_t)n * L + c] = v;
+    if (probs) probs[(size_t)n * L + c] = sigmoid ? 1.f / (1.f + expf(-v)) : v;
 }
 
 // ---------------------------------------------------------------------------
@@ -800,9 +822,16 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
     if (s.kind == ST_HEAD) {
         AA_CHECK(s.cin == 256 && s.cout_pad == 32, AA_ERR_UNSUPPORTED, "head %d->%d unsupported", s.cin,
                  s.cout);
-        hipLaunchKernelGGL((conv_head<T, 256, 4, 2>), dim3(n), dim3(256), 0, st, (const T*)in,
-                           s.Hin * s.Win, (const T*)s.d_w, s.d_b, s.cout, s.act, s.alpha, s.sigmoid,
-                           logits, probs);
+        // pixel ranges of 64 spread over blocks (a window alone is too little
+        // work for one block's dependent load chain); their column maxima go to
+        // the free ping-pong buffer `out` and head_final reduces them
+        const int HW = s.Hin * s.Win, parts = (HW + 63) / 64;
+        float* part = static_cast<float*>(out);
+        hipLaunchKernelGGL((conv_head<T, 256, 1, 2>), dim3(n, parts), dim3(256), 0, st, (const T*)in, HW,
+                           (const T*)s.d_w, s.d_b, s.cout, s.act, s.alpha, s.sigmoid, logits, probs, part);
+        AA_LAUNCH_CHECK();
+        hipLaunchKernelGGL(head_final, dim3(n), dim3(64), 0, st, part, parts, 32, s.d_b, s.cout, s.act, s.alpha,
+                           s.sigmoid, logits, probs);
         AA_LAUNCH_CHECK();
         return AA_OK;
     }
@@ -1042,6 +1071,13 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         if (s.skipped) continue;
         const size_t e = (size_t)s.Hout * s.Wout * s.cout;
         m->act_elems[k % 2] = std::max(m->act_elems[k % 2], e);
+    }
+    if (!m->st.empty() && m->st.back().kind == ST_HEAD) {  // the head's partial maxima use its free buffer
+        const Stage& h = m->st.back();
+        const size_t es = precision == AA_PREC_BF16 ? 2 : 4;
+        const size_t parts = ((size_t)h.Hin * h.Win + 63) / 64;
+        const size_t k = m->st.size() - 1;
+        m->act_elems[k % 2] = std::max(m->act_elems[k % 2], (parts * 32 * sizeof(float) + es - 1) / es);
     }
     *model = m;
     return AA_OK;
