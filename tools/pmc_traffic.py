@@ -56,6 +56,13 @@ def main():
     for (_, name, fk, dur), (_, _, wk, _) in zip(f, w):
         fb = 2.0 * fk * 1024.0
         wb = wk * 1024.0
+        if "head_final" in name and kernels:  # second launch of the head stage: one entry per stage
+            k = kernels[-1]
+            k["fetch_bytes"] += round(fb)
+            k["write_bytes"] += round(wb)
+            k["hbm_bytes"] += round(fb + wb)
+            k["dur_us_profiled"] = round(k["dur_us_profiled"] + dur, 2)
+            continue
         kernels.append({"name": name[:120], "fetch_bytes": round(fb), "write_bytes": round(wb),
                         "hbm_bytes": round(fb + wb), "dur_us_profiled": round(dur, 2)})
     json.dump({"workload": WORKLOAD, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
