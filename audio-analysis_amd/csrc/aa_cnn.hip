@@ -315,9 +315,9 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
         // (b) first conv: wave -> 8 output channels (wave-uniform, so its 72
         // weights and 8 biases are scalar loads), lane -> one patch column; the
         // lane slides the 3x3 window down its column (3 new LDS reads per
-        // output row) and computes channel pairs with packed FMAs.  Per
-        // channel the arithmetic is the same f32 fma chain (taps in order,
-        // then + bias) as conv_small.  Activation as max(v, a v): the planner
+        // output row) and computes channel pairs with packed FMAs, each f32
+        // chain started at the bias (only the bf16 path fuses; the f32 parity
+        // mode runs conv_small).  Activation as max(v, a v): the planner
         // fuses only when the activation has 0 <= a <= 1 (none: 1, relu: 0).
         static_assert(NTHR == 256 && PW <= 64, "fused first layer: 4 waves, patch width <= 64");
         const int cg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -343,9 +343,9 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
             for (int r = 0; r < PH; ++r) {
 #pragma unroll
                 for (int j = 0; j < 3; ++j) xr[(r + 2) % 3][j] = X[(r + 2) * XW + col + j];
-                f32x2 acc[4];
+                f32x2 acc[4];  // the bias starts the chain (bf16 path only: f32 parity runs conv_small)
 #pragma unroll
-                for (int k = 0; k < 4; ++k) acc[k] = f32x2{0.f, 0.f};
+                for (int k = 0; k < 4; ++k) acc[k] = b1[k];
 #pragma unroll
                 for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -358,7 +358,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                 float o[8];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const f32x2 v = acc[k] + b1[k];
+                    const f32x2 v = acc[k];
                     const f32x2 sv = v * ae;
                     o[2 * k] = fmaxf(v.x, sv.x);
                     o[2 * k + 1] = fmaxf(v.y, sv.y);
