@@ -7,9 +7,10 @@
 //                 wave FFT (aa_wavefft.h).  The real split yields every bin:
 //                 the lane holding Z[k] and its mirror Z[2048 - k] forms
 //                 X[k] = E + W^k O and X[2048 - k] = conj(E - W^k O).  Writes
-//                 the frame-major magnitude S[f][0..2048], the frame's median
-//                 over bins (radix select on the f32 bit patterns, values in
-//                 registers, an LDS histogram per wave) and the maximum.
+//                 the frame-major magnitude S[f][0..2048] and the maximum.
+//   sn_colmed     the frame's median over bins: radix select on the f32 bit
+//                 patterns of the S row, values in registers, digits below the
+//                 row's common min/max prefix, 4 LDS histograms per wave
 //   sn_transpose  S -> ST[bin][frame] (64 x 64 tiles through LDS)
 //   sn_select     per-bin median over frames: radix select over the ST row
 //                 (staged in LDS), both middle elements for an even count
@@ -32,7 +33,7 @@
 
 namespace aa {
 
-constexpr int kSnWpb = 8;      // waves per sn_stft block (1 block per CU: 2 waves per SIMD)
+constexpr int kSnWpb = 4;      // waves per sn_stft block (3 blocks per CU: 3 waves per SIMD)
 constexpr int kSnBins = 2049;  // n_fft / 2 + 1
 constexpr int kSnLd = 2080;    // S row stride in floats (128-B aligned rows)
 constexpr int kSnHist = 256;   // radix-select buckets (8 bits per pass)
@@ -88,19 +89,17 @@ __device__ __forceinline__ unsigned hist_pick(const unsigned* hist, unsigned ran
 // ---------------------------------------------------------------------------
 // sn_stft: one wave per frame, persistent over frames (XCD-contiguous ranges
 // of frames like fe_stft_mel_4096: neighbouring frames share 4096 - hop
-// samples through one L2).  Register budget 256 (2 waves per SIMD): the wave
-// FFT, the 2-bin split and the 33-value select need ~180 VGPRs; at the
-// 128-VGPR budget of 4 waves per SIMD they spill.
+// samples through one L2).  Register budget 168 (3 waves per SIMD): the wave
+// FFT and the 2-bin split need ~170 VGPRs; at the 128-VGPR budget of 4 waves
+// per SIMD they spill heavily.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(2, 2))) void sn_stft(
+__global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(3, 3))) void sn_stft(
     const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const float2* __restrict__ tw,
-    const float2* __restrict__ tw4096, float* __restrict__ S, unsigned* __restrict__ colmed,
-    unsigned* __restrict__ gmax) {
+    const float2* __restrict__ tw4096, float* __restrict__ S, unsigned* __restrict__ gmax) {
     extern __shared__ float lds[];
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     float2* wb = reinterpret_cast<float2*>(lds) + wave * kHalf;
-    unsigned* hist = reinterpret_cast<unsigned*>(reinterpret_cast<float2*>(lds) + kSnWpb * kHalf) + wave * kSnHist;
     const int k1 = lane >> 1, h = lane & 1;
     float2 t1 = tw[lane];                 // W2048^c
     float2 t8 = tw[(8 * lane) & 2047];    // W2048^(8c)
@@ -165,7 +164,7 @@ __global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(2, 
         wave_sync();
         if (lane == 1) P[31] = mid;
         wave_sync();
-        // ---- the frame's row of S, its maximum and its median over bins ----
+        // ---- the frame's row of S and its maximum ----
         // bin lane + 64 i sits at float lb - 128 i (i < 16) / hb + 128 i (i >= 16)
         unsigned v[33];  // v[32] = bin 2048 (counted by lane 0)
         {
@@ -186,28 +185,87 @@ __global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
         for (int i = 0; i < 32; ++i) wmax = max(wmax, v[i]);
         wmax = max(wmax, v[32]);
-        unsigned prefix = 0, pmask = 0, rank = kSnBins / 2;
-#pragma unroll 1
-        for (int shift = 24; shift >= 0; shift -= 8) {
-            reinterpret_cast<uint4*>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
-            wave_sync();
-#pragma unroll
-            for (int i = 0; i < 33; ++i)
-                if ((i < 32 || lane == 0) && (v[i] & pmask) == prefix) atomicAdd(&hist[(v[i] >> shift) & 255u], 1u);
-            wave_sync();
-            unsigned below, cnt;
-            const unsigned dig = hist_pick(hist, rank, lane, &below, &cnt);
-            prefix |= dig << shift;
-            pmask |= 255u << shift;
-            rank -= below;
-            wave_sync();
-        }
-        if (lane == 0) colmed[fi] = prefix;
         wave_sync();  // the buffer is rewritten by the next frame
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (unsigned)__shfl_xor((int)wmax, o, 64));
     if (lane == 0 && wmax) atomicMax(gmax, wmax);
+}
+
+// ---------------------------------------------------------------------------
+// sn_colmed: the median over bins of every frame (numpy, odd count 2049: the
+// middle element) by radix select, one wave per S row: the row's 2049 values
+// in registers (33 per lane), 8-bit digits counted in a per-wave LDS histogram.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, int n_frames,
+                                                 unsigned* __restrict__ colmed) {
+    // per wave 4 copies of the histogram (lane & 3 picks one): a frame's
+    // values crowd a few buckets, and same-address LDS atomics serialise
+    __shared__ unsigned hists[4][4][kSnHist];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int fi = blockIdx.x * 4 + wv;
+    if (fi >= n_frames) return;  // wave-uniform
+    unsigned* hist = hists[wv][0];
+    unsigned* myh = hists[wv][lane & 3];
+    const unsigned* row = reinterpret_cast<const unsigned*>(S) + (size_t)fi * kSnLd;
+    unsigned v[33];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = row[lane + 64 * i];
+    v[32] = row[2048];  // counted by lane 0 only
+    // digits start below the bits the row's min and max share (a spectrum
+    // spans a few binades: the first histogram then spreads over the exponents
+    // present instead of piling onto a handful of counters)
+    unsigned mn = v[0], mx = v[0];
+#pragma unroll
+    for (int i = 1; i < 32; ++i) {
+        mn = min(mn, v[i]);
+        mx = max(mx, v[i]);
+    }
+    if (lane == 0) {
+        mn = min(mn, v[32]);
+        mx = max(mx, v[32]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if (mn == mx) {
+        if (lane == 0) colmed[fi] = mn;
+        return;
+    }
+    const int hb = 31 - __clz(mn ^ mx);
+    unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
+    unsigned prefix = mn & pmask, rank = kSnBins / 2;
+#pragma unroll 1
+    for (int sh = hb - 7;; sh -= 8) {
+        const int shift = max(sh, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(hists[wv][q])[lane] = make_uint4(0u, 0u, 0u, 0u);
+        wave_sync();
+#pragma unroll
+        for (int i = 0; i < 33; ++i)
+            if ((i < 32 || lane == 0) && (v[i] & pmask) == prefix) atomicAdd(&myh[(v[i] >> shift) & 255u], 1u);
+        wave_sync();
+        {  // fold the copies into copy 0 (lane owns buckets 4 lane .. 4 lane + 3)
+            uint4 t = reinterpret_cast<uint4*>(hists[wv][0])[lane];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                const uint4 u = reinterpret_cast<uint4*>(hists[wv][q])[lane];
+                t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+            }
+            reinterpret_cast<uint4*>(hist)[lane] = t;
+        }
+        wave_sync();
+        unsigned below, cnt;
+        const unsigned dig = hist_pick(hist, rank, lane, &below, &cnt);
+        prefix = (prefix & ~(255u << shift)) | (dig << shift);
+        pmask |= 255u << shift;
+        rank -= below;
+        wave_sync();
+        if (shift == 0) break;
+    }
+    if (lane == 0) colmed[fi] = prefix;
 }
 
 // ---------------------------------------------------------------------------
@@ -810,16 +868,18 @@ extern "C" int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* 
     hipStream_t st = static_cast<hipStream_t>(stream);
     AA_HIP(hipMemsetAsync(ws.gmax, 0, 64, st));
     AA_HIP(hipMemsetAsync(n_out, 0, 2 * sizeof(int32_t), st));
-    const size_t lds = sizeof(float2) * kSnWpb * kHalf + sizeof(unsigned) * kSnWpb * kSnHist;
+    const size_t lds = sizeof(float2) * kSnWpb * kHalf;
     static bool attr_set = false;
     if (!attr_set) {
         AA_HIP(hipFuncSetAttribute((const void*)sn_stft, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr_set = true;
     }
-    int grid = std::min((F + kSnWpb - 1) / kSnWpb, 256);  // persistent: 1 block per CU
+    int grid = std::min((F + kSnWpb - 1) / kSnWpb, 256 * 3);  // persistent: 3 blocks per CU
     grid = (grid + 7) & ~7;
     hipLaunchKernelGGL(sn_stft, dim3(grid), dim3(64 * kSnWpb), lds, st, pcm, (int)n_samples, p->cfg.hop_length, F,
-                       p->d_tw, p->d_tw4096, ws.S, ws.colmed, ws.gmax);
+                       p->d_tw, p->d_tw4096, ws.S, ws.gmax);
+    AA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sn_colmed, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, F, ws.colmed);
     AA_LAUNCH_CHECK();
     const int words = (F + 63) / 64, ldt = words * 64;
     hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST);
