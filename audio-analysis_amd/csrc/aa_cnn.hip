@@ -34,6 +34,7 @@ namespace aa {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __bf16 bf16;
 
 // ---- 8-element fragments and the MFMA step over one 32-deep K chunk -------
@@ -259,6 +260,34 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
     const int oh0 = th * TH, ow0 = tw * TW;
     constexpr int PH = TH + KH - 1, PW = TW + KW - 1;
 
+    // The first NB - 1 weight slices of the K loop's LDS ring (described
+    // there) are issued before the patch is staged, so their L2 round trip
+    // overlaps the staging instead of following it.
+    const int wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int NTAP = KH * KW;
+    constexpr int CPC = CIN / 32;
+    constexpr int NW = WM * WN;
+    constexpr int NB = conv_ring<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>();
+    constexpr int SLICE = BN * CSTR;                               // elements
+    constexpr int SLICE_LDS = conv_slice_lds_bytes<T, CIN, BN>();  // bytes
+    constexpr int GPS = SLICE_LDS / 1024;                          // wave-instructions per slice
+    constexpr int GHI = (GPS + NW - 1) / NW, GLO = GPS / NW;       // this wave's share: GHI if wave < GPS % NW
+    char* Bs = smem + conv_b_offset<T, KH, KW, CIN, TH, TW, FUSED>();
+    const size_t tap_stride = (size_t)gridDim.y * SLICE;
+    const T* wsl = wt + (size_t)blockIdx.y * SLICE + (threadIdx.x & 63) * VEC;
+#define AA_GLDS(t)                                                                                       \
+    _Pragma("unroll") for (int u_ = 0; u_ < GHI; ++u_) {                                               \
+        const int g_ = u_ * NW + wave0;                                                                  \
+        if (GPS % NW == 0 || g_ < GPS)                                                                  \
+            __builtin_amdgcn_global_load_lds(                                                           \
+                (const __attribute__((address_space(1))) void*)(wsl + (size_t)(t) * tap_stride + g_ * (1024 / sizeof(T))), \
+                (__attribute__((address_space(3))) void*)(Bs + ((t) % NB) * SLICE_LDS + g_ * 1024), 16, 0, 0); \
+    }
+    if constexpr (!(DIAG & 32)) {
+#pragma unroll
+        for (int t = 0; t < NB - 1; ++t) AA_GLDS(t)
+    }
+
     // ---- stage the input patch ----
     if constexpr (DIAG & 1) {
     } else if constexpr (!FUSED) {
@@ -312,70 +341,126 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                 if (idx < XN) X[idx] = fc.has_mag ? powf(v[u], fc.mag_exp) : v[u];
             }
         }
-        // (b) first conv: wave -> 8 output channels (wave-uniform, so its 72
-        // weights and 8 biases are scalar loads), lane -> one patch column; the
-        // lane slides the 3x3 window down its column (3 new LDS reads per
-        // output row) and computes channel pairs with packed FMAs, each f32
-        // chain started at the bias (only the bf16 path fuses; the f32 parity
-        // mode runs conv_small).  Activation as max(v, a v): the planner
-        // fuses only when the activation has 0 <= a <= 1 (none: 1, relu: 0).
-        static_assert(NTHR == 256 && PW <= 64, "fused first layer: 4 waves, patch width <= 64");
-        const int cg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const int col = threadIdx.x & 63;
-        f32x2 w1[9][4];
-        f32x2 b1[4];
+        if constexpr (sizeof(T) == 2) {
+            // (b) first conv on the matrix cores: per 32 patch pixels one
+            // v_mfma_f32_32x32x16_bf16, D[32 ch][32 px] = W[32 ch][16 k] X[16 k][32 px]
+            // with the 9 taps in k (0..8; weights 0 for k = 9..15, so those
+            // B entries may hold any finite value), the bias as the C input,
+            // then the activation, bf16, and 8-byte stores of 4 channels into
+            // the patch.  Lane l: pixel l % 32, k-group / channel quad l / 32.
+            // (bf16 path only: the f32 parity mode runs conv_small.)
+            const int wave1 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            const int l32 = threadIdx.x & 31, kg = (threadIdx.x >> 5) & 1;
+            bf16x8 wa;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            b1[k] = f32x2{fc.b[cg * 8 + 2 * k], fc.b[cg * 8 + 2 * k + 1]};
+            for (int j = 0; j < 8; ++j) {
+                const int tap = 8 * kg + j;
+                wa[j] = tap < 9 ? (bf16)fc.w[l32 * 9 + tap] : (bf16)0.f;
+            }
+            f32x16 cb;  // D row (channel) of register r: 8 (r / 4) + 4 kg + r % 4
 #pragma unroll
-            for (int t = 0; t < 9; ++t)
-                w1[t][k] = f32x2{fc.w[(cg * 8 + 2 * k) * 9 + t], fc.w[(cg * 8 + 2 * k + 1) * 9 + t]};
-        }
-        const float ae = fc.alpha;  // host: act folded to a slope in [0, 1]
-        __syncthreads();
-        if (col < PW) {
-            float xr[3][3];
+            for (int r = 0; r < 16; ++r) cb[r] = fc.b[8 * (r >> 2) + 4 * kg + (r & 3)];
+            const float ae = fc.alpha;  // host: act folded to a slope in [0, 1]
+            // tap offsets into X: k = 8 kg + j; k-group 1 only needs tap 8 (j = 0)
+            const int off0 = kg ? 2 * XW + 2 : 0;
+            __syncthreads();
+            constexpr int NPX = PH * PW;
+            for (int g = wave1; g * 32 < NPX; g += 4) {
+                const int pix = min(g * 32 + l32, NPX - 1);
+                const int r = pix / PW, c = pix - r * PW;
+                const float* xp = X + r * XW + c;
+                float xv[8];
+                xv[0] = xp[off0];
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int j = 1; j < 8; ++j) xv[j] = xp[(j / 3) * XW + j % 3];
+                // the log-mel as bf16 hi + lo (x - hi, exact in f32): two MFMAs
+                // keep ~16 significant bits of the input
+                bf16x8 xh, xl;
 #pragma unroll
-                for (int j = 0; j < 3; ++j) xr[i][j] = X[i * XW + col + j];
-#pragma unroll
-            for (int r = 0; r < PH; ++r) {
-#pragma unroll
-                for (int j = 0; j < 3; ++j) xr[(r + 2) % 3][j] = X[(r + 2) * XW + col + j];
-                f32x2 acc[4];  // the bias starts the chain (bf16 path only: f32 parity runs conv_small)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) acc[k] = b1[k];
-#pragma unroll
-                for (int i = 0; i < 3; ++i)
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) {
-                        const float xv = xr[(r + i) % 3][j];
-#pragma unroll
-                        for (int k = 0; k < 4; ++k)
-                            acc[k] = __builtin_elementwise_fma(f32x2{xv, xv}, w1[i * 3 + j][k], acc[k]);
-                    }
-                float o[8];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const f32x2 v = acc[k];
-                    const f32x2 sv = v * ae;
-                    o[2 * k] = fmaxf(v.x, sv.x);
-                    o[2 * k + 1] = fmaxf(v.y, sv.y);
+                for (int j = 0; j < 8; ++j) {
+                    xh[j] = (bf16)xv[j];
+                    xl[j] = (bf16)(xv[j] - (float)xh[j]);
                 }
-                T* dst = patch + (r * PW + col) * CSTR + cg * 8;
-                if constexpr (sizeof(T) == 2) {
-                    bf16x8 v;
+                f32x16 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xh, cb, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xl, d, 0, 0, 0);
+                if (g * 32 + l32 < NPX) {
+                    T* dst = patch + pix * CSTR + 4 * kg;
 #pragma unroll
-                    for (int ch = 0; ch < 8; ++ch) v[ch] = (bf16)o[ch];
-                    *reinterpret_cast<bf16x8*>(dst) = v;
-                } else {
-                    reinterpret_cast<float4*>(dst)[0] = make_float4(o[0], o[1], o[2], o[3]);
-                    reinterpret_cast<float4*>(dst)[1] = make_float4(o[4], o[5], o[6], o[7]);
+                    for (int q = 0; q < 4; ++q) {
+                        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                        bf16x4 o;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) o[e] = (bf16)fmaxf(d[4 * q + e], d[4 * q + e] * ae);
+                        *reinterpret_cast<bf16x4*>(dst + 8 * q) = o;
+                    }
+                }
+            }
+        } else {
+            // (b) first conv: wave -> 8 output channels (wave-uniform, so its 72
+            // weights and 8 biases are scalar loads), lane -> one patch column; the
+            // lane slides the 3x3 window down its column (3 new LDS reads per
+            // output row) and computes channel pairs with packed FMAs, each f32
+            // chain started at the bias (only the bf16 path fuses; the f32 parity
+            // mode runs conv_small).  Activation as max(v, a v): the planner
+            // fuses only when the activation has 0 <= a <= 1 (none: 1, relu: 0).
+            static_assert(NTHR == 256 && PW <= 64, "fused first layer: 4 waves, patch width <= 64");
+            const int cg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            const int col = threadIdx.x & 63;
+            f32x2 w1[9][4];
+            f32x2 b1[4];
+    #pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                b1[k] = f32x2{fc.b[cg * 8 + 2 * k], fc.b[cg * 8 + 2 * k + 1]};
+    #pragma unroll
+                for (int t = 0; t < 9; ++t)
+                    w1[t][k] = f32x2{fc.w[(cg * 8 + 2 * k) * 9 + t], fc.w[(cg * 8 + 2 * k + 1) * 9 + t]};
+            }
+            const float ae = fc.alpha;  // host: act folded to a slope in [0, 1]
+            __syncthreads();
+            if (col < PW) {
+                float xr[3][3];
+    #pragma unroll
+                for (int i = 0; i < 2; ++i)
+    #pragma unroll
+                    for (int j = 0; j < 3; ++j) xr[i][j] = X[i * XW + col + j];
+    #pragma unroll
+                for (int r = 0; r < PH; ++r) {
+    #pragma unroll
+                    for (int j = 0; j < 3; ++j) xr[(r + 2) % 3][j] = X[(r + 2) * XW + col + j];
+                    f32x2 acc[4];  // the bias starts the chain (bf16 path only: f32 parity runs conv_small)
+    #pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[k] = b1[k];
+    #pragma unroll
+                    for (int i = 0; i < 3; ++i)
+    #pragma unroll
+                        for (int j = 0; j < 3; ++j) {
+                            const float xv = xr[(r + i) % 3][j];
+    #pragma unroll
+                            for (int k = 0; k < 4; ++k)
+                                acc[k] = __builtin_elementwise_fma(f32x2{xv, xv}, w1[i * 3 + j][k], acc[k]);
+                        }
+                    float o[8];
+    #pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const f32x2 v = acc[k];
+                        const f32x2 sv = v * ae;
+                        o[2 * k] = fmaxf(v.x, sv.x);
+                        o[2 * k + 1] = fmaxf(v.y, sv.y);
+                    }
+                    T* dst = patch + (r * PW + col) * CSTR + cg * 8;
+                    if constexpr (sizeof(T) == 2) {
+                        bf16x8 v;
+    #pragma unroll
+                        for (int ch = 0; ch < 8; ++ch) v[ch] = (bf16)o[ch];
+                        *reinterpret_cast<bf16x8*>(dst) = v;
+                    } else {
+                        reinterpret_cast<float4*>(dst)[0] = make_float4(o[0], o[1], o[2], o[3]);
+                        reinterpret_cast<float4*>(dst)[1] = make_float4(o[4], o[5], o[6], o[7]);
+                    }
                 }
             }
         }
-    }
+        }
     __syncthreads();
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -406,29 +491,6 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
     // flight), one barrier publishes slice t to every wave and retires all
     // reads of the buffer slice t + NB - 1 will overwrite, then that slice is
     // issued.  A fragments come from the staged patch. ----
-    constexpr int NTAP = KH * KW;
-    constexpr int CPC = CIN / 32;
-    constexpr int NW = WM * WN;
-    constexpr int NB = conv_ring<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>();
-    constexpr int SLICE = BN * CSTR;                               // elements
-    constexpr int SLICE_LDS = conv_slice_lds_bytes<T, CIN, BN>();  // bytes
-    constexpr int GPS = SLICE_LDS / 1024;                          // wave-instructions per slice
-    constexpr int GHI = (GPS + NW - 1) / NW, GLO = GPS / NW;       // this wave's share: GHI if wave < GPS % NW
-    char* Bs = smem + conv_b_offset<T, KH, KW, CIN, TH, TW, FUSED>();
-    const size_t tap_stride = (size_t)gridDim.y * SLICE;
-    const T* wsl = wt + (size_t)blockIdx.y * SLICE + lane * VEC;
-#define AA_GLDS(t)                                                                                       \
-    _Pragma("unroll") for (int u_ = 0; u_ < GHI; ++u_) {                                               \
-        const int g_ = u_ * NW + wave;                                                                  \
-        if (GPS % NW == 0 || g_ < GPS)                                                                  \
-            __builtin_amdgcn_global_load_lds(                                                           \
-                (const __attribute__((address_space(1))) void*)(wsl + (size_t)(t) * tap_stride + g_ * (1024 / sizeof(T))), \
-                (__attribute__((address_space(3))) void*)(Bs + ((t) % NB) * SLICE_LDS + g_ * 1024), 16, 0, 0); \
-    }
-    if constexpr (!(DIAG & 32)) {
-#pragma unroll
-        for (int t = 0; t < NB - 1; ++t) AA_GLDS(t)
-    }
     const int brow = (wn * NF * 16 + (lane & 15)) * CSTR + q8;
     const bool hi_share = (GPS % NW == 0) || wave < GPS % NW;
     // Fragments are double-buffered in registers: while chunk q's MFMAs run,
