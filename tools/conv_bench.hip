@@ -82,7 +82,11 @@ int main(int argc, char** argv) {
         X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 15, 24, true)     \
         X(bf16, 9, 3, 64, 3, 4, 2, 4, 4, 6, 33, true)      \
         X(bf16, 9, 3, 64, 3, 4, 1, 5, 8, 9, 33, true)      \
-        X(bf16, 9, 3, 64, 3, 2, 2, 10, 4, 9, 33, true)
+        X(bf16, 9, 3, 64, 3, 2, 2, 10, 4, 9, 33, true)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true)      \
+        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 21, 18, true)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 18, 21, true)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 5, 4, 15, 21, true)
         AA_TRY(AA_BENCH)
 #undef AA_TRY
         // candidate tilings of the small-K layers (c3: 3x3 32->64, c4: 3x3
@@ -99,6 +103,13 @@ int main(int argc, char** argv) {
         X(bf16, 3, 3, 64, 1, 4, 1, 6, 4, 12, 32, true)     \
         X(bf16, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)      \
         X(bf16, 3, 3, 64, 1, 4, 1, 3, 4, 6, 32, true)      \
+        X(bf16, 3, 3, 32, 1, 2, 2, 6, 2, 10, 18, true)     \
+        X(bf16, 3, 3, 64, 1, 2, 2, 6, 2, 10, 18, true)     \
+        X(bf16, 3, 3, 32, 1, 2, 2, 8, 2, 10, 24, true)     \
+        X(bf16, 3, 3, 64, 1, 2, 2, 8, 2, 10, 24, true)     \
+        X(bf16, 3, 3, 32, 1, 4, 2, 6, 2, 10, 36, true)     \
+        X(bf16, 3, 3, 64, 1, 4, 2, 6, 2, 10, 36, true)     \
+        X(bf16, 3, 3, 64, 1, 2, 2, 6, 2, 25, 6, true)      \
         X(bf16, 1, 3, 128, 1, 1, 4, 9, 2, 6, 24, true)     \
         X(bf16, 1, 3, 128, 1, 2, 2, 9, 2, 13, 20, true)    \
         X(bf16, 1, 3, 128, 1, 1, 4, 5, 2, 4, 20, false)    \
