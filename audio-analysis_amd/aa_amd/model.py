@@ -127,7 +127,7 @@ class Model(_lib.StageTiming):
             raise
         layers, blob = layer_table(arch, tensors)
         self.in_shape = tuple(int(v) for v in in_shape)  # (H, W, C)
-        prec = {"f32": _lib.AA_PREC_F32, "bf16": _lib.AA_PREC_BF16}[precision]
+        prec = {"f32": _lib.AA_PREC_F32, "bf16": _lib.AA_PREC_BF16, "fp8": _lib.AA_PREC_FP8}[precision]
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             _lib.check(_lib.lib().aa_model_create(layers, len(layers), blob.ctypes.data, blob.size,

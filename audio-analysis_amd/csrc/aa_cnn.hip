@@ -36,6 +36,18 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __bf16 bf16;
+// OCP e4m3fn byte (gfx950's fp8; not the MI300 fnuz encoding)
+struct fp8 {
+    uint8_t v;
+};
+
+// 4 / 8 floats -> e4m3fn bytes, round to nearest even, saturated to +-448
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+    const float M = 448.f;
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(a, -M), M), fminf(fmaxf(b, -M), M), 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(c, -M), M), fminf(fmaxf(d, -M), M), w, true);
+    return (uint32_t)w;
+}
 
 // ---- 8-element fragments and the MFMA step over one 32-deep K chunk -------
 template <typename T>
@@ -44,6 +56,11 @@ template <>
 struct Frag<bf16> {
     bf16x8 v;
     __device__ __forceinline__ void load(const bf16* p) { v = *reinterpret_cast<const bf16x8*>(p); }
+};
+template <>
+struct Frag<fp8> {
+    long v;
+    __device__ __forceinline__ void load(const fp8* p) { v = *reinterpret_cast<const long*>(p); }
 };
 template <>
 struct Frag<float> {
@@ -60,6 +77,11 @@ struct Frag<float> {
 __device__ __forceinline__ f32x4 mfma_chunk(const Frag<bf16>& a, const Frag<bf16>& b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, c, 0, 0, 0);
 }
+// fp8: the same lane layout with 8 bytes per lane (non-scaled form: the bf16 rate,
+// half the staging and fragment bytes)
+__device__ __forceinline__ f32x4 mfma_chunk(const Frag<fp8>& a, const Frag<fp8>& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a.v, b.v, c, 0, 0, 0);
+}
 // f32: sub-step s feeds k = 8(l>>4) + s into the instruction's k slot (l>>4),
 // identically for A and B, so the 8 instructions cover the 32-chunk exactly.
 __device__ __forceinline__ f32x4 mfma_chunk(const Frag<float>& a, const Frag<float>& b, f32x4 c) {
@@ -74,6 +96,8 @@ template <>
 __device__ __forceinline__ float to_t<float>(float x) { return x; }
 template <>
 __device__ __forceinline__ bf16 to_t<bf16>(float x) { return (bf16)x; }
+template <>
+__device__ __forceinline__ fp8 to_t<fp8>(float x) { return fp8{(uint8_t)(pack4_fp8(x, 0.f, 0.f, 0.f) & 0xff)}; }
 
 enum { ACT_NONE = 0, ACT_LEAKY = 1, ACT_RELU = 2 };
 __device__ __forceinline__ float apply_act(float v, int act, float alpha) {
@@ -121,7 +145,10 @@ __global__ __launch_bounds__(256) void conv_small(const float* __restrict__ in, 
             for (int t = 0; t < KH * KW; ++t) s = fmaf(x[t], sw[(c0 + c) * KH * KW + t], s);
             r[c] = apply_act(s + sb[c0 + c], act, alpha);
         }
-        if constexpr (sizeof(TO) == 2) {
+        if constexpr (sizeof(TO) == 1) {
+            *reinterpret_cast<uint2*>(o + c0) =
+                make_uint2(pack4_fp8(r[0], r[1], r[2], r[3]), pack4_fp8(r[4], r[5], r[6], r[7]));
+        } else if constexpr (sizeof(TO) == 2) {
             bf16x8 v;
 #pragma unroll
             for (int c = 0; c < 8; ++c) v[c] = (bf16)r[c];
@@ -139,11 +166,12 @@ __global__ __launch_bounds__(256) void conv_small(const float* __restrict__ in, 
 // ---------------------------------------------------------------------------
 // Padded row length (elements) of the staged patch and of the weight slices:
 // bf16 rows padded by 32 B (stride = 2 mod 4 16-B units, which makes every
-// ds_read_b128 lane group of the fragment reads conflict-free); f32 (parity
-// mode) keeps a 16-B pad.
+// ds_read_b128 lane group of the fragment reads conflict-free); fp8 rows
+// padded by 16 B (48 / 80 / 144-B strides put the 16 rows of a ds_read_b64
+// half-wave on distinct 4-bank groups); f32 (parity mode) keeps a 16-B pad.
 template <typename T>
 __host__ __device__ constexpr int conv_cstr(int cin) {
-    return cin + (sizeof(T) == 2 ? 16 : 4);
+    return cin + (sizeof(T) == 1 ? 16 : sizeof(T) == 2 ? 16 : 4);
 }
 
 // LDS of one conv_mfma block: [staged patch][f32 log-mel patch if FUSED]
@@ -341,7 +369,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                 if (idx < XN) X[idx] = fc.has_mag ? powf(v[u], fc.mag_exp) : v[u];
             }
         }
-        if constexpr (sizeof(T) == 2) {
+        if constexpr (sizeof(T) <= 2) {
             // (b) first conv on the matrix cores: per 32 patch pixels one
             // v_mfma_f32_32x32x16_bf16, D[32 ch][32 px] = W[32 ch][16 k] X[16 k][32 px]
             // with the 9 taps in k (0..8; weights 0 for k = 9..15, so those
@@ -387,11 +415,18 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                     T* dst = patch + pix * CSTR + 4 * kg;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                        bf16x4 o;
+                        if constexpr (sizeof(T) == 1) {
+                            float o[4];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) o[e] = (bf16)fmaxf(d[4 * q + e], d[4 * q + e] * ae);
-                        *reinterpret_cast<bf16x4*>(dst + 8 * q) = o;
+                            for (int e = 0; e < 4; ++e) o[e] = fmaxf(d[4 * q + e], d[4 * q + e] * ae);
+                            *reinterpret_cast<uint32_t*>(dst + 8 * q) = pack4_fp8(o[0], o[1], o[2], o[3]);
+                        } else {
+                            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                            bf16x4 o;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) o[e] = (bf16)fmaxf(d[4 * q + e], d[4 * q + e] * ae);
+                            *reinterpret_cast<bf16x4*>(dst + 8 * q) = o;
+                        }
                     }
                 }
             }
@@ -512,7 +547,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
         _Pragma("unroll") for (int j = 0; j < NF; ++j) dst[j].load(bt_ + j * 16 * CSTR);   \
     }
     // f32 (parity mode) fragments are twice as wide: single-buffered there
-    constexpr bool DB = sizeof(T) == 2;
+    constexpr bool DB = sizeof(T) <= 2;
     if constexpr (DB) AA_LOAD_A(fa, 0, 0)
     for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); ++t) {
         // slices t+1 .. min(t+NB-2, NTAP-1) may stay in flight
@@ -572,12 +607,16 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
     // output channels c0 .. c0 + 3 of pixel p, stored as one 8-byte (bf16) /
     // 16-byte (f32) vector per fragment
     ET* E = reinterpret_cast<ET*>(smem);
+    // fp8: per-output-channel dequantisation scales follow the bias (both padded to cout_pad)
+    const float* wscale = bias + gridDim.y * BN;
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
         const int c0 = wn * NF * 16 + j * 16 + 4 * (lane >> 4);
-        float bj[4];
+        float bj[4], sj[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) bj[r] = EBF16 ? bias[blockIdx.y * BN + c0 + r] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sj[r] = (EBF16 && sizeof(T) == 1) ? wscale[blockIdx.y * BN + c0 + r] : 1.f;
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             const int p = (wm * MF + i) * 16 + (lane & 15);
@@ -587,7 +626,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                     typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
                     bf16x4 v;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = (bf16)(acc[i][j][r] + bj[r]);
+                    for (int r = 0; r < 4; ++r) v[r] = (bf16)(sizeof(T) == 1 ? fmaf(acc[i][j][r], sj[r], bj[r]) : acc[i][j][r] + bj[r]);
                     *reinterpret_cast<bf16x4*>(e) = v;
                 } else {
                     *reinterpret_cast<float4*>(e) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
@@ -605,9 +644,11 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
     const int oh0s = oh0 / POOL, ow0s = ow0 / POOL;
     const int col = (threadIdx.x % G) * 8;
     const int ch0 = blockIdx.y * BN + col;
-    float bv[8];
+    float bv[8], sv[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) bv[c] = EBF16 ? 0.f : bias[ch0 + c];  // bias is padded to cout_pad
+#pragma unroll
+    for (int c = 0; c < 8; ++c) sv[c] = (!EBF16 && sizeof(T) == 1) ? wscale[ch0 + c] : 1.f;
     T* dst = out + (size_t)n * Hout * Wout * cout_store;
     for (int q = threadIdx.x / G; q < PHo * PWo; q += NTHR / G) {
         const int pr = q / PWo, pc = q - (q / PWo) * PWo;
@@ -632,13 +673,15 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
             }
         if (gh >= Hout || gw >= Wout) continue;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = apply_act(v[c] + bv[c], act, alpha);
+        for (int c = 0; c < 8; ++c) v[c] = apply_act((!EBF16 && sizeof(T) == 1) ? fmaf(v[c], sv[c], bv[c]) : v[c] + bv[c], act, alpha);
         if constexpr ((DIAG & 4) != 0) {
             if (v[0] != 12345.f) continue;  // keep the values live, store (almost) never
         }
         T* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
         if (ch0 + 8 <= cout_store) {
-            if constexpr (sizeof(T) == 2) {
+            if constexpr (sizeof(T) == 1) {
+                *reinterpret_cast<uint2*>(o) = make_uint2(pack4_fp8(v[0], v[1], v[2], v[3]), pack4_fp8(v[4], v[5], v[6], v[7]));
+            } else if constexpr (sizeof(T) == 2) {
                 bf16x8 pk;
 #pragma unroll
                 for (int c = 0; c < 8; ++c) pk[c] = (bf16)v[c];
@@ -662,7 +705,7 @@ __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int H
                                                  const T* __restrict__ wt, const float* __restrict__ bias,
                                                  int L, int act, float alpha, int sigmoid,
                                                  float* __restrict__ logits, float* __restrict__ probs,
-                                                 float* __restrict__ part) {
+                                                 float* __restrict__ part, const float* __restrict__ wscale) {
     const int n = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q8 = 8 * (lane >> 4);
@@ -727,7 +770,7 @@ __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int H
     if (threadIdx.x < 16 * NF && (int)threadIdx.x < L) {
         const int c = threadIdx.x;
         float v = fmaxf(fmaxf(red[0][c], red[1][c]), fmaxf(red[2][c], red[3][c]));
-        v = apply_act(v + bias[c], act, alpha);
+        v = apply_act(wscale ? fmaf(v, wscale[c], bias[c]) : v + bias[c], act, alpha);
         logits[(size_t)n * L + c] = v;
         if (probs) probs[(size_t)n * L + c] = sigmoid ? 1.f / (1.f + expf(-v)) : v;
     }
@@ -737,13 +780,13 @@ __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int H
 __global__ __launch_bounds__(64) void head_final(const float* __restrict__ part, int nparts, int width,
                                                  const float* __restrict__ bias, int L, int act, float alpha,
                                                  int sigmoid, float* __restrict__ logits,
-                                                 float* __restrict__ probs) {
+                                                 float* __restrict__ probs, const float* __restrict__ wscale) {
     const int n = blockIdx.x, c = threadIdx.x;
     if (c >= L) return;
     const float* p = part + (size_t)n * nparts * width + c;
     float v = p[0];
     for (int k = 1; k < nparts; ++k) v = fmaxf(v, p[(size_t)k * width]);
-    v = apply_act(v + bias[c], act, alpha);
+    v = apply_act(wscale ? fmaf(v, wscale[c], bias[c]) : v + bias[c], act, alpha);
     logits[(size_t)n * L + c] = v;
     if (probs) probs[(size_t)n * L + c] = sigmoid ? 1.f / (1.f + expf(-v)) : v;
 }
@@ -852,16 +895,27 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     X(bf16, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)           \
     X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true)           \
     X(bf16, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)         \
+    X(fp8, 3, 3, 32, 3, 4, 1, 9, 2, 12, 48, true)           \
+    X(fp8, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true)            \
+    X(fp8, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)            \
+    X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true)            \
+    X(fp8, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)          \
     X(float, 3, 3, 32, 3, 2, 2, 9, 1, 6, 48, false)         \
     X(float, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false)         \
     X(float, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false)         \
     X(float, 9, 3, 64, 3, 1, 4, 7, 1, 3, 33, false)         \
     X(float, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)
 
+template <typename T>
+constexpr int prec_of() {
+    return sizeof(T) == 1 ? AA_PREC_FP8 : sizeof(T) == 2 ? AA_PREC_BF16 : AA_PREC_F32;
+}
+static size_t prec_bytes(int prec) { return prec == AA_PREC_FP8 ? 1 : prec == AA_PREC_BF16 ? 2 : 4; }
+
 // output channels per block of the instantiation serving this stage (0: none)
 static int mfma_bn(int prec, int kh, int kw, int cin, int pool) {
 #define AA_BN(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB)                                       \
-    if ((prec == AA_PREC_BF16) == (sizeof(T_) == 2) && kh == KH && kw == KW && cin == CIN && pool == POOL) \
+    if (prec_of<T_>() == prec && kh == KH && kw == KW && cin == CIN && pool == POOL) \
         return WN * NF * 16;
     AA_CONV_CFGS(AA_BN)
 #undef AA_BN
@@ -889,11 +943,12 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
         // the free ping-pong buffer `out` and head_final reduces them
         const int HW = s.Hin * s.Win, parts = (HW + 63) / 64;
         float* part = static_cast<float*>(out);
+        const float* hsc = sizeof(T) == 1 ? s.d_b + s.cout_pad : nullptr;  // fp8 dequantisation scales
         hipLaunchKernelGGL((conv_head<T, 256, 1, 2>), dim3(n, parts), dim3(256), 0, st, (const T*)in, HW,
-                           (const T*)s.d_w, s.d_b, s.cout, s.act, s.alpha, s.sigmoid, logits, probs, part);
+                           (const T*)s.d_w, s.d_b, s.cout, s.act, s.alpha, s.sigmoid, logits, probs, part, hsc);
         AA_LAUNCH_CHECK();
         hipLaunchKernelGGL(head_final, dim3(n), dim3(64), 0, st, part, parts, 32, s.d_b, s.cout, s.act, s.alpha,
-                           s.sigmoid, logits, probs);
+                           s.sigmoid, logits, probs, hsc);
         AA_LAUNCH_CHECK();
         return AA_OK;
     }
@@ -937,6 +992,27 @@ static uint16_t f2bf(float f) {  // round to nearest even
     return (uint16_t)(u >> 16);
 }
 
+// f32 -> OCP e4m3fn byte, round to nearest even, saturated to +-448 (the
+// device's v_cvt_pk_fp8_f32 conversion of the same value)
+static uint8_t f2fp8(float f) {
+    const uint8_t sgn = std::signbit(f) ? 0x80 : 0;
+    double a = std::fabs((double)f);
+    if (std::isnan(f)) return 0x7f;
+    if (a >= 448.0) return sgn | 0x7e;
+    if (a < std::ldexp(1.0, -6)) {  // subnormal: multiples of 2^-9
+        const int q = (int)std::nearbyint(a * 512.0);
+        return sgn | (uint8_t)q;  // q == 8 is the smallest normal's encoding
+    }
+    int ex;
+    std::frexp(a, &ex);  // a = m 2^ex, m in [0.5, 1)
+    const int e = ex - 1;
+    double q = std::nearbyint(std::ldexp(a, 3 - e));  // 8 .. 16
+    int ee = e;
+    if (q >= 16.0) { q = 8.0; ++ee; }
+    if (ee > 8 || (ee == 8 && q > 14.0)) return sgn | 0x7e;
+    return sgn | (uint8_t)(((ee + 7) << 3) | ((int)q - 8));
+}
+
 }  // namespace aa
 
 using namespace aa;
@@ -944,7 +1020,7 @@ using namespace aa;
 extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const float* blob, int64_t blob_len,
                                int32_t in_h, int32_t in_w, int32_t in_c, int32_t precision, void** model) {
     AA_CHECK(layers && blob && model && n_layers > 0, AA_ERR_INVALID, "aa_model_create: null argument");
-    AA_CHECK(precision == AA_PREC_F32 || precision == AA_PREC_BF16, AA_ERR_INVALID,
+    AA_CHECK(precision == AA_PREC_F32 || precision == AA_PREC_BF16 || precision == AA_PREC_FP8, AA_ERR_INVALID,
              "aa_model_create: precision %d", precision);
     auto get = [&](int64_t off, int64_t n) -> const float* {
         if (off < 0 || off + n > blob_len) return nullptr;
@@ -1056,9 +1132,12 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         // its LDS image) plus 1 KiB of slack for the last slice's rounding;
         // the 1x1 head [cout_pad][C_in]
         const bool bf = (precision == AA_PREC_BF16) && s.kind != ST_SMALL;
-        const int cstr = s.kind == ST_MFMA ? (bf ? conv_cstr<bf16>(s.cin) : conv_cstr<float>(s.cin)) : s.cin;
+        const bool f8 = (precision == AA_PREC_FP8) && s.kind != ST_SMALL;
+        const int wes = bf ? 2 : f8 ? 1 : 4;
+        const int cstr = s.kind == ST_MFMA ? (bf ? conv_cstr<bf16>(s.cin) : f8 ? conv_cstr<fp8>(s.cin) : conv_cstr<float>(s.cin))
+                                           : s.cin;
         const int ntap = s.kh * s.kw;
-        const size_t slack = s.kind == ST_MFMA ? 1024 / (bf ? 2 : 4) : 0;
+        const size_t slack = s.kind == ST_MFMA ? 1024 / wes : 0;
         std::vector<float> wpk(s.kind == ST_SMALL ? (size_t)s.cout * K : (size_t)ntap * s.cout_pad * cstr + slack, 0.f);
         for (int o = 0; o < s.cout; ++o)
             for (int k = 0; k < K; ++k) {
@@ -1070,12 +1149,30 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                     wpk[((size_t)t * s.cout_pad + o) * cstr + c] = (float)v;
                 }
             }
-        std::vector<float> bias(s.cout_pad, 0.f);
+        // fp8: [bias | per-channel dequantisation scale], both cout_pad long
+        std::vector<float> bias(f8 ? 2 * s.cout_pad : s.cout_pad, 0.f);
         for (int o = 0; o < s.cout; ++o) bias[o] = (float)shift[o];
-        const size_t wbytes = wpk.size() * (bf ? 2 : 4);
+        const size_t wbytes = wpk.size() * wes;
         hipError_t e = hipMalloc(&s.d_w, wbytes);
         if (e == hipSuccess) {
-            if (bf) {
+            if (f8) {
+                // per output channel: the largest |w| maps to 240 (e4m3fn tops
+                // out at 448), the kernel's epilogue multiplies by amax / 240
+                std::vector<uint8_t> h(wpk.size(), 0);
+                for (int o = 0; o < s.cout_pad; ++o) {
+                    float amax = 0.f;
+                    for (int t = 0; t < ntap; ++t)
+                        for (int c = 0; c < s.cin; ++c) amax = std::max(amax, std::fabs(wpk[((size_t)t * s.cout_pad + o) * cstr + c]));
+                    const float sc = amax > 0.f ? 240.f / amax : 1.f;
+                    bias[s.cout_pad + o] = 1.f / sc;
+                    for (int t = 0; t < ntap; ++t)
+                        for (int c = 0; c < s.cin; ++c) {
+                            const size_t k = ((size_t)t * s.cout_pad + o) * cstr + c;
+                            h[k] = f2fp8(wpk[k] * sc);
+                        }
+                }
+                e = hipMemcpy(s.d_w, h.data(), wbytes, hipMemcpyHostToDevice);
+            } else if (bf) {
                 std::vector<uint16_t> h(wpk.size());
                 for (size_t k = 0; k < wpk.size(); ++k) h[k] = f2bf(wpk[k]);
                 e = hipMemcpy(s.d_w, h.data(), wbytes, hipMemcpyHostToDevice);
@@ -1083,15 +1180,15 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                 e = hipMemcpy(s.d_w, wpk.data(), wbytes, hipMemcpyHostToDevice);
             }
         }
-        if (e == hipSuccess) e = hipMalloc((void**)&s.d_b, sizeof(float) * s.cout_pad);
-        if (e == hipSuccess) e = hipMemcpy(s.d_b, bias.data(), sizeof(float) * s.cout_pad, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc((void**)&s.d_b, sizeof(float) * bias.size());
+        if (e == hipSuccess) e = hipMemcpy(s.d_b, bias.data(), sizeof(float) * bias.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) {
             m->st.push_back(s);
             fail(AA_ERR_HIP, hipGetErrorString(e));
             break;
         }
         s.flops = 2.0 * s.Hc * s.Wc * K * s.cout;
-        const double es = (precision == AA_PREC_BF16) ? 2.0 : 4.0;
+        const double es = (double)prec_bytes(precision);
         s.bytes = (s.kind == ST_SMALL ? 4.0 : es) * s.Hin * s.Win * s.cin +
                   (s.kind == ST_HEAD ? 4.0 * s.cout : es * s.Hout * s.Wout * s.cout);
         char nm[96];
@@ -1122,7 +1219,7 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         m->st[1].flops += m->st[0].flops;
         // the fused pair reads the first conv's f32 input and writes the
         // second's output; the first conv's activations never reach HBM
-        const double es1 = (precision == AA_PREC_BF16) ? 2.0 : 4.0;
+        const double es1 = (double)prec_bytes(precision);
         m->st[1].bytes = 4.0 * m->st[0].Hin * m->st[0].Win * m->st[0].cin +
                          (m->st[1].bytes - es1 * m->st[1].Hin * m->st[1].Win * m->st[1].cin);
         m->st[1].name = m->st[0].name + "+" + m->st[1].name;
@@ -1136,7 +1233,7 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
     }
     if (!m->st.empty() && m->st.back().kind == ST_HEAD) {  // the head's partial maxima use its free buffer
         const Stage& h = m->st.back();
-        const size_t es = precision == AA_PREC_BF16 ? 2 : 4;
+        const size_t es = prec_bytes(precision);
         const size_t parts = ((size_t)h.Hin * h.Win + 63) / 64;
         const size_t k = m->st.size() - 1;
         m->act_elems[k % 2] = std::max(m->act_elems[k % 2], (parts * 32 * sizeof(float) + es - 1) / es);
@@ -1157,7 +1254,7 @@ extern "C" int aa_model_n_outputs(const void* model) {
 extern "C" size_t aa_model_workspace_bytes(const void* model, int32_t max_batch) {
     if (!model || max_batch < 0) return 0;
     const Model* m = static_cast<const Model*>(model);
-    const size_t es = m->prec == AA_PREC_BF16 ? 2 : 4;
+    const size_t es = prec_bytes(m->prec);
     return align_up(m->act_elems[0] * es * max_batch, 256) + align_up(m->act_elems[1] * es * max_batch, 256);
 }
 
@@ -1169,7 +1266,7 @@ extern "C" int aa_model_forward(void* model, const float* x, int32_t n, float* l
     const size_t need = aa_model_workspace_bytes(m, n);
     AA_CHECK(workspace && workspace_bytes >= need, AA_ERR_WORKSPACE, "aa_model_forward: workspace %zu < %zu",
              workspace_bytes, need);
-    const size_t es = m->prec == AA_PREC_BF16 ? 2 : 4;
+    const size_t es = prec_bytes(m->prec);
     char* buf[2] = {static_cast<char*>(workspace),
                     static_cast<char*>(workspace) + align_up(m->act_elems[0] * es * n, 256)};
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1182,8 +1279,9 @@ extern "C" int aa_model_forward(void* model, const float* x, int32_t n, float* l
         hipEvent_t e0;
         int rc = m->timer.begin((int)k, st, &e0);
         if (rc != AA_OK) return rc;
-        rc = (m->prec == AA_PREC_BF16) ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st, first)
-                                       : launch_stage<float>(*m, s, in, out, logits, probs, n, st, first);
+        rc = m->prec == AA_PREC_BF16  ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st, first)
+             : m->prec == AA_PREC_FP8 ? launch_stage<fp8>(*m, s, in, out, logits, probs, n, st, first)
+                                      : launch_stage<float>(*m, s, in, out, logits, probs, n, st, first);
         if (rc != AA_OK) return rc;
         rc = m->timer.end((int)k, st, e0);
         if (rc != AA_OK) return rc;

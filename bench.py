@@ -36,7 +36,10 @@ METRIC = "audio-seconds classified/sec/GPU on 60 s mono; max|delta logit| vs CPU
 WINDOWS_PER_CLIP = 39
 SECONDS_PER_WINDOW = 60.0 / WINDOWS_PER_CLIP
 BATCH_A, BATCH_B = 39, 25
-PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s, MI355X_MICROARCH.md
+# dense MFMA TFLOP/s, MI355X_MICROARCH.md (fp8: the dtype's dense peak, reached
+# only by the block-scaled K=128 form; the non-scaled 16x16x32 fp8 MFMA the
+# kernels use issues at the bf16 rate)
+PEAK = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}
 VALU_F32_PEAK = 157.3                   # FP32 VALU TFLOP/s (fma counted as 2)
 HBM_PEAK_GBS = 8000.0
 WORKLOAD = ("config2: 64 windows/step (39 of clip A + 25 of clip B, 60 s 48 kHz mono), "
@@ -48,7 +51,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "fp8"],
+                    help="fp8: OCP e4m3fn CNN (BASELINE configs[4] precision; the front end stays f32)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bound on the CPU-baseline sample (0 disables)")
     ap.add_argument("--no-parity", action="store_true")
@@ -103,17 +107,18 @@ def cpu_baseline(pcm, views, model_path, fe_cfg, budget_s):
     return done * SECONDS_PER_WINDOW / dt, done, dt, threads, np.concatenate(logits)
 
 
-def load_traffic(n_dispatch):
+def load_traffic(n_dispatch, precision):
     """HBM bytes per launch of each kernel of one step, in dispatch order, from
     the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE summary of this same
     workload (tools/pmc_traffic.py; FETCH_SIZE doubled per
     MI355X_MICROARCH.md).  None when no summary of this workload exists."""
-    for path in sorted((ROOT / "profiles").glob("*/pmc_traffic.json"), reverse=True):
+    for path in sorted((ROOT / "profiles").glob("*/pmc_traffic*.json"), reverse=True):
         try:
             d = json.loads(path.read_text())
         except (OSError, ValueError):
             continue
-        if d.get("workload") == WORKLOAD and len(d.get("kernels", [])) == n_dispatch:
+        if (d.get("workload") == WORKLOAD and d.get("precision", "bf16") == precision
+                and len(d.get("kernels", [])) == n_dispatch):
             return d, path.relative_to(ROOT).as_posix()
     return None, None
 
@@ -299,7 +304,7 @@ def main():
     avg_s = dom_live["avg_ms"] * 1e-3
     achieved = (dom["bytes"] / avg_s / 1e9) if unit == "GB/s" else (dom["flops"] / avg_s / 1e12)
     traffic, traffic_src = None, None
-    tr, tr_path = load_traffic(len(launches) + 1) if S == 1 else (None, None)  # + track_mean
+    tr, tr_path = load_traffic(len(launches) + 1, args.precision) if S == 1 else (None, None)  # + track_mean
     if tr is not None:
         k = tr["kernels"][launches.index((dom["owner"], dom["idx"]))]
         traffic = k["hbm_bytes"]

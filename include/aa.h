@@ -128,6 +128,9 @@ typedef struct aa_layer {
 typedef enum aa_precision {
     AA_PREC_F32 = 0,  /* f32 MFMA (exact f32 fma chain): the parity mode */
     AA_PREC_BF16 = 1, /* bf16 activations/weights, f32 accumulation */
+    AA_PREC_FP8 = 2,  /* OCP e4m3fn activations/weights (per-output-channel weight
+                       * scales), f32 accumulation; f32 log-mel input, the first
+                       * conv on bf16 hi+lo as in AA_PREC_BF16 */
 } aa_precision;
 
 int aa_model_create(const aa_layer* layers, int32_t n_layers, const float* blob, int64_t blob_len,

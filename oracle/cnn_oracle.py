@@ -81,6 +81,77 @@ def forward(path_or_arch, x_nhwc: np.ndarray, dtype=torch.float32, tensors=None)
     return logits.cpu().numpy(), x.cpu().numpy()
 
 
+def _fp8(x):
+    """Round to OCP e4m3fn (nearest even, saturated to +-448), back to f32."""
+    return x.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).to(torch.float32)
+
+
+@torch.no_grad()
+def forward_fp8_emulated(path, x_nhwc: np.ndarray):
+    """CPU emulation of libaa's AA_PREC_FP8 numerics (the checker of that mode,
+    not a reference result): BN folded into the conv (per output channel), a
+    C_in = 1 first conv with bf16 weights on the f32 input, every later conv's
+    folded weights quantised per output channel to e4m3fn with the largest |w|
+    at 240 and dequantised after the f32 accumulation, pre-pool values rounded
+    to bf16 (the epilogue tile), every stored activation rounded to e4m3fn, f32
+    logits.  Returns (logits, probs)."""
+    arch, tensors = load_arch(path)
+    t = lambda k: torch.from_numpy(np.asarray(tensors[k])).to(torch.float64)
+    x = torch.from_numpy(np.ascontiguousarray(x_nhwc)).to(torch.float32).permute(0, 3, 1, 2)
+    i, logits = 0, None
+    while i < len(arch):
+        layer = arch[i]
+        kind, name = layer["type"], layer.get("name")
+        if kind == "magtransform":
+            x = torch.pow(x, torch.sigmoid(t(name + ".a").reshape(-1)[0].float()))
+            i += 1
+            continue
+        assert kind == "conv2d", kind
+        w = t(name + ".kernel").permute(3, 2, 0, 1)  # OIHW
+        cout = w.shape[0]
+        b = t(name + ".bias") if layer.get("use_bias", False) else torch.zeros(cout, dtype=torch.float64)
+        i += 1
+        if i < len(arch) and arch[i]["type"] == "batchnorm":
+            bn, nm = arch[i], arch[i]["name"]
+            sc = t(nm + ".gamma") / torch.sqrt(t(nm + ".moving_variance") + float(bn.get("eps", 1e-3)))
+            b = (b - t(nm + ".moving_mean")) * sc + t(nm + ".beta")
+            w = w * sc[:, None, None, None]
+            i += 1
+        w, b = w.float(), b.float()
+        first = w.shape[1] == 1
+        if first:
+            y = F.conv2d(x, w.to(torch.bfloat16).float(), b)
+        else:
+            amax = w.abs().amax(dim=(1, 2, 3))
+            s = torch.where(amax > 0, 240.0 / amax, torch.ones_like(amax))
+            wq = _fp8(w * s[:, None, None, None])
+            y = F.conv2d(x, wq) * (1.0 / s)[None, :, None, None] + b[None, :, None, None]
+        act, pool, head = None, None, False
+        while i < len(arch) and arch[i]["type"] in ("leakyrelu", "maxpool2d", "globalmaxpool2d", "activation"):
+            k = arch[i]["type"]
+            if k == "leakyrelu":
+                act = float(arch[i].get("alpha", 0.3))
+            elif k == "maxpool2d":
+                pool = tuple(arch[i]["pool"])
+            elif k == "globalmaxpool2d":
+                head = True
+            i += 1
+        if head:
+            logits = torch.amax(y, dim=(2, 3))
+            if act is not None:
+                logits = F.leaky_relu(logits, act)
+            x = torch.sigmoid(logits)
+            break
+        if not first:
+            y = y.to(torch.bfloat16).float()
+        if pool is not None:
+            y = F.max_pool2d(y, pool, pool)
+        if act is not None:
+            y = F.leaky_relu(y, act)
+        x = _fp8(y)
+    return logits.numpy(), x.numpy()
+
+
 def ensemble_track_mean(probs_per_model):
     """np.mean over models then over windows (src/identify_tracks.py:548-551)."""
     p = np.mean(probs_per_model, axis=0)

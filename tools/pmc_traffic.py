@@ -48,6 +48,7 @@ def last_step(ds):
 
 def main():
     fetch, write, out = sys.argv[1:4]
+    precision = sys.argv[4] if len(sys.argv) > 4 else "bf16"
     f = last_step(dispatches(fetch))
     w = last_step(dispatches(write))
     assert [x[1] for x in f] == [x[1] for x in w], "the two passes ran different kernels"
@@ -65,8 +66,9 @@ def main():
             continue
         kernels.append({"name": name[:120], "fetch_bytes": round(fb), "write_bytes": round(wb),
                         "hbm_bytes": round(fb + wb), "dur_us_profiled": round(dur, 2)})
-    json.dump({"workload": WORKLOAD, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
-               "bench.py --steps 3 --warmup 2; FETCH_SIZE x2 (gfx950 correction), KiB x 1024",
+    json.dump({"workload": WORKLOAD, "precision": precision,
+               "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
+               f"bench.py --precision {precision} --steps 3 --warmup 2; FETCH_SIZE x2 (gfx950 correction), KiB x 1024",
                "kernels": kernels}, open(out, "w"), indent=1)
     for k in kernels:
         print(f"{k['name'][:60]:60s} fetch {k['fetch_bytes']/1e6:8.2f} MB  write {k['write_bytes']/1e6:8.2f} MB")
