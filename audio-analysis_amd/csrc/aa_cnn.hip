@@ -890,15 +890,15 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
 // output channels per block.  The f32 rows are the parity mode (smaller
 // tiles: the same LDS budget holds half the elements).
 #define AA_CONV_CFGS(X)                                     \
-    X(bf16, 3, 3, 32, 3, 4, 1, 9, 2, 12, 48, true)          \
+    X(bf16, 3, 3, 32, 3, 4, 1, 6, 2, 18, 21, true)          \
     X(bf16, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true)           \
     X(bf16, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)           \
     X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true)           \
     X(bf16, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)         \
-    X(fp8, 3, 3, 32, 3, 4, 1, 9, 2, 12, 48, true)           \
+    X(fp8, 3, 3, 32, 3, 4, 1, 6, 2, 12, 30, true)           \
     X(fp8, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true)            \
     X(fp8, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)            \
-    X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true)            \
+    X(fp8, 9, 3, 64, 3, 2, 4, 11, 2, 39, 9, true)           \
     X(fp8, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)          \
     X(float, 3, 3, 32, 3, 2, 2, 9, 1, 6, 48, false)         \
     X(float, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false)         \

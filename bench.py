@@ -126,7 +126,7 @@ def load_traffic(n_dispatch, precision):
 def main_stream(args, world, rank, dev):
     """configs[2]: clips streamed through aa_amd.stream.StreamRunner (host PCM
     -> pinned staging -> copy stream, double-buffered against the kernels),
-    model1+model2+model3 bf16 sharing one front end; one 0-60 s track per clip
+    model1+model2+model3 (--precision, bf16 by default) sharing one front end; one 0-60 s track per clip
     (39 windows).  value = clips x 60 s over all ranks / max-over-ranks wall
     time, host->device transfer included."""
     from aa_amd.frontend import FeSettings
@@ -142,7 +142,7 @@ def main_stream(args, world, rank, dev):
     make_ensemble(root)
     paths = [root / m / "audioModel.safetensors" for m in ("model1", "model2", "model3")]
     pool = [synth.clip(1000 * rank + i) for i in range(8)]  # distinct PCM, cycled (host synthesis untimed)
-    runner = StreamRunner(paths, fe_s, precision="bf16", device=dev, max_windows=8 * WINDOWS_PER_CLIP,
+    runner = StreamRunner(paths, fe_s, precision=args.precision, device=dev, max_windows=8 * WINDOWS_PER_CLIP,
                           max_samples=8 * len(pool[0]))
 
     def clips(n):
@@ -167,7 +167,7 @@ def main_stream(args, world, rank, dev):
     out = {"metric": METRIC, "value": round(world * args.clips * 60.0 / elapsed, 1), "unit": "audio-s/s",
            "n_gpus": world, "steps": args.clips, "warmup": 32,
            "ms_per_step": round(1e3 * elapsed / args.clips, 4), "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "bf16",
+           "vs_baseline": None, "dtype": args.precision,
            "data": "synthetic (48 kHz int16-quantised noise+chirps, seeded), seeded random-init model1/2/3",
            "config": {"workload": "config3: 60 s clips streamed from host memory, 39 windows each, "
                                   "model1+model2+model3 ensemble, 8 clips per batch",

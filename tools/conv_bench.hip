@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 using namespace aa;
@@ -39,7 +40,10 @@ static float time_one(int n, int Hin, int Win, int cout, void* in, void* w, floa
 }
 
 int main(int argc, char** argv) {
-    const bool pmc = argc > 1;  // PMC runs: the model's configurations once each, no ablations
+    // "fp8": the fp8 candidate tilings only; any other argument: PMC runs (the
+    // model's configurations once each, no ablations)
+    const bool fp8mode = argc > 1 && std::string(argv[1]) == "fp8";
+    const bool pmc = argc > 1 && !fp8mode;
     const int n = 64;
     std::vector<uint16_t> h(200u << 20);  // 400 MB: larger than every layer's input
     for (auto& x : h) x = 0x3c00 + (rand() & 0x3ff);  // bf16 ~1..2 with random mantissa
@@ -72,8 +76,76 @@ int main(int argc, char** argv) {
                                                                                         out, fc, it);     \
         const double fl = 2.0 * n * (H - KH + 1) * (W - KW + 1) * KH * KW * CIN * C;                      \
         printf("%-6s %dx%d cin %3d pool %d  WM%d WN%d MF%d NF%d %2dx%2d  full %7.1f us (%6.1f TF)  only-mfma %7.1f us\n", \
-               sizeof(T_) == 2 ? "bf16" : "f32", KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, full,        \
+               sizeof(T_) == 1 ? "fp8" : sizeof(T_) == 2 ? "bf16" : "f32", KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, full,        \
                fl / full * 1e-6, mf);                                                                     \
+    }
+    if (fp8mode) {
+        for (auto& x : h) x = 0x3838;  // e4m3fn 0.5 pairs: finite activations and weights
+        (void)hipMemcpy(in, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+        (void)hipMemcpy(w, h.data(), 8u << 20, hipMemcpyHostToDevice);
+        (void)hipMemset(b, 0, 4096);
+#define AA_TRY8(X)                                        \
+        X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true)      \
+        X(fp8, 9, 3, 64, 3, 4, 2, 7, 4, 12, 33, true)     \
+        X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 21, 18, true)     \
+        X(fp8, 9, 3, 64, 3, 4, 2, 5, 4, 15, 21, true)     \
+        X(fp8, 9, 3, 64, 3, 4, 2, 8, 4, 51, 9, true)      \
+        X(fp8, 9, 3, 64, 3, 2, 4, 12, 2, 39, 9, true)     \
+        X(fp8, 9, 3, 64, 3, 2, 4, 12, 2, 21, 18, true)    \
+        X(fp8, 9, 3, 64, 3, 2, 4, 12, 2, 42, 9, true)     \
+        X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 42, 9, true)      \
+        X(fp8, 9, 3, 64, 3, 2, 4, 11, 2, 39, 9, true)     \
+        X(bf16, 9, 3, 64, 3, 2, 4, 11, 2, 39, 9, true)    \
+        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 42, 9, true)     \
+        X(bf16, 9, 3, 64, 3, 2, 4, 12, 2, 21, 18, true)   \
+        X(bf16, 9, 3, 64, 3, 2, 4, 12, 2, 39, 9, true)    \
+        X(fp8, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true)      \
+        X(fp8, 3, 3, 32, 1, 2, 2, 6, 2, 10, 18, true)     \
+        X(fp8, 3, 3, 32, 1, 4, 2, 6, 2, 10, 36, true)     \
+        X(fp8, 3, 3, 32, 1, 2, 2, 8, 2, 10, 24, true)     \
+        X(fp8, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)      \
+        X(fp8, 3, 3, 64, 1, 2, 2, 6, 2, 10, 18, true)     \
+        X(fp8, 3, 3, 64, 1, 4, 2, 6, 2, 10, 36, true)     \
+        X(fp8, 3, 3, 64, 1, 2, 2, 8, 2, 10, 24, true)     \
+        X(fp8, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)    \
+        X(fp8, 1, 3, 128, 1, 1, 4, 5, 2, 4, 20, false)    \
+        X(fp8, 1, 3, 128, 1, 2, 2, 9, 2, 13, 20, true)
+        AA_TRY8(AA_BENCH)
+#undef AA_TRY8
+        float* w1;
+        float* b1;
+        (void)hipMalloc(&w1, 32 * 9 * 4);
+        (void)hipMalloc(&b1, 32 * 4);
+        std::vector<float> hw(32 * 9, 0.05f), hb(32, 0.01f);
+        (void)hipMemcpy(w1, hw.data(), hw.size() * 4, hipMemcpyHostToDevice);
+        (void)hipMemcpy(b1, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
+        FirstConv f1{w1, b1, 1, 0.3f, 0, 1.f, 160, 226};
+        const int H = 158, W = 224;
+#define AA_FT8(MF, TH, TW)                                                                                 \
+    printf("fp8 fused c1+c2 MF%2d %2dx%2d: %7.1f us\n", MF, TH, TW,                                        \
+           time_one<fp8, 3, 3, 32, 4, 1, MF, 2, 3, TH, TW, 0, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
+        AA_FT8(9, 12, 48) AA_FT8(7, 9, 48) AA_FT8(6, 9, 42) AA_FT8(8, 9, 54) AA_FT8(5, 6, 51) AA_FT8(8, 12, 42)
+        AA_FT8(6, 6, 63) AA_FT8(7, 6, 72) AA_FT8(7, 12, 36) AA_FT8(9, 15, 36) AA_FT8(10, 15, 42) AA_FT8(8, 15, 33)
+        AA_FT8(6, 12, 30) AA_FT8(8, 12, 39) AA_FT8(5, 12, 24) AA_FT8(4, 12, 18) AA_FT8(5, 9, 33) AA_FT8(6, 9, 39)
+        AA_FT8(6, 15, 24) AA_FT8(5, 15, 21) AA_FT8(6, 18, 21) AA_FT8(6, 21, 18) AA_FT8(7, 24, 18) AA_FT8(5, 21, 15)
+        AA_FT8(6, 24, 15) AA_FT8(7, 27, 15) AA_FT8(7, 36, 12) AA_FT8(7, 39, 9) AA_FT8(5, 24, 12) AA_FT8(4, 18, 12)
+#undef AA_FT8
+        // the same fused candidates in bf16 (the LDS image is larger there)
+        for (auto& x : h) x = 0x3c00 + (rand() & 0x3ff);
+        (void)hipMemcpy(in, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+        (void)hipMemcpy(w, h.data(), 8u << 20, hipMemcpyHostToDevice);
+#define AA_FTB(MF, TH, TW)                                                                                 \
+    printf("bf16 fused c1+c2 MF%2d %2dx%2d: %7.1f us\n", MF, TH, TW,                                       \
+           time_one<bf16, 3, 3, 32, 4, 1, MF, 2, 3, TH, TW, 0, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
+        AA_FTB(9, 12, 48) AA_FTB(7, 9, 48) AA_FTB(6, 9, 42) AA_FTB(8, 9, 54) AA_FTB(5, 6, 51) AA_FTB(8, 12, 42)
+        AA_FTB(6, 6, 63) AA_FTB(7, 6, 72) AA_FTB(6, 12, 30) AA_FTB(8, 12, 39) AA_FTB(8, 15, 33) AA_FTB(7, 12, 36)
+        AA_FTB(5, 12, 24) AA_FTB(4, 12, 18) AA_FTB(5, 15, 21) AA_FTB(5, 9, 33) AA_FTB(4, 9, 24) AA_FTB(3, 6, 24)
+        AA_FTB(6, 18, 21) AA_FTB(6, 21, 18) AA_FTB(7, 24, 18) AA_FTB(6, 18, 18) AA_FTB(8, 24, 21) AA_FTB(4, 18, 12)
+        AA_FTB(5, 21, 15) AA_FTB(6, 24, 15) AA_FTB(7, 27, 15) AA_FTB(6, 30, 12) AA_FTB(7, 36, 12) AA_FTB(7, 39, 9)
+        AA_FTB(5, 39, 6) AA_FTB(8, 39, 12) AA_FTB(5, 24, 12)
+#undef AA_FTB
+        printf("last error: %s\n", hipGetErrorString(hipGetLastError()));
+        return 0;
     }
     AA_CONV_CFGS(AA_BENCH)
     if (!pmc && argc == 1) {  // candidate tilings of the 9x3 layer
