@@ -209,7 +209,7 @@ int main(int argc, char** argv) {
         const int H = 158, W = 224;
 #define AA_FUSED(D)                                                                                        \
     printf("fused c1+c2 DIAG %2d: %7.1f us\n", D,                                                         \
-           time_one<bf16, 3, 3, 32, 4, 1, 9, 2, 3, 12, 48, D, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
+           time_one<bf16, 3, 3, 32, 4, 1, 6, 2, 3, 18, 21, D, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
         AA_FUSED(0)
         if (pmc) return 0;
         AA_FUSED(2) AA_FUSED(4) AA_FUSED(6) AA_FUSED(7) AA_FUSED(3)
