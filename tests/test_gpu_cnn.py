@@ -74,6 +74,24 @@ def test_cnn_fp8(gpu, model_root, T):
     assert e_emu <= FP8_EMU_MAX and m_emu <= FP8_EMU_MEAN
 
 
+@pytest.mark.parametrize("which", ["model2", "mag"])
+def test_cnn_fp8_variants(gpu, model_root, tmp_path, which):
+    """fp8 on a wider ensemble member and on a MagTransform model (the fused
+    first conv's power prologue), against the emulation."""
+    if which == "mag":
+        path = make_model(tmp_path / "mag8", name="magmodel", seed=11, mag=2)
+        x = calibration_input(6, 160, 226, False, np.random.default_rng(6))
+    else:
+        path = model_root / which / "audioModel.safetensors"
+        x = calibration_input(6, 160, 226, True, np.random.default_rng(7))
+    lg, _ = _run(path, x, "fp8")
+    elg, _ = cnn_oracle.forward_fp8_emulated(path, x)
+    d = np.abs(lg - elg)
+    print(f"{which} fp8 max|dlogit| vs emulation {d.max():.3e} (mean {d.mean():.3e})")
+    assert np.isfinite(lg).all()
+    assert d.max() <= FP8_EMU_MAX and d.mean() <= FP8_EMU_MEAN
+
+
 def test_cnn_magtransform(gpu, tmp_path):
     path = make_model(tmp_path / "mag", name="magmodel", seed=11, mag=2)
     x = calibration_input(3, 160, 226, False, np.random.default_rng(5))
