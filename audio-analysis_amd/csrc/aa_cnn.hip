@@ -247,7 +247,8 @@ struct FirstConv {
 // staging, bit 1 the MFMA loop, bit 2 the epilogue stores, bit 3 makes every
 // lane read pixel 0 (no LDS bank conflicts), bit 4 re-reads chunk 0's weights
 // (L1-resident, no L2 stream), bit 5 skips the weight loads in the loop, bit 7
-// skips the fragment reads after the first (MFMA issue alone).
+// skips the fragment reads after the first (MFMA issue alone), bit 6 the
+// fused first conv's compute, bit 9 its log-mel patch load.
 // Waves per SIMD a conv_mfma block shape reaches (LDS-limited), told to the
 // compiler so it schedules for latency at that occupancy instead of trimming
 // registers for an occupancy the LDS footprint never allows.
@@ -355,7 +356,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
         const size_t pbytes = ((size_t)PH * PW * CSTR * sizeof(T) + 15) & ~(size_t)15;
         float* X = reinterpret_cast<float*>(smem + pbytes);
         const float* lm = reinterpret_cast<const float*>(in) + (size_t)n * fc.H0 * fc.W0;
-        for (int i0 = 0; i0 < XN; i0 += 4 * NTHR) {
+        for (int i0 = 0; i0 < ((DIAG & 512) ? 0 : XN); i0 += 4 * NTHR) {
             float v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -398,7 +399,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
             // chain's latency (in-pipeline A/B: +0.7 % bench; fp8 -0.7 %, so one)
             constexpr int NG = (NPX + 31) / 32;
             constexpr int UG = sizeof(T) == 2 ? 2 : 1;
-            for (int g0 = wave1; g0 < NG; g0 += 4 * UG) {
+            for (int g0 = wave1; g0 < ((DIAG & 64) ? 0 : NG); g0 += 4 * UG) {
                 bf16x8 xh[UG], xl[UG];
                 int pix[UG];
 #pragma unroll

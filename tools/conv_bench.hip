@@ -212,7 +212,8 @@ int main(int argc, char** argv) {
            time_one<bf16, 3, 3, 32, 4, 1, 6, 2, 3, 18, 21, D, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
         AA_FUSED(0)
         if (pmc) return 0;
-        AA_FUSED(2) AA_FUSED(4) AA_FUSED(6) AA_FUSED(7) AA_FUSED(3)
+        AA_FUSED(2) AA_FUSED(4) AA_FUSED(6) AA_FUSED(7) AA_FUSED(3) AA_FUSED(6 | 64) AA_FUSED(6 | 512)
+        AA_FUSED(6 | 64 | 512) AA_FUSED(64) AA_FUSED(512)
 #undef AA_FUSED
 #define AA_FT(MF, TH, TW)                                                                                  \
     printf("fused c1+c2 MF%2d %2dx%2d: %7.1f us\n", MF, TH, TW,                                            \
