@@ -19,6 +19,7 @@ ABI_VERSION = 1
 AA_PREC_F32 = 0
 AA_PREC_BF16 = 1
 AA_PREC_FP8 = 2
+AA_PREC_BF16X3 = 3
 
 AA_OP = {
     "conv2d": 1,

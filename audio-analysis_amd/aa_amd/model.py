@@ -110,11 +110,12 @@ def layer_table(arch, tensors):
 
 
 class Model(_lib.StageTiming):
-    """A loaded network on one device.  ``precision``: "f32" (exact-f32 MFMA,
-    the parity mode) or "bf16"."""
+    """A loaded network on one device.  ``precision``: "bf16x3" (split-bf16,
+    the default: ~17-bit products on bf16 MFMA, within the 1e-3 logit gate),
+    "f32" (exact-f32 MFMA), "bf16" or "fp8" (throughput modes)."""
     _timing_prefix = "aa_model"
 
-    def __init__(self, model_path, in_shape, precision="bf16", device=None, meta=None):
+    def __init__(self, model_path, in_shape, precision="bf16x3", device=None, meta=None):
         self.path = Path(model_path)
         self.meta = meta if meta is not None else load_model_meta(model_path)
         self.device = torch.device(device or "cuda")
@@ -127,7 +128,8 @@ class Model(_lib.StageTiming):
             raise
         layers, blob = layer_table(arch, tensors)
         self.in_shape = tuple(int(v) for v in in_shape)  # (H, W, C)
-        prec = {"f32": _lib.AA_PREC_F32, "bf16": _lib.AA_PREC_BF16, "fp8": _lib.AA_PREC_FP8}[precision]
+        prec = {"f32": _lib.AA_PREC_F32, "bf16": _lib.AA_PREC_BF16, "fp8": _lib.AA_PREC_FP8,
+                "bf16x3": _lib.AA_PREC_BF16X3}[precision]
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             _lib.check(_lib.lib().aa_model_create(layers, len(layers), blob.ctypes.data, blob.size,

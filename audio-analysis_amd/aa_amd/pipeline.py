@@ -53,13 +53,13 @@ class Classifier:
 
     @classmethod
     def shared(cls, precision=None, device=None):
-        precision = precision or os.environ.get("AA_PRECISION", "f32")
+        precision = precision or os.environ.get("AA_PRECISION", "bf16x3")
         key = (precision, str(device or "cuda"))
         if key not in cls._shared:
             cls._shared[key] = cls(precision, device)
         return cls._shared[key]
 
-    def __init__(self, precision="f32", device=None):
+    def __init__(self, precision="bf16x3", device=None):
         self.precision = precision
         self.device = torch.device(device or "cuda")
         self._models = {}

@@ -41,7 +41,7 @@ class StreamRunner:
     in input order; ``scores`` is the float32 [L] mean over models and windows
     (what apply_group_scores thresholds)."""
 
-    def __init__(self, model_paths: Sequence, settings: FeSettings, precision="bf16", device=None,
+    def __init__(self, model_paths: Sequence, settings: FeSettings, precision="bf16x3", device=None,
                  max_windows=512, max_samples=16 * 2_880_000, segment_stride=1.5, pad_short_tracks=False,
                  metas=None):
         self.device = torch.device(device or "cuda")

@@ -40,6 +40,35 @@ typedef __bf16 bf16;
 struct fp8 {
     uint8_t v;
 };
+// Split-bf16 precision tag (AA_PREC_BF16X3): activations stay f32 in HBM; at
+// LDS staging every value x becomes bf16 hi = rn(x) and lo = rn(x - hi)
+// (x - hi is exact in f32), weights likewise on the host, and each product
+// is hi*hi + hi*lo + lo*hi on three bf16 MFMAs with f32 accumulation.  The
+// representation error is <= 2^-18 |x| per operand and the dropped lo*lo
+// term <= 2^-18 |x w|, so a MAC carries ~17 significant bits instead of
+// bf16's 8 -- enough for the 1e-3 logit gate at 3/16 of the f32-MFMA cost.
+struct bf16x3 {};
+
+// Storage types of a precision: L = LDS / fragment element, G = HBM
+// activation element.
+template <typename T>
+struct Prec {
+    using L = T;
+    using G = T;
+};
+template <>
+struct Prec<bf16x3> {
+    using L = bf16;
+    using G = float;
+};
+template <typename T>
+constexpr bool is_split() { return std::is_same<T, bf16x3>::value; }
+template <typename T>
+constexpr bool is_fp8() { return std::is_same<T, fp8>::value; }
+
+// bf16 hi + lo of an f32 (round to nearest even both times)
+__device__ __forceinline__ bf16 bf_hi(float x) { return (bf16)x; }
+__device__ __forceinline__ bf16 bf_lo(float x) { return (bf16)(x - (float)(bf16)x); }
 
 // 4 / 8 floats -> e4m3fn bytes, round to nearest even, saturated to +-448
 __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
@@ -88,6 +117,22 @@ __device__ __forceinline__ f32x4 mfma_chunk(const Frag<float>& a, const Frag<flo
 #pragma unroll
     for (int s = 0; s < 8; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[s], b.v[s], c, 0, 0, 0);
     return c;
+}
+// split-bf16: the hi fragment at p, the lo fragment LO elements further (the
+// [hi C][lo C] row layout); hi*hi + hi*lo + lo*hi, the bf16 lane layout
+template <int LO>
+struct FragSplit {
+    bf16x8 h, l;
+    __device__ __forceinline__ void load(const bf16* p) {
+        h = *reinterpret_cast<const bf16x8*>(p);
+        l = *reinterpret_cast<const bf16x8*>(p + LO);
+    }
+};
+template <int LO>
+__device__ __forceinline__ f32x4 mfma_chunk(const FragSplit<LO>& a, const FragSplit<LO>& b, f32x4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);
 }
 
 template <typename T>
@@ -169,9 +214,11 @@ __global__ __launch_bounds__(256) void conv_small(const float* __restrict__ in, 
 // ds_read_b128 lane group of the fragment reads conflict-free); fp8 rows
 // padded by 16 B (48 / 80 / 144-B strides put the 16 rows of a ds_read_b64
 // half-wave on distinct 4-bank groups); f32 (parity mode) keeps a 16-B pad.
+// Split-bf16: a pixel / weight row is [hi C][lo C][16 pad], 4C + 32 bytes
+// (again 2 mod 4 16-B units for C % 32 == 0).
 template <typename T>
 __host__ __device__ constexpr int conv_cstr(int cin) {
-    return cin + (sizeof(T) == 1 ? 16 : sizeof(T) == 2 ? 16 : 4);
+    return is_split<T>() ? 2 * cin + 16 : cin + (sizeof(T) == 1 ? 16 : sizeof(T) == 2 ? 16 : 4);
 }
 
 // LDS of one conv_mfma block: [staged patch][f32 log-mel patch if FUSED]
@@ -179,7 +226,7 @@ __host__ __device__ constexpr int conv_cstr(int cin) {
 template <typename T, int KH, int KW, int CIN, int TH, int TW, bool FUSED>
 __host__ __device__ constexpr size_t conv_b_offset() {
     constexpr int CSTR = conv_cstr<T>(CIN);
-    size_t off = ((size_t)(TH + KH - 1) * (TW + KW - 1) * CSTR * sizeof(T) + 15) & ~(size_t)15;
+    size_t off = ((size_t)(TH + KH - 1) * (TW + KW - 1) * CSTR * sizeof(typename Prec<T>::L) + 15) & ~(size_t)15;
     if (FUSED) off += ((sizeof(float) * (TH + KH + 1) * (TW + KW + 1)) + 15) & ~(size_t)15;
     return off;
 }
@@ -188,7 +235,7 @@ __host__ __device__ constexpr size_t conv_b_offset() {
 // wave-instructions of global_load_lds (the tail lanes land in the rounding).
 template <typename T, int CIN, int BN>
 __host__ __device__ constexpr int conv_slice_lds_bytes() {
-    return (BN * conv_cstr<T>(CIN) * (int)sizeof(T) + 1023) / 1024 * 1024;
+    return (BN * conv_cstr<T>(CIN) * (int)sizeof(typename Prec<T>::L) + 1023) / 1024 * 1024;
 }
 
 template <typename T, int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool EBF16>
@@ -265,24 +312,28 @@ template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, i
 __global__ __launch_bounds__(WM * WN * 64)
 __attribute__((amdgpu_waves_per_eu(conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>(),
                                     conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>())))
-void conv_mfma(const T* __restrict__ in, int Hin, int Win,
-                                                 const T* __restrict__ wt, const float* __restrict__ bias,
-                                                 T* __restrict__ out, int Hout, int Wout, int cout_store,
+void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
+                                                 const typename Prec<T>::L* __restrict__ wt, const float* __restrict__ bias,
+                                                 typename Prec<T>::G* __restrict__ out, int Hout, int Wout, int cout_store,
                                                  int tiles_w, int act, float alpha, FirstConv fc) {
+    using LT = typename Prec<T>::L;  // LDS / fragment element
+    using GT = typename Prec<T>::G;  // HBM activation element
+    constexpr bool SPLIT = is_split<T>();
+    constexpr bool F8 = is_fp8<T>();
     static_assert(TH % POOL == 0 && TW % POOL == 0, "pool-aligned tile");
     static_assert(TH * TW <= WM * MF * 16, "tile covered by the waves' fragments");
+    static_assert(!(SPLIT && EBF16), "split-bf16 keeps an f32 epilogue tile");
     constexpr int NTHR = WM * WN * 64;
     static_assert(CIN % 32 == 0, "C_in multiple of 32");
     constexpr int BN = WN * NF * 16;
-    constexpr int VEC = 16 / sizeof(T);
+    constexpr int VEC = 16 / sizeof(LT);
     constexpr int CSTR = conv_cstr<T>(CIN);  // padded pixel / weight-row stride
-    constexpr int KTOT = KH * KW * CIN;
     // epilogue tile: f32, or bf16 with the bias already added (rounding is
     // monotone, so max-pooling the rounded values equals rounding the max)
     using ET = typename std::conditional<EBF16, bf16, float>::type;
     constexpr int ESTR = BN + (EBF16 ? 8 : 4);
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    T* patch = reinterpret_cast<T*>(smem);
+    LT* patch = reinterpret_cast<LT*>(smem);
 
     const int n = blockIdx.z;
     const int th = blockIdx.x / tiles_w, tw = blockIdx.x - (blockIdx.x / tiles_w) * tiles_w;
@@ -303,13 +354,13 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
     constexpr int GHI = (GPS + NW - 1) / NW, GLO = GPS / NW;       // this wave's share: GHI if wave < GPS % NW
     char* Bs = smem + conv_b_offset<T, KH, KW, CIN, TH, TW, FUSED>();
     const size_t tap_stride = (size_t)gridDim.y * SLICE;
-    const T* wsl = wt + (size_t)blockIdx.y * SLICE + (threadIdx.x & 63) * VEC;
+    const LT* wsl = wt + (size_t)blockIdx.y * SLICE + (threadIdx.x & 63) * VEC;
 #define AA_GLDS(t)                                                                                       \
     _Pragma("unroll") for (int u_ = 0; u_ < GHI; ++u_) {                                               \
         const int g_ = u_ * NW + wave0;                                                                  \
         if (GPS % NW == 0 || g_ < GPS)                                                                  \
             __builtin_amdgcn_global_load_lds(                                                           \
-                (const __attribute__((address_space(1))) void*)(wsl + (size_t)(t) * tap_stride + g_ * (1024 / sizeof(T))), \
+                (const __attribute__((address_space(1))) void*)(wsl + (size_t)(t) * tap_stride + g_ * (1024 / sizeof(LT))), \
                 (__attribute__((address_space(3))) void*)(Bs + ((t) % NB) * SLICE_LDS + g_ * 1024), 16, 0, 0); \
     }
     if constexpr (!(DIAG & 32)) {
@@ -319,6 +370,43 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
 
     // ---- stage the input patch ----
     if constexpr (DIAG & 1) {
+    } else if constexpr (!FUSED && SPLIT) {
+        // f32 activations, 16-B loads (4 channels), split into the hi and lo
+        // planes of the pixel's LDS row
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        constexpr int VPP = CIN / 4;
+        constexpr int U = 4;
+        const int total = PH * PW * VPP;
+        const float* src = in + (size_t)n * Hin * Win * CIN;
+        for (int i0 = 0; i0 < total; i0 += U * NTHR) {
+            float4 v[U];
+            bool ok[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int idx = i0 + u * NTHR + threadIdx.x;
+                const int pix = idx / VPP, cv = idx - pix * VPP;
+                const int r = pix / PW, c = pix - r * PW;
+                const int gh = oh0 + r, gw = ow0 + c;
+                ok[u] = idx < total && gh < Hin && gw < Win;
+                const int ch = min(gh, Hin - 1), cw = min(gw, Win - 1);
+                v[u] = *reinterpret_cast<const float4*>(src + ((size_t)ch * Win + cw) * CIN + cv * 4);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int idx = i0 + u * NTHR + threadIdx.x;
+                if (idx < total) {
+                    const int pix = idx / VPP, cv = idx - pix * VPP;
+                    const float4 x = ok[u] ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    bf16x4 h, l;
+                    { const float s_ = x.x; h[0] = bf_hi(s_); l[0] = bf_lo(s_); }
+                    { const float s_ = x.y; h[1] = bf_hi(s_); l[1] = bf_lo(s_); }
+                    { const float s_ = x.z; h[2] = bf_hi(s_); l[2] = bf_lo(s_); }
+                    { const float s_ = x.w; h[3] = bf_hi(s_); l[3] = bf_lo(s_); }
+                    *reinterpret_cast<bf16x4*>(patch + pix * CSTR + cv * 4) = h;
+                    *reinterpret_cast<bf16x4*>(patch + pix * CSTR + CIN + cv * 4) = l;
+                }
+            }
+        }
     } else if constexpr (!FUSED) {
         // batched, unconditional 16-B loads from clamped addresses (a
         // load-or-zero branch would serialise them); out-of-image pixels only
@@ -326,7 +414,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
         constexpr int VPP = CIN / VEC;  // 16-B vectors per pixel
         constexpr int U = 4;
         const int total = PH * PW * VPP;
-        const T* src = in + (size_t)n * Hin * Win * CIN;
+        const GT* src = in + (size_t)n * Hin * Win * CIN;
         for (int i0 = 0; i0 < total; i0 += U * NTHR) {
             uint4 v[U];
             bool ok[U];
@@ -353,7 +441,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
         static_assert(CIN == 32, "fused first layer produces 32 channels");
         // (a) log-mel patch (PH+2) x (PW+2), f32, after the activation patch
         constexpr int XW = PW + 2, XN = (PH + 2) * XW;
-        const size_t pbytes = ((size_t)PH * PW * CSTR * sizeof(T) + 15) & ~(size_t)15;
+        const size_t pbytes = ((size_t)PH * PW * CSTR * sizeof(LT) + 15) & ~(size_t)15;
         float* X = reinterpret_cast<float*>(smem + pbytes);
         const float* lm = reinterpret_cast<const float*>(in) + (size_t)n * fc.H0 * fc.W0;
         for (int i0 = 0; i0 < ((DIAG & 512) ? 0 : XN); i0 += 4 * NTHR) {
@@ -370,21 +458,23 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                 if (idx < XN) X[idx] = fc.has_mag ? powf(v[u], fc.mag_exp) : v[u];
             }
         }
-        if constexpr (sizeof(T) <= 2) {
+        if constexpr (sizeof(LT) <= 2) {
             // (b) first conv on the matrix cores: per 32 patch pixels one
             // v_mfma_f32_32x32x16_bf16, D[32 ch][32 px] = W[32 ch][16 k] X[16 k][32 px]
             // with the 9 taps in k (0..8; weights 0 for k = 9..15, so those
             // B entries may hold any finite value), the bias as the C input,
             // then the activation, bf16, and 8-byte stores of 4 channels into
             // the patch.  Lane l: pixel l % 32, k-group / channel quad l / 32.
-            // (bf16 path only: the f32 parity mode runs conv_small.)
+            // Split-bf16 adds the weights' lo part (a third MFMA) and stores
+            // the activations as hi and lo planes.
             const int wave1 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
             const int l32 = threadIdx.x & 31, kg = (threadIdx.x >> 5) & 1;
-            bf16x8 wa;
+            bf16x8 wa, wal;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int tap = 8 * kg + j;
-                wa[j] = tap < 9 ? (bf16)fc.w[l32 * 9 + tap] : (bf16)0.f;
+                const float wv = tap < 9 ? fc.w[l32 * 9 + tap] : 0.f;
+                { const float s_ = wv; wa[j] = bf_hi(s_); wal[j] = bf_lo(s_); }
             }
             f32x16 cb;  // D row (channel) of register r: 8 (r / 4) + 4 kg + r % 4
 #pragma unroll
@@ -398,7 +488,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
             // (and their LDS reads) interleave instead of waiting out each
             // chain's latency (in-pipeline A/B: +0.7 % bench; fp8 -0.7 %, so one)
             constexpr int NG = (NPX + 31) / 32;
-            constexpr int UG = sizeof(T) == 2 ? 2 : 1;
+            constexpr int UG = (std::is_same<T, bf16>::value || SPLIT) ? 2 : 1;
             for (int g0 = wave1; g0 < ((DIAG & 64) ? 0 : NG); g0 += 4 * UG) {
                 bf16x8 xh[UG], xl[UG];
                 int pix[UG];
@@ -424,13 +514,24 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                 for (int u = 0; u < UG; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xh[u], cb, 0, 0, 0);
 #pragma unroll
                 for (int u = 0; u < UG; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xl[u], d[u], 0, 0, 0);
+                if constexpr (SPLIT) {
+#pragma unroll
+                    for (int u = 0; u < UG; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wal, xh[u], d[u], 0, 0, 0);
+                }
 #pragma unroll
                 for (int u = 0; u < UG; ++u) {
                     if ((g0 + 4 * u) * 32 + l32 < NPX) {
-                        T* dst = patch + pix[u] * CSTR + 4 * kg;
+                        LT* dst = patch + pix[u] * CSTR + 4 * kg;
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
-                            if constexpr (sizeof(T) == 1) {
+                            if constexpr (SPLIT) {
+                                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                                bf16x4 h, l;
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) { const float s_ = fmaxf(d[u][4 * q + e], d[u][4 * q + e] * ae); h[e] = bf_hi(s_); l[e] = bf_lo(s_); }
+                                *reinterpret_cast<bf16x4*>(dst + 8 * q) = h;
+                                *reinterpret_cast<bf16x4*>(dst + CIN + 8 * q) = l;
+                            } else if constexpr (F8) {
                                 float o[4];
 #pragma unroll
                                 for (int e = 0; e < 4; ++e) o[e] = fmaxf(d[u][4 * q + e], d[u][4 * q + e] * ae);
@@ -498,8 +599,8 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                         o[2 * k] = fmaxf(v.x, sv.x);
                         o[2 * k + 1] = fmaxf(v.y, sv.y);
                     }
-                    T* dst = patch + (r * PW + col) * CSTR + cg * 8;
-                    if constexpr (sizeof(T) == 2) {
+                    LT* dst = patch + (r * PW + col) * CSTR + cg * 8;
+                    if constexpr (sizeof(LT) == 2) {
                         bf16x8 v;
     #pragma unroll
                         for (int ch = 0; ch < 8; ++ch) v[ch] = (bf16)o[ch];
@@ -548,7 +649,8 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
     // chunk q+1's fragments are in flight.  Across a tap boundary only the A
     // fragments (from the static patch) can run ahead; the next slice's B
     // fragments follow the barrier that publishes it.
-    Frag<T> fa[MF], fb[NF], na[MF], nb[NF];
+    using FT = typename std::conditional<SPLIT, FragSplit<CIN>, Frag<LT>>::type;
+    FT fa[MF], fb[NF], na[MF], nb[NF];
 #define AA_LOAD_A(dst, tap, cc_)                                                             \
     if (!(DIAG & 128) || (tap) == 0)                                                         \
     {                                                                                        \
@@ -559,11 +661,11 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
 #define AA_LOAD_B(dst, buf, cc_)                                                             \
     if (!(DIAG & 128) || (buf) < 0)                                                          \
     {                                                                                        \
-        const T* bt_ = reinterpret_cast<const T*>(Bs + (buf) * SLICE_LDS) + brow + (cc_) * 32; \
+        const LT* bt_ = reinterpret_cast<const LT*>(Bs + (buf) * SLICE_LDS) + brow + (cc_) * 32; \
         _Pragma("unroll") for (int j = 0; j < NF; ++j) dst[j].load(bt_ + j * 16 * CSTR);   \
     }
     // f32 (parity mode) fragments are twice as wide: single-buffered there
-    constexpr bool DB = sizeof(T) <= 2;
+    constexpr bool DB = !std::is_same<T, float>::value;
     if constexpr (DB) AA_LOAD_A(fa, 0, 0)
     for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); ++t) {
         // slices t+1 .. min(t+NB-2, NTAP-1) may stay in flight
@@ -632,7 +734,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
 #pragma unroll
         for (int r = 0; r < 4; ++r) bj[r] = EBF16 ? bias[blockIdx.y * BN + c0 + r] : 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sj[r] = (EBF16 && sizeof(T) == 1) ? wscale[blockIdx.y * BN + c0 + r] : 1.f;
+        for (int r = 0; r < 4; ++r) sj[r] = (EBF16 && F8) ? wscale[blockIdx.y * BN + c0 + r] : 1.f;
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             const int p = (wm * MF + i) * 16 + (lane & 15);
@@ -642,7 +744,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                     typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
                     bf16x4 v;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = (bf16)(sizeof(T) == 1 ? fmaf(acc[i][j][r], sj[r], bj[r]) : acc[i][j][r] + bj[r]);
+                    for (int r = 0; r < 4; ++r) v[r] = (bf16)(F8 ? fmaf(acc[i][j][r], sj[r], bj[r]) : acc[i][j][r] + bj[r]);
                     *reinterpret_cast<bf16x4*>(e) = v;
                 } else {
                     *reinterpret_cast<float4*>(e) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
@@ -664,8 +766,8 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
 #pragma unroll
     for (int c = 0; c < 8; ++c) bv[c] = EBF16 ? 0.f : bias[ch0 + c];  // bias is padded to cout_pad
 #pragma unroll
-    for (int c = 0; c < 8; ++c) sv[c] = (!EBF16 && sizeof(T) == 1) ? wscale[ch0 + c] : 1.f;
-    T* dst = out + (size_t)n * Hout * Wout * cout_store;
+    for (int c = 0; c < 8; ++c) sv[c] = (!EBF16 && F8) ? wscale[ch0 + c] : 1.f;
+    GT* dst = out + (size_t)n * Hout * Wout * cout_store;
     for (int q = threadIdx.x / G; q < PHo * PWo; q += NTHR / G) {
         const int pr = q / PWo, pc = q - (q / PWo) * PWo;
         const int gh = oh0s + pr, gw = ow0s + pc;
@@ -689,15 +791,15 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
             }
         if (gh >= Hout || gw >= Wout) continue;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = apply_act((!EBF16 && sizeof(T) == 1) ? fmaf(v[c], sv[c], bv[c]) : v[c] + bv[c], act, alpha);
+        for (int c = 0; c < 8; ++c) v[c] = apply_act((!EBF16 && F8) ? fmaf(v[c], sv[c], bv[c]) : v[c] + bv[c], act, alpha);
         if constexpr ((DIAG & 4) != 0) {
             if (v[0] != 12345.f) continue;  // keep the values live, store (almost) never
         }
-        T* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
+        GT* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
         if (ch0 + 8 <= cout_store) {
-            if constexpr (sizeof(T) == 1) {
+            if constexpr (F8) {
                 *reinterpret_cast<uint2*>(o) = make_uint2(pack4_fp8(v[0], v[1], v[2], v[3]), pack4_fp8(v[4], v[5], v[6], v[7]));
-            } else if constexpr (sizeof(T) == 2) {
+            } else if constexpr (sizeof(GT) == 2) {
                 bf16x8 pk;
 #pragma unroll
                 for (int c = 0; c < 8; ++c) pk[c] = (bf16)v[c];
@@ -707,7 +809,7 @@ void conv_mfma(const T* __restrict__ in, int Hin, int Win,
                 reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
             }
         } else {
-            for (int c = 0; c < 8 && ch0 + c < cout_store; ++c) o[c] = to_t<T>(v[c]);
+            for (int c = 0; c < 8 && ch0 + c < cout_store; ++c) o[c] = to_t<GT>(v[c]);
         }
     }
 }
@@ -894,8 +996,10 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     const int tiles_h = (s.Hout * POOL + TH - 1) / TH;
     const int tiles_w = (s.Wout * POOL + TW - 1) / TW;
     dim3 grid(tiles_h * tiles_w, s.cout_pad / BN, n);
-    hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, st, (const T*)in, s.Hin, s.Win, (const T*)s.d_w, s.d_b,
-                       (T*)out, s.Hout, s.Wout, s.cout, tiles_w, s.act, s.alpha, fc);
+    using GT = typename Prec<T>::G;
+    using LT = typename Prec<T>::L;
+    hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, st, (const GT*)in, s.Hin, s.Win, (const LT*)s.d_w, s.d_b,
+                       (GT*)out, s.Hout, s.Wout, s.cout, tiles_w, s.act, s.alpha, fc);
     AA_LAUNCH_CHECK();
     return AA_OK;
 }
@@ -920,12 +1024,18 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     X(float, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false)         \
     X(float, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false)         \
     X(float, 9, 3, 64, 3, 1, 4, 7, 1, 3, 33, false)         \
-    X(float, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)
+    X(float, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)        \
+    X(bf16x3, 3, 3, 32, 3, 2, 2, 9, 1, 6, 48, false)        \
+    X(bf16x3, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false)        \
+    X(bf16x3, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false)        \
+    X(bf16x3, 9, 3, 64, 3, 1, 4, 7, 1, 3, 33, false)        \
+    X(bf16x3, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)
 
 template <typename T>
 constexpr int prec_of() {
-    return sizeof(T) == 1 ? AA_PREC_FP8 : sizeof(T) == 2 ? AA_PREC_BF16 : AA_PREC_F32;
+    return is_split<T>() ? AA_PREC_BF16X3 : sizeof(T) == 1 ? AA_PREC_FP8 : sizeof(T) == 2 ? AA_PREC_BF16 : AA_PREC_F32;
 }
+// bytes of one stored activation (split-bf16 keeps f32 activations)
 static size_t prec_bytes(int prec) { return prec == AA_PREC_FP8 ? 1 : prec == AA_PREC_BF16 ? 2 : 4; }
 
 // output channels per block of the instantiation serving this stage (0: none)
@@ -945,8 +1055,9 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
         AA_CHECK(s.kh == 3 && s.kw == 3 && s.cout == 32 && s.cin == 1, AA_ERR_UNSUPPORTED,
                  "first conv %dx%d %d->%d unsupported", s.kh, s.kw, s.cin, s.cout);
         dim3 grid((s.Hc * s.Wc + 255) / 256, n);
-        hipLaunchKernelGGL((conv_small<T, 3, 3, 32>), grid, dim3(256), 0, st, (const float*)in, s.Hin,
-                           s.Win, (const float*)s.d_w, s.d_b, s.has_mag, s.mag_exp, (T*)out, s.Hc, s.Wc,
+        using GT = typename Prec<T>::G;
+        hipLaunchKernelGGL((conv_small<GT, 3, 3, 32>), grid, dim3(256), 0, st, (const float*)in, s.Hin,
+                           s.Win, (const float*)s.d_w, s.d_b, s.has_mag, s.mag_exp, (GT*)out, s.Hc, s.Wc,
                            s.act, s.alpha);
         AA_LAUNCH_CHECK();
         return AA_OK;
@@ -959,9 +1070,12 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
         // the free ping-pong buffer `out` and head_final reduces them
         const int HW = s.Hin * s.Win, parts = (HW + 63) / 64;
         float* part = static_cast<float*>(out);
-        const float* hsc = sizeof(T) == 1 ? s.d_b + s.cout_pad : nullptr;  // fp8 dequantisation scales
-        hipLaunchKernelGGL((conv_head<T, 256, 1, 2>), dim3(n, parts), dim3(256), 0, st, (const T*)in, HW,
-                           (const T*)s.d_w, s.d_b, s.cout, s.act, s.alpha, s.sigmoid, logits, probs, part, hsc);
+        const float* hsc = is_fp8<T>() ? s.d_b + s.cout_pad : nullptr;  // fp8 dequantisation scales
+        // split-bf16: the head reads f32 activations and runs the exact f32
+        // MFMA (its 1x1 contraction is <1 % of the network's FLOPs)
+        using HT = typename Prec<T>::G;
+        hipLaunchKernelGGL((conv_head<HT, 256, 1, 2>), dim3(n, parts), dim3(256), 0, st, (const HT*)in, HW,
+                           (const HT*)s.d_w, s.d_b, s.cout, s.act, s.alpha, s.sigmoid, logits, probs, part, hsc);
         AA_LAUNCH_CHECK();
         hipLaunchKernelGGL(head_final, dim3(n), dim3(64), 0, st, part, parts, 32, s.d_b, s.cout, s.act, s.alpha,
                            s.sigmoid, logits, probs, hsc);
@@ -1007,6 +1121,12 @@ static uint16_t f2bf(float f) {  // round to nearest even
     u += 0x7fff + ((u >> 16) & 1);
     return (uint16_t)(u >> 16);
 }
+static float bf2f(uint16_t b) {
+    const uint32_t u = (uint32_t)b << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
 
 // f32 -> OCP e4m3fn byte, round to nearest even, saturated to +-448 (the
 // device's v_cvt_pk_fp8_f32 conversion of the same value)
@@ -1036,7 +1156,8 @@ using namespace aa;
 extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const float* blob, int64_t blob_len,
                                int32_t in_h, int32_t in_w, int32_t in_c, int32_t precision, void** model) {
     AA_CHECK(layers && blob && model && n_layers > 0, AA_ERR_INVALID, "aa_model_create: null argument");
-    AA_CHECK(precision == AA_PREC_F32 || precision == AA_PREC_BF16 || precision == AA_PREC_FP8, AA_ERR_INVALID,
+    AA_CHECK(precision == AA_PREC_F32 || precision == AA_PREC_BF16 || precision == AA_PREC_FP8 ||
+                 precision == AA_PREC_BF16X3, AA_ERR_INVALID,
              "aa_model_create: precision %d", precision);
     auto get = [&](int64_t off, int64_t n) -> const float* {
         if (off < 0 || off + n > blob_len) return nullptr;
@@ -1149,8 +1270,11 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         // the 1x1 head [cout_pad][C_in]
         const bool bf = (precision == AA_PREC_BF16) && s.kind != ST_SMALL;
         const bool f8 = (precision == AA_PREC_FP8) && s.kind != ST_SMALL;
-        const int wes = bf ? 2 : f8 ? 1 : 4;
-        const int cstr = s.kind == ST_MFMA ? (bf ? conv_cstr<bf16>(s.cin) : f8 ? conv_cstr<fp8>(s.cin) : conv_cstr<float>(s.cin))
+        // split-bf16: MFMA stages hold [hi C][lo C] bf16 rows; the head stays f32
+        const bool sp = (precision == AA_PREC_BF16X3) && s.kind == ST_MFMA;
+        const int wes = (bf || sp) ? 2 : f8 ? 1 : 4;
+        const int cstr = s.kind == ST_MFMA ? (bf ? conv_cstr<bf16>(s.cin) : f8 ? conv_cstr<fp8>(s.cin)
+                                              : sp ? conv_cstr<bf16x3>(s.cin) : conv_cstr<float>(s.cin))
                                            : s.cin;
         const int ntap = s.kh * s.kw;
         const size_t slack = s.kind == ST_MFMA ? 1024 / wes : 0;
@@ -1160,6 +1284,10 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                 const double v = kern[(size_t)k * s.cout + o] * scale[o];
                 if (s.kind == ST_SMALL) {
                     wpk[(size_t)o * K + k] = (float)v;
+                } else if (sp) {  // hi at c, the f32 value at cin + c (split below)
+                    const int t = k / s.cin, c = k - t * s.cin;
+                    wpk[((size_t)t * s.cout_pad + o) * cstr + c] = (float)v;
+                    wpk[((size_t)t * s.cout_pad + o) * cstr + s.cin + c] = (float)v;
                 } else {
                     const int t = k / s.cin, c = k - t * s.cin;
                     wpk[((size_t)t * s.cout_pad + o) * cstr + c] = (float)v;
@@ -1191,6 +1319,18 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             } else if (bf) {
                 std::vector<uint16_t> h(wpk.size());
                 for (size_t k = 0; k < wpk.size(); ++k) h[k] = f2bf(wpk[k]);
+                e = hipMemcpy(s.d_w, h.data(), wbytes, hipMemcpyHostToDevice);
+            } else if (sp) {
+                // row [hi C][lo C][pad]: hi = rn_bf16(w), lo = rn_bf16(w - hi)
+                std::vector<uint16_t> h(wpk.size(), 0);
+                const size_t rows = (size_t)ntap * s.cout_pad;
+                for (size_t r = 0; r < rows; ++r)
+                    for (int c = 0; c < s.cin; ++c) {
+                        const float w = wpk[r * cstr + c];
+                        const uint16_t hi = f2bf(w);
+                        h[r * cstr + c] = hi;
+                        h[r * cstr + s.cin + c] = f2bf(w - bf2f(hi));
+                    }
                 e = hipMemcpy(s.d_w, h.data(), wbytes, hipMemcpyHostToDevice);
             } else {
                 e = hipMemcpy(s.d_w, wpk.data(), wbytes, hipMemcpyHostToDevice);
@@ -1295,9 +1435,10 @@ extern "C" int aa_model_forward(void* model, const float* x, int32_t n, float* l
         hipEvent_t e0;
         int rc = m->timer.begin((int)k, st, &e0);
         if (rc != AA_OK) return rc;
-        rc = m->prec == AA_PREC_BF16  ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st, first)
-             : m->prec == AA_PREC_FP8 ? launch_stage<fp8>(*m, s, in, out, logits, probs, n, st, first)
-                                      : launch_stage<float>(*m, s, in, out, logits, probs, n, st, first);
+        rc = m->prec == AA_PREC_BF16     ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st, first)
+             : m->prec == AA_PREC_FP8    ? launch_stage<fp8>(*m, s, in, out, logits, probs, n, st, first)
+             : m->prec == AA_PREC_BF16X3 ? launch_stage<bf16x3>(*m, s, in, out, logits, probs, n, st, first)
+                                         : launch_stage<float>(*m, s, in, out, logits, probs, n, st, first);
         if (rc != AA_OK) return rc;
         rc = m->timer.end((int)k, st, e0);
         if (rc != AA_OK) return rc;

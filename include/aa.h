@@ -131,6 +131,10 @@ typedef enum aa_precision {
     AA_PREC_FP8 = 2,  /* OCP e4m3fn activations/weights (per-output-channel weight
                        * scales), f32 accumulation; f32 log-mel input, the first
                        * conv on bf16 hi+lo as in AA_PREC_BF16 */
+    AA_PREC_BF16X3 = 3, /* split bf16: f32 activations, operands split into
+                         * bf16 hi + lo, hi*hi + hi*lo + lo*hi on bf16 MFMA
+                         * with f32 accumulation (~17-bit products): meets the
+                         * 1e-3 logit gate; the default of classify() */
 } aa_precision;
 
 int aa_model_create(const aa_layer* layers, int32_t n_layers, const float* blob, int64_t blob_len,

@@ -1,8 +1,10 @@
 """GPU parity: libaa.so CNN vs the torch-CPU fp32 oracle (oracle/cnn_oracle.py).
 
-Gate (north star): max |delta logit| <= 1e-3 in the f32 MFMA mode (exact f32
-fma chains; the residual is summation order and the BN fold).  bf16 is the
-throughput mode: its delta is reported and bounded loosely, not gated at 1e-3.
+Gate (north star): max |delta logit| <= 1e-3 in the gated modes: split-bf16
+("bf16x3", classify()'s default: ~17-bit products on bf16 MFMA, f32
+activations) and f32 MFMA (exact f32 fma chains; the residual is summation
+order and the BN fold).  bf16 is the throughput mode: its delta is reported
+and bounded loosely, not gated at 1e-3.
 fp8 (OCP e4m3fn activations and per-channel-scaled weights, BASELINE configs[4])
 likewise: reported, bounded loosely.
 """
@@ -44,6 +46,29 @@ def test_cnn_f32_parity(gpu, model_root, T):
     print(f"T={T} f32 max|dlogit|={err:.3e}")
     assert err <= LOGIT_TOL
     assert np.abs(pr - rpr).max() <= LOGIT_TOL
+
+
+@pytest.mark.parametrize("name", ["model1", "model2", "model3"])
+@pytest.mark.parametrize("T", [226, 513])
+def test_cnn_bf16x3_parity(gpu, model_root, name, T):
+    """Split-bf16 (the default precision) holds the 1e-3 logit gate on every
+    ensemble member at both hop lengths (T = 226 / 513)."""
+    path = model_root / name / "audioModel.safetensors"
+    x = calibration_input(6, 160, T, True, np.random.default_rng(T + len(name)))
+    lg, pr = _run(path, x, "bf16x3")
+    rlg, rpr = cnn_oracle.forward(path, x)
+    err = np.abs(lg - rlg).max()
+    print(f"{name} T={T} bf16x3 max|dlogit|={err:.3e} (logit range {rlg.min():.2f}..{rlg.max():.2f})")
+    assert err <= LOGIT_TOL
+    assert np.abs(pr - rpr).max() <= LOGIT_TOL
+
+
+def test_cnn_bf16x3_magtransform(gpu, tmp_path):
+    path = make_model(tmp_path / "mag3", name="magmodel", seed=11, mag=2)
+    x = calibration_input(3, 160, 226, False, np.random.default_rng(5))
+    lg, _ = _run(path, x, "bf16x3")
+    rlg, _ = cnn_oracle.forward(path, x)
+    assert np.abs(lg - rlg).max() <= LOGIT_TOL
 
 
 def test_cnn_bf16_delta(gpu, model_root):
