@@ -1025,11 +1025,11 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     X(float, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false)         \
     X(float, 9, 3, 64, 3, 1, 4, 7, 1, 3, 33, false)         \
     X(float, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)        \
-    X(bf16x3, 3, 3, 32, 3, 2, 2, 9, 1, 6, 48, false)        \
-    X(bf16x3, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false)        \
-    X(bf16x3, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false)        \
-    X(bf16x3, 9, 3, 64, 3, 1, 4, 7, 1, 3, 33, false)        \
-    X(bf16x3, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)
+    X(bf16x3, 3, 3, 32, 3, 4, 1, 3, 2, 6, 30, false)        \
+    X(bf16x3, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, false)        \
+    X(bf16x3, 3, 3, 64, 1, 4, 2, 4, 2, 16, 16, false)       \
+    X(bf16x3, 9, 3, 64, 3, 4, 2, 3, 2, 9, 21, false)        \
+    X(bf16x3, 1, 3, 128, 1, 4, 1, 3, 4, 7, 20, false)
 
 template <typename T>
 constexpr int prec_of() {
