@@ -941,6 +941,12 @@ __global__ void track_mean(const float* __restrict__ probs, int n_models, long l
     out[(size_t)t * L + c] = n > 0 ? __fdiv_rn(acc, (float)n) : NAN;
 }
 
+}  // namespace aa
+
+#include "aa_conv_x3.h"
+
+namespace aa {
+
 // ---------------------------------------------------------------------------
 // host: planner, workspace, forward, timing
 // ---------------------------------------------------------------------------
@@ -1024,12 +1030,18 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     X(float, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false)         \
     X(float, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false)         \
     X(float, 9, 3, 64, 3, 1, 4, 7, 1, 3, 33, false)         \
-    X(float, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)        \
-    X(bf16x3, 3, 3, 32, 3, 4, 1, 3, 2, 6, 30, false)        \
-    X(bf16x3, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, false)        \
-    X(bf16x3, 3, 3, 64, 1, 4, 2, 4, 2, 16, 16, false)       \
-    X(bf16x3, 9, 3, 64, 3, 4, 2, 3, 2, 9, 21, false)        \
-    X(bf16x3, 1, 3, 128, 1, 4, 1, 3, 4, 7, 20, false)
+    X(float, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)
+
+// conv_x3 (split-bf16) instantiations: (kernel, C_in, pool) -> waves (WM x
+// WN), fragments per wave (MF x NF), output tile TH x TW, weight ring in LDS
+// (1) or per-wave B fragments from global (0); picked by
+// tools/conv_bench_x3.hip sweeps
+#define AA_X3_CFGS(X)                           \
+    X(3, 3, 32, 3, 4, 1, 3, 2, 9, 21, 0)        \
+    X(3, 3, 32, 1, 4, 2, 3, 2, 10, 18, 1)       \
+    X(3, 3, 64, 1, 4, 2, 3, 2, 12, 14, 1)       \
+    X(9, 3, 64, 3, 4, 2, 4, 2, 39, 6, 0)        \
+    X(1, 3, 128, 1, 4, 2, 3, 2, 7, 20, 1)
 
 template <typename T>
 constexpr int prec_of() {
@@ -1045,7 +1057,37 @@ static int mfma_bn(int prec, int kh, int kw, int cin, int pool) {
         return WN * NF * 16;
     AA_CONV_CFGS(AA_BN)
 #undef AA_BN
+#define AA_BN3(KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, RING)                                               \
+    if (prec == AA_PREC_BF16X3 && kh == KH && kw == KW && cin == CIN && pool == POOL) return WN * NF * 16;
+    AA_X3_CFGS(AA_BN3)
+#undef AA_BN3
     return 0;
+}
+
+template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool RING, bool FUSED>
+static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream_t st, const Stage* first) {
+    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, RING>;
+    constexpr int BN = WN * NF * 16;
+    const size_t lds = x3_lds_bytes<KH, KW, CIN, BN, TH, TW, FUSED, RING>();
+    FirstConv fc{};
+    if (FUSED) {
+        const float slope = first->act == ACT_LEAKY ? first->alpha : first->act == ACT_RELU ? 0.f : 1.f;
+        fc = FirstConv{(const float*)first->d_w, first->d_b, first->act, slope, first->has_mag,
+                       first->mag_exp, first->Hin, first->Win};
+    }
+    AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
+    static size_t attr = 0;
+    if (lds > attr) {
+        AA_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = lds;
+    }
+    const int tiles_h = (s.Hout * POOL + TH - 1) / TH;
+    const int tiles_w = (s.Wout * POOL + TW - 1) / TW;
+    dim3 grid(tiles_h * tiles_w, s.cout_pad / BN, n);
+    hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, st, (const float*)in, s.Hin, s.Win, (const bf16*)s.d_w,
+                       s.d_b, (float*)out, s.Hout, s.Wout, s.cout, tiles_w, s.act, s.alpha, fc);
+    AA_LAUNCH_CHECK();
+    return AA_OK;
 }
 
 template <typename T>
@@ -1085,6 +1127,21 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
     if (s.fused_first) {
         AA_CHECK(s.kh == 3 && s.kw == 3 && s.cin == 32 && s.pool == 3, AA_ERR_UNSUPPORTED,
                  "no fused first-layer kernel for %s", s.name.c_str());
+    }
+    if constexpr (is_split<T>()) {
+#define AA_LAUNCH3(KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, RING)                                        \
+        if (s.kh == KH && s.kw == KW && s.cin == CIN && s.pool == POOL) {                                  \
+            if (s.fused_first) {                                                                           \
+                if constexpr (CIN == 32 && KH == 3 && KW == 3 && WM * WN == 4)                             \
+                    return launch_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, RING, true>(s, in, out, n, st, first); \
+            } else {                                                                                       \
+                return launch_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, RING, false>(s, in, out, n, st, first); \
+            }                                                                                              \
+        }
+        AA_X3_CFGS(AA_LAUNCH3)
+#undef AA_LAUNCH3
+        set_error("conv %dx%d cin %d pool %d: no split-bf16 kernel instantiation", s.kh, s.kw, s.cin, s.pool);
+        return AA_ERR_UNSUPPORTED;
     }
 #define AA_LAUNCH(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB)                                        \
     if constexpr (std::is_same<T, T_>::value) {                                                          \
@@ -1321,16 +1378,24 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                 for (size_t k = 0; k < wpk.size(); ++k) h[k] = f2bf(wpk[k]);
                 e = hipMemcpy(s.d_w, h.data(), wbytes, hipMemcpyHostToDevice);
             } else if (sp) {
-                // row [hi C][lo C][pad]: hi = rn_bf16(w), lo = rn_bf16(w - hi)
+                // conv_x3 steps (32-channel group g, tap t) in order s = g * ntap + t,
+                // each [cout_pad][8 units of 8 bf16]: units 0-3 hi = rn_bf16(w) of
+                // channels 32 g + 8 u .. + 7, units 4-7 lo = rn_bf16(w - hi), unit u
+                // of row o stored in slot (u + o) & 7 (aa_conv_x3.h)
                 std::vector<uint16_t> h(wpk.size(), 0);
-                const size_t rows = (size_t)ntap * s.cout_pad;
-                for (size_t r = 0; r < rows; ++r)
-                    for (int c = 0; c < s.cin; ++c) {
-                        const float w = wpk[r * cstr + c];
-                        const uint16_t hi = f2bf(w);
-                        h[r * cstr + c] = hi;
-                        h[r * cstr + s.cin + c] = f2bf(w - bf2f(hi));
-                    }
+                const int ng = s.cin / 32;
+                for (int g = 0; g < ng; ++g)
+                    for (int t = 0; t < ntap; ++t)
+                        for (int o = 0; o < s.cout_pad; ++o) {
+                            const size_t row = ((size_t)(g * ntap + t) * s.cout_pad + o) * 64;
+                            for (int c = 0; c < 32; ++c) {
+                                const float w = wpk[((size_t)t * s.cout_pad + o) * cstr + 32 * g + c];
+                                const uint16_t hi = f2bf(w);
+                                const int u = c / 8;
+                                h[row + ((u + o) & 7) * 8 + c % 8] = hi;
+                                h[row + ((u + 4 + o) & 7) * 8 + c % 8] = f2bf(w - bf2f(hi));
+                            }
+                        }
                 e = hipMemcpy(s.d_w, h.data(), wbytes, hipMemcpyHostToDevice);
             } else {
                 e = hipMemcpy(s.d_w, wpk.data(), wbytes, hipMemcpyHostToDevice);

@@ -1,0 +1,440 @@
+// Split-bf16 implicit-GEMM convolution (AA_PREC_BF16X3), included by
+// aa_cnn.hip after conv_mfma (shares FirstConv, wait_vm_lgkm, bf_hi/bf_lo).
+//
+// Same GEMM as conv_mfma -- M = output pixels of a TH x TW tile, N = output
+// channels, K = taps x C_in, D = W X^T on v_mfma_f32_16x16x32_bf16 -- with
+// every operand split into bf16 hi + lo and each product formed as
+// hi*hi + hi*lo + lo*hi (three MFMAs, f32 accumulation).  What differs is the
+// LDS image, shaped by the split's doubled operand bytes:
+//
+//  * Channel groups.  C_in is consumed 32 channels at a time: the patch of
+//    group g is staged, its KH*KW taps run, then group g+1 replaces it.  The
+//    patch therefore holds 32 channels (hi + lo = 128 B per pixel) whatever
+//    C_in is, so a block stays under 80 KiB and two blocks share a CU: one
+//    block's staging overlaps the other's MFMAs.
+//  * No padding, a rotation swizzle instead.  Pixel (R, C) of the patch is
+//    stored at (R*PW + C) * 128 B; its 16-B unit u (hi: channels 8u..8u+7,
+//    u = 0..3; lo: u = 4..7) sits in slot (u + R*TW + C) & 7.  A fragment's
+//    16 lanes read 16 consecutive TILE pixels p, whose v = R*TW + C = p +
+//    kh*TW + kw is consecutive even where the run wraps a tile row, and
+//    whose pixel parity follows v (KW - 1 is even), so every ds_read_b128
+//    lane group hits 16 distinct 4-bank groups for every tap and tile width
+//    (a padded row only achieves that for runs that do not wrap).
+//  * Weights packed per (group, tap) step as [cout][8 units] with unit u of
+//    row o in slot (u + o) & 7: the same conflict-free read for B fragments;
+//    a block's slice of a step is BN * 128 contiguous bytes, streamed by
+//    global_load_lds through the LDS ring as in conv_mfma.
+#pragma once
+
+namespace aa {
+
+constexpr int X3_CG = 32;  // channels per staged group
+
+template <int KH, int KW, int TH, int TW, bool FUSED>
+__host__ __device__ constexpr size_t x3_patch_bytes() {
+    size_t b = (size_t)(TH + KH - 1) * (TW + KW - 1) * 128;
+    if (FUSED) b += ((sizeof(float) * (TH + KH + 1) * (TW + KW + 1)) + 15) & ~(size_t)15;
+    return b;
+}
+
+template <int KH, int KW, int BN, int TH, int TW, bool FUSED>
+constexpr size_t x3_lds_bytes_nb(int nb) {  // nb = 0: no LDS ring (B fragments from global)
+    const size_t main = x3_patch_bytes<KH, KW, TH, TW, FUSED>() + (size_t)nb * BN * 128;
+    const size_t epi = (size_t)TH * TW * (BN + 4) * 4;
+    return main > epi ? main : epi;
+}
+
+// ring depth: as in conv_ring, deepen while the blocks per CU a 3-deep ring
+// allows stay resident (at most 8 slices, one per step)
+template <int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool RING = true>
+constexpr int x3_ring() {
+    if (!RING) return 0;
+    constexpr size_t cap = 160 * 1024;
+    constexpr int NSTEP = KH * KW * (CIN / X3_CG);
+    const size_t blocks = cap / x3_lds_bytes_nb<KH, KW, BN, TH, TW, FUSED>(3);
+    int nb = 3;  // the pipelined loop reads slice s+1 while s+NB-1 is issued
+    while (nb < 8 && nb < NSTEP && blocks * x3_lds_bytes_nb<KH, KW, BN, TH, TW, FUSED>(nb + 1) <= cap) ++nb;
+    return nb;
+}
+
+template <int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool RING = true>
+constexpr size_t x3_lds_bytes() {
+    return x3_lds_bytes_nb<KH, KW, BN, TH, TW, FUSED>(x3_ring<KH, KW, CIN, BN, TH, TW, FUSED, RING>());
+}
+
+template <int KH, int KW, int CIN, int WM, int WN, int NF, int TH, int TW, bool FUSED, bool RING>
+constexpr int x3_waves_per_simd() {
+    constexpr size_t lds = x3_lds_bytes<KH, KW, CIN, WN * NF * 16, TH, TW, FUSED, RING>();
+    constexpr int blocks = (int)((160 * 1024) / lds);
+    constexpr int w = (blocks * WM * WN + 3) / 4;
+    return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
+// byte offset of unit u of patch pixel (R, C)
+__device__ __forceinline__ int x3_addr(int R, int C, int u, int PW, int TW) {
+    return (R * PW + C) * 128 + (((u + R * TW + C) & 7) << 4);
+}
+
+// RING = false: no weight ring and no per-step barrier -- every wave loads
+// its own B fragments (its NF x 16 output-channel rows of the step) straight
+// from global memory (L2-resident weights) one step ahead, so waves only
+// synchronise at the two barriers around each group's staging.
+template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool FUSED = false,
+          int DIAG = 0, bool RING = true>
+__global__ __launch_bounds__(WM * WN * 64)
+__attribute__((amdgpu_waves_per_eu(1, x3_waves_per_simd<KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, RING>())))
+void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restrict__ wt,
+             const float* __restrict__ bias, float* __restrict__ out, int Hout, int Wout, int cout_store,
+             int tiles_w, int act, float alpha, FirstConv fc) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    static_assert(TH % POOL == 0 && TW % POOL == 0, "pool-aligned tile");
+    static_assert(TH * TW <= WM * MF * 16, "tile covered by the waves' fragments");
+    static_assert(CIN % X3_CG == 0, "C_in multiple of 32");
+    static_assert((KW - 1) % 2 == 0, "odd kernel width (the swizzle needs even row jumps)");
+    static_assert(!FUSED || (CIN == 32 && WM * WN == 4), "fused first layer: 32 channels, 4 waves");
+    constexpr int NTHR = WM * WN * 64;
+    constexpr int BN = WN * NF * 16;
+    constexpr int PH = TH + KH - 1, PW = TW + KW - 1;
+    constexpr int NTAP = KH * KW, NG = CIN / X3_CG, NSTEP = NTAP * NG;
+    constexpr int NW = WM * WN;
+    constexpr int NB = RING ? x3_ring<KH, KW, CIN, BN, TH, TW, FUSED, RING>() : 1;
+    constexpr int SLICE = BN * 64;                  // bf16 elements of one step's slice
+    constexpr int SLICE_LDS = BN * 128;             // bytes (a multiple of 1 KiB)
+    constexpr int GPS = SLICE_LDS / 1024;           // global_load_lds wave-instructions per slice
+    constexpr int GHI = (GPS + NW - 1) / NW, GLO = GPS / NW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* patch = smem;
+    char* Bs = smem + x3_patch_bytes<KH, KW, TH, TW, FUSED>();
+
+    const int n = blockIdx.z;
+    const int th = blockIdx.x / tiles_w, tw = blockIdx.x - (blockIdx.x / tiles_w) * tiles_w;
+    const int oh0 = th * TH, ow0 = tw * TW;
+    const int wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+
+    // weight ring: slice of step s = wt[s][cout_pad][64] rows of this block
+    const size_t step_stride = (size_t)gridDim.y * SLICE;
+    const bf16* wsl = wt + (size_t)blockIdx.y * SLICE + lane * 8;
+#define X3_GLDS(s)                                                                                       \
+    _Pragma("unroll") for (int u_ = 0; u_ < GHI; ++u_) {                                               \
+        const int g_ = u_ * NW + wave0;                                                                  \
+        if (GPS % NW == 0 || g_ < GPS)                                                                  \
+            __builtin_amdgcn_global_load_lds(                                                           \
+                (const __attribute__((address_space(1))) void*)(wsl + (size_t)(s) * step_stride + g_ * 512), \
+                (__attribute__((address_space(3))) void*)(Bs + ((s) % NB) * SLICE_LDS + g_ * 1024), 16, 0, 0); \
+    }
+    if constexpr (RING && !(DIAG & 32)) {
+#pragma unroll
+        for (int s = 0; s < NB - 1; ++s)
+            if (s < NSTEP) { X3_GLDS(s) }
+    }
+
+    // per-lane fragment geometry: tile pixel p of fragment i -> patch byte
+    // base (tap 0) and its swizzle phase (p + q) for this lane's unit q
+    const int wave = wave0, wm = wave % WM, wn = wave / WM;
+    const int q = lane >> 4;
+    int abase[MF], aph[MF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+        int p = (wm * MF + i) * 16 + (lane & 15);
+        if (p >= TH * TW || (DIAG & 8)) p = 0;  // padding rows: computed, never stored
+        const int r = p / TW, c = p - (p / TW) * TW;
+        abase[i] = (r * PW + c) * 128;
+        aph[i] = p + q;  // v = r*TW + c = p
+    }
+    int bofs[NF];  // byte offset of the lane's hi unit in a slice (lo: ^ 64)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+        const int row = wn * NF * 16 + j * 16 + (lane & 15);
+        bofs[j] = row * 128 + (((q + row) & 7) << 4);
+    }
+    const bf16* wblk = wt + (size_t)blockIdx.y * SLICE;  // RING = false: this block's rows of step 0
+    const bool hi_share = (GPS % NW == 0) || wave < GPS % NW;
+
+    f32x4 acc[MF][NF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    struct FragSet {
+        bf16x8 ah[MF], al[MF], bh[NF], bl[NF];
+    };
+    FragSet F0, F1;
+    auto read_a = [&](FragSet& f, int t) {
+        if (DIAG & 128) return;
+        const int kh = t / KW, kw = t - (t / KW) * KW;
+        const int toff = (kh * PW + kw) * 128, tv = kh * TW + kw;
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+            const int a = abase[i] + toff + (((aph[i] + tv) & 7) << 4);
+            f.ah[i] = *reinterpret_cast<const bf16x8*>(patch + a);
+            f.al[i] = *reinterpret_cast<const bf16x8*>(patch + (a ^ 64));
+        }
+    };
+    auto read_b = [&](FragSet& f, int s) {
+        if (DIAG & 128) return;
+        if constexpr (!RING) {
+            const char* bsl = reinterpret_cast<const char*>(wblk + (size_t)((DIAG & 16) ? 0 : s) * step_stride);
+#pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                f.bh[j] = *reinterpret_cast<const bf16x8*>(bsl + bofs[j]);
+                f.bl[j] = *reinterpret_cast<const bf16x8*>(bsl + (bofs[j] ^ 64));
+            }
+            return;
+        }
+        const char* bsl = Bs + ((DIAG & 16) ? 0 : (s % NB)) * SLICE_LDS;
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+            f.bh[j] = *reinterpret_cast<const bf16x8*>(bsl + bofs[j]);
+            f.bl[j] = *reinterpret_cast<const bf16x8*>(bsl + (bofs[j] ^ 64));
+        }
+    };
+    auto step = [&](FragSet& cur, FragSet& nxt, int g, int t) {
+        const int s = g * NTAP + t;
+        // own share of slice s+1 landed (s+2 .. s+NB-2 may stay in flight), own LDS reads done
+        if constexpr (RING) {
+            const int ahead = s + 1 < NSTEP ? min(NB - 3, NSTEP - 2 - s) : 0;
+            if (DIAG & 32) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            } else if (hi_share) {
+                wait_vm_lgkm<GHI>(ahead);
+            } else {
+                wait_vm_lgkm<GLO>(ahead);
+            }
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!(DIAG & 32)) {
+                if (s + NB - 1 < NSTEP) { X3_GLDS(s + NB - 1) }  // into the buffer B(s-1) was read from
+            }
+        }
+        if (s + 1 < NSTEP) read_b(nxt, s + 1);
+        if (t + 1 < NTAP) read_a(nxt, t + 1);
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bh[j], cur.ah[i], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bl[j], cur.ah[i], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bh[j], cur.al[i], acc[i][j], 0, 0, 0);
+            }
+    };
+
+    if constexpr (!RING) read_b(F0, 0);  // its latency hides behind the first staging
+    for (int g = 0; g < NG; ++g) {
+        // ---- stage channel group g of the patch (hi / lo planes, swizzled) ----
+        if (g > 0) __syncthreads();  // every wave is done with group g-1's patch
+        if constexpr (DIAG & 1) {
+        } else if constexpr (!FUSED) {
+            constexpr int ITEMS = (PH * PW + 7) / 8 * 64;  // (pixel, channel quad), pixels in 8s
+            constexpr int U = 4;
+            const float* src = in + (size_t)n * Hin * Win * CIN + g * X3_CG;
+            for (int i0 = 0; i0 < ITEMS; i0 += U * NTHR) {
+                float4 v[U];
+                bool ok[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int idx = i0 + u * NTHR + threadIdx.x;
+                    // lanes 0-7 / 8-15 of a 16-lane store group take pixels 4 apart:
+                    // their swizzle slots are disjoint
+                    const int blk = idx >> 6, w8 = (idx >> 3) & 7;
+                    const int pix = blk * 8 + ((w8 & 1) << 2) + (w8 >> 1), cq = idx & 7;
+                    const int R = pix / PW, C = pix - R * PW;
+                    const int gh = oh0 + R, gw = ow0 + C;
+                    ok[u] = pix < PH * PW && gh < Hin && gw < Win;
+                    const int ch = min(gh, Hin - 1), cw = min(gw, Win - 1);
+                    v[u] = *reinterpret_cast<const float4*>(src + ((size_t)ch * Win + cw) * CIN + cq * 4);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int idx = i0 + u * NTHR + threadIdx.x;
+                    const int blk = idx >> 6, w8 = (idx >> 3) & 7;
+                    const int pix = blk * 8 + ((w8 & 1) << 2) + (w8 >> 1), cq = idx & 7;
+                    if (pix < PH * PW) {
+                        const int R = pix / PW, C = pix - R * PW;
+                        const float4 x = ok[u] ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        bf16x4 h, l;
+                        h[0] = bf_hi(x.x); l[0] = bf_lo(x.x);
+                        h[1] = bf_hi(x.y); l[1] = bf_lo(x.y);
+                        h[2] = bf_hi(x.z); l[2] = bf_lo(x.z);
+                        h[3] = bf_hi(x.w); l[3] = bf_lo(x.w);
+                        const int a = x3_addr(R, C, cq >> 1, PW, TW) + (cq & 1) * 8;
+                        *reinterpret_cast<bf16x4*>(patch + a) = h;
+                        *reinterpret_cast<bf16x4*>(patch + (a ^ 64)) = l;
+                    }
+                }
+            }
+        } else {
+            // fused first layer (C_in = 1, 3x3 -> 32): log-mel patch (PH+2) x (PW+2)
+            // in LDS after the activation patch, then per 32 patch pixels three
+            // v_mfma_f32_32x32x16_bf16 (weights hi/lo x log-mel hi/lo, the 9 taps
+            // in k, the bias as C), activation, hi/lo into the swizzled patch
+            constexpr int XW = PW + 2, XN = (PH + 2) * XW;
+            float* X = reinterpret_cast<float*>(smem + (size_t)PH * PW * 128);
+            const float* lm = in + (size_t)n * fc.H0 * fc.W0;
+            for (int i0 = 0; i0 < ((DIAG & 512) ? 0 : XN); i0 += 4 * NTHR) {
+                float v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int idx = min(i0 + u * NTHR + (int)threadIdx.x, XN - 1);
+                    const int r = idx / XW, c = idx - r * XW;
+                    v[u] = lm[(size_t)min(oh0 + r, fc.H0 - 1) * fc.W0 + min(ow0 + c, fc.W0 - 1)];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int idx = i0 + u * NTHR + threadIdx.x;
+                    if (idx < XN) X[idx] = fc.has_mag ? powf(v[u], fc.mag_exp) : v[u];
+                }
+            }
+            const int l32 = lane & 31, kg = lane >> 5;
+            bf16x8 wa, wal;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int tap = 8 * kg + j;
+                const float wv = tap < 9 ? fc.w[l32 * 9 + tap] : 0.f;
+                wa[j] = bf_hi(wv);
+                wal[j] = bf_lo(wv);
+            }
+            f32x16 cb;  // D row (channel) of register r: 8 (r / 4) + 4 kg + r % 4
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cb[r] = fc.b[8 * (r >> 2) + 4 * kg + (r & 3)];
+            const float ae = fc.alpha;  // host: act folded to a slope in [0, 1]
+            const int off0 = kg ? 2 * XW + 2 : 0;  // k-group 1 only needs tap 8 (j = 0)
+            __syncthreads();
+            constexpr int NPX = PH * PW;
+            constexpr int NGRP = (NPX + 31) / 32;
+            for (int g0 = wave0; g0 < ((DIAG & 64) ? 0 : NGRP); g0 += 8) {
+                bf16x8 xh[2], xl[2];
+                int pix[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    pix[u] = min((g0 + 4 * u) * 32 + l32, NPX - 1);
+                    const int r = pix[u] / PW, c = pix[u] - r * PW;
+                    const float* xp = X + r * XW + c;
+                    float xv[8];
+                    xv[0] = xp[off0];
+#pragma unroll
+                    for (int j = 1; j < 8; ++j) xv[j] = xp[(j / 3) * XW + j % 3];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        xh[u][j] = bf_hi(xv[j]);
+                        xl[u][j] = bf_lo(xv[j]);
+                    }
+                }
+                f32x16 d[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xh[u], cb, 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xl[u], d[u], 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wal, xh[u], d[u], 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    if ((g0 + 4 * u) * 32 + l32 < NPX) {
+                        const int R = pix[u] / PW, C = pix[u] - R * PW;
+#pragma unroll
+                        for (int qq = 0; qq < 4; ++qq) {  // channels 8 qq + 4 kg + e: unit qq, byte 8 kg
+                            bf16x4 h, l;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const float o = fmaxf(d[u][4 * qq + e], d[u][4 * qq + e] * ae);
+                                h[e] = bf_hi(o);
+                                l[e] = bf_lo(o);
+                            }
+                            const int a = x3_addr(R, C, qq, PW, TW) + kg * 8;
+                            *reinterpret_cast<bf16x4*>(patch + a) = h;
+                            *reinterpret_cast<bf16x4*>(patch + (a ^ 64)) = l;
+                        }
+                    }
+                }
+            }
+        }
+
+        // ---- the group's taps: one 32-deep K chunk each, through the ring.
+        // Software-pipelined by one step: the barrier at the top of step s
+        // publishes slice s+1, and B(s+1) / A(s+1) are read into the other
+        // fragment set while step s's MFMAs run on operands already in
+        // registers -- no wave waits out an LDS read after a barrier. ----
+        if (g == 0) {  // slice 0: this wave's share landed before the barrier publishing the patch
+            if constexpr (RING && !(DIAG & 32)) {
+                if (hi_share) wait_vm_lgkm<GHI>(min(NB - 2, NSTEP - 1));
+                else wait_vm_lgkm<GLO>(min(NB - 2, NSTEP - 1));
+            }
+        }
+        __syncthreads();
+        if (g == 0) {
+            if constexpr (RING) read_b(F0, 0);  // (RING = false: issued before the first staging)
+        }
+        else if constexpr ((NTAP - 1) % 2 == 0) {  // the previous group's last step left B in F1
+#pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                F0.bh[j] = F1.bh[j];
+                F0.bl[j] = F1.bl[j];
+            }
+        }
+        if (!(DIAG & 2)) read_a(F0, 0);
+        for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); t += 2) {
+            step(F0, F1, g, t);
+            if (t + 1 < NTAP) step(F1, F0, g, t + 1);
+        }
+    }
+#undef X3_GLDS
+    __syncthreads();  // patch and ring no longer needed: the f32 tile reuses LDS
+
+    // ---- epilogue: f32 tile [TH*TW][BN+4], pool, bias, activation, NHWC f32 ----
+    constexpr int ESTR = BN + 4;
+    float* E = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+        const int c0 = wn * NF * 16 + j * 16 + 4 * q;
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+            const int p = (wm * MF + i) * 16 + (lane & 15);
+            if (p < TH * TW)
+                *reinterpret_cast<float4*>(E + p * ESTR + c0) =
+                    make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+    }
+    __syncthreads();
+    constexpr int PHo = TH / POOL, PWo = TW / POOL;
+    constexpr int G = BN / 8;
+    static_assert(NTHR % G == 0, "fixed channel group per thread");
+    const int oh0s = oh0 / POOL, ow0s = ow0 / POOL;
+    const int col = (threadIdx.x % G) * 8;
+    const int ch0 = blockIdx.y * BN + col;
+    float bv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bv[c] = bias[ch0 + c];  // bias is padded to cout_pad
+    float* dst = out + (size_t)n * Hout * Wout * cout_store;
+    for (int qo = threadIdx.x / G; qo < PHo * PWo; qo += NTHR / G) {
+        const int pr = qo / PWo, pc = qo - (qo / PWo) * PWo;
+        const int gh = oh0s + pr, gw = ow0s + pc;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = -INFINITY;
+#pragma unroll
+        for (int dy = 0; dy < POOL; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < POOL; ++dx) {
+                const float* e = E + ((pr * POOL + dy) * TW + pc * POOL + dx) * ESTR + col;
+                const float4 a = reinterpret_cast<const float4*>(e)[0], b = reinterpret_cast<const float4*>(e)[1];
+                v[0] = fmaxf(v[0], a.x); v[1] = fmaxf(v[1], a.y); v[2] = fmaxf(v[2], a.z); v[3] = fmaxf(v[3], a.w);
+                v[4] = fmaxf(v[4], b.x); v[5] = fmaxf(v[5], b.y); v[6] = fmaxf(v[6], b.z); v[7] = fmaxf(v[7], b.w);
+            }
+        if (gh >= Hout || gw >= Wout) continue;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = apply_act(v[c] + bv[c], act, alpha);
+        if constexpr ((DIAG & 4) != 0) {
+            if (v[0] != 12345.f) continue;  // keep the values live, store (almost) never
+        }
+        float* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
+        if (ch0 + 8 <= cout_store) {
+            reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
+            reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+            for (int c = 0; c < 8 && ch0 + c < cout_store; ++c) o[c] = v[c];
+        }
+    }
+}
+
+}  // namespace aa

@@ -1,4 +1,4 @@
-// Diagnostic harness: time split-bf16 (bf16x3) conv_mfma tilings of model1's
+// Diagnostic harness: time split-bf16 (bf16x3) conv_x3 tilings of model1's
 // layers at T = 226 on random f32 activations, 64 windows per launch.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include
 //   tools/conv_bench_x3.hip audio-analysis_amd/csrc/aa_api.cpp -o tools/conv_bench_x3 ; run on the GPU box.
@@ -10,15 +10,13 @@
 
 using namespace aa;
 
-template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW,
-          bool FUSED, int DIAG = 0>
+template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool FUSED,
+          int DIAG = 0, bool RING = true>
 static void time_one(const char* tag, int n, int Hin, int Win, int cout, const void* in, const void* w,
                      const float* b, void* out, FirstConv fc, int iters) {
-    using GT = typename Prec<T>::G;
-    using LT = typename Prec<T>::L;
-    auto k = conv_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, DIAG, false, true>;
+    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, DIAG, RING>;
     constexpr int BN = WN * NF * 16;
-    const size_t lds = conv_lds_bytes<T, KH, KW, CIN, BN, TH, TW, FUSED, false>();
+    const size_t lds = x3_lds_bytes<KH, KW, CIN, BN, TH, TW, FUSED, RING>();
     if (lds > 160 * 1024) {
         printf("%-8s %dx%d cin %3d WM%d WN%d MF%2d NF%d %2dx%2d  LDS %zu: skip\n", tag, KH, KW, CIN, WM, WN, MF, NF,
                TH, TW, lds);
@@ -33,12 +31,12 @@ static void time_one(const char* tag, int n, int Hin, int Win, int cout, const v
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     for (int i = 0; i < 3; ++i)
-        hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, 0, (const GT*)in, Hin, Win, (const LT*)w, b, (GT*)out,
-                           Hout, Wout, cout, tiles_w, 1, 0.3f, fc);
+        hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, 0, (const float*)in, Hin, Win, (const bf16*)w, b,
+                           (float*)out, Hout, Wout, cout, tiles_w, 1, 0.3f, fc);
     (void)hipEventRecord(e0, 0);
     for (int i = 0; i < iters; ++i)
-        hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, 0, (const GT*)in, Hin, Win, (const LT*)w, b, (GT*)out,
-                           Hout, Wout, cout, tiles_w, 1, 0.3f, fc);
+        hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, 0, (const float*)in, Hin, Win, (const bf16*)w, b,
+                           (float*)out, Hout, Wout, cout, tiles_w, 1, 0.3f, fc);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0;
@@ -46,8 +44,8 @@ static void time_one(const char* tag, int n, int Hin, int Win, int cout, const v
     const float us = 1e3f * ms / iters;
     double fl = 2.0 * n * Hc * Wc * KH * KW * CIN * cout;
     if (FUSED) fl += 2.0 * n * (Hin) * (Win) * 9 * 32;
-    printf("%-8s %dx%d cin %3d WM%d WN%d MF%2d NF%d %2dx%2d  LDS %6zu  grid %6d  %7.1f us  %6.1f TF (%.3f of 833)\n",
-           tag, KH, KW, CIN, WM, WN, MF, NF, TH, TW, lds, grid.x * grid.y * grid.z, us, fl / us * 1e-6,
+    printf("%-8s%s %dx%d cin %3d WM%d WN%d MF%2d NF%d %2dx%2d  LDS %6zu  grid %6d  %7.1f us  %6.1f TF (%.3f of 833)\n",
+           tag, RING ? "" : "G", KH, KW, CIN, WM, WN, MF, NF, TH, TW, lds, grid.x * grid.y * grid.z, us, fl / us * 1e-6,
            fl / us * 1e-6 / 833.3);
 }
 
@@ -78,43 +76,56 @@ int main(int argc, char** argv) {
     if (which == 9) {
         // DIAG bits (aa_cnn.hip): 1 no staging, 4 no stores, 32 no weight stream,
         // 128 no fragment reads after the first, 2 no MFMA loop
-#define ABL5(D) time_one<bf16x3, 9, 3, 64, 4, 2, 3, 2, 3, 9, 21, false, D>("c5 d" #D, n, 48, 70, 128, in, w, b, out, fc, it);
-#define ABL2(D) time_one<bf16x3, 3, 3, 32, 4, 1, 3, 2, 3, 6, 30, true, D>("c2 d" #D, n, 158, 224, 32, in, w, b, out, f1, it);
-#define ABL4(D) time_one<bf16x3, 3, 3, 64, 4, 2, 4, 2, 1, 16, 16, false, D>("c4 d" #D, n, 50, 72, 64, in, w, b, out, fc, it);
+#define ABL5(D) time_one<9, 3, 64, 3, 2, 5, 2, 3, 39, 6, false, D>("c5 d" #D, n, 48, 70, 128, in, w, b, out, fc, it);
+#define ABL2(D) time_one<3, 3, 32, 4, 1, 3, 2, 3, 6, 30, true, D>("c2 d" #D, n, 158, 224, 32, in, w, b, out, f1, it);
+#define ABL4(D) time_one<3, 3, 64, 4, 2, 4, 2, 1, 16, 16, false, D>("c4 d" #D, n, 50, 72, 64, in, w, b, out, fc, it);
         ABL5(0) ABL5(1) ABL5(2) ABL5(4) ABL5(33) ABL5(161) ABL5(165) ABL5(37)
         ABL2(0) ABL2(2) ABL2(64) ABL2(4) ABL2(32) ABL2(160) ABL2(96)
         ABL4(0) ABL4(1) ABL4(2) ABL4(33) ABL4(161) ABL4(165)
         return 0;
     }
     // model1 at T = 226: (Hin, Win) of each conv's input
-#define C2(WM, WN, MF, NF, TH, TW) time_one<bf16x3, 3, 3, 32, WM, WN, MF, NF, 3, TH, TW, true>("c1+c2", n, 158, 224, 32, in, w, b, out, f1, it);
-#define C3(WM, WN, MF, NF, TH, TW) time_one<bf16x3, 3, 3, 32, WM, WN, MF, NF, 1, TH, TW, false>("c3", n, 52, 74, 64, in, w, b, out, fc, it);
-#define C4(WM, WN, MF, NF, TH, TW) time_one<bf16x3, 3, 3, 64, WM, WN, MF, NF, 1, TH, TW, false>("c4", n, 50, 72, 64, in, w, b, out, fc, it);
-#define C5(WM, WN, MF, NF, TH, TW) time_one<bf16x3, 9, 3, 64, WM, WN, MF, NF, 3, TH, TW, false>("c5", n, 48, 70, 128, in, w, b, out, fc, it);
-#define C6(WM, WN, MF, NF, TH, TW) time_one<bf16x3, 1, 3, 128, WM, WN, MF, NF, 1, TH, TW, false>("c6", n, 13, 22, 256, in, w, b, out, fc, it);
+#define C2(WM, WN, MF, NF, TH, TW) time_one<3, 3, 32, WM, WN, MF, NF, 3, TH, TW, true>("c1+c2", n, 158, 224, 32, in, w, b, out, f1, it);
+#define C3(WM, WN, MF, NF, TH, TW) time_one<3, 3, 32, WM, WN, MF, NF, 1, TH, TW, false>("c3", n, 52, 74, 64, in, w, b, out, fc, it);
+#define C4(WM, WN, MF, NF, TH, TW) time_one<3, 3, 64, WM, WN, MF, NF, 1, TH, TW, false>("c4", n, 50, 72, 64, in, w, b, out, fc, it);
+#define C5(WM, WN, MF, NF, TH, TW) time_one<9, 3, 64, WM, WN, MF, NF, 3, TH, TW, false>("c5", n, 48, 70, 128, in, w, b, out, fc, it);
+#define G2(WM, WN, MF, NF, TH, TW) time_one<3, 3, 32, WM, WN, MF, NF, 3, TH, TW, true, 0, false>("c1+c2", n, 158, 224, 32, in, w, b, out, f1, it);
+#define G3(WM, WN, MF, NF, TH, TW) time_one<3, 3, 32, WM, WN, MF, NF, 1, TH, TW, false, 0, false>("c3", n, 52, 74, 64, in, w, b, out, fc, it);
+#define G4(WM, WN, MF, NF, TH, TW) time_one<3, 3, 64, WM, WN, MF, NF, 1, TH, TW, false, 0, false>("c4", n, 50, 72, 64, in, w, b, out, fc, it);
+#define G5(WM, WN, MF, NF, TH, TW) time_one<9, 3, 64, WM, WN, MF, NF, 3, TH, TW, false, 0, false>("c5", n, 48, 70, 128, in, w, b, out, fc, it);
+#define G6(WM, WN, MF, NF, TH, TW) time_one<1, 3, 128, WM, WN, MF, NF, 1, TH, TW, false, 0, false>("c6", n, 13, 22, 256, in, w, b, out, fc, it);
+#define C6(WM, WN, MF, NF, TH, TW) time_one<1, 3, 128, WM, WN, MF, NF, 1, TH, TW, false>("c6", n, 13, 22, 256, in, w, b, out, fc, it);
+    if (which == 10) {  // the shipped c5 / c2 tiles alone (PMC passes)
+        C5(3, 2, 5, 2, 39, 6) C2(4, 1, 3, 2, 6, 30)
+        return 0;
+    }
     if (!which || which == 2) {
-        C2(2, 2, 9, 1, 6, 48) C2(4, 1, 3, 2, 9, 21) C2(4, 1, 4, 2, 12, 21) C2(4, 1, 5, 2, 12, 24)
-        C2(4, 1, 6, 2, 12, 30) C2(4, 1, 4, 2, 9, 27) C2(4, 1, 4, 2, 6, 42) C2(2, 2, 6, 1, 9, 21)
-        C2(4, 1, 6, 2, 18, 21) C2(4, 1, 2, 2, 6, 18) C2(4, 1, 3, 2, 6, 30) C2(2, 2, 4, 1, 6, 21)
+        C2(4, 1, 3, 2, 6, 30) C2(4, 1, 4, 2, 12, 21) C2(4, 1, 6, 2, 12, 30) C2(4, 1, 6, 2, 6, 60)
+        C2(4, 1, 3, 2, 9, 21) C2(4, 1, 5, 2, 6, 48)
+        G2(4, 1, 3, 2, 6, 30) G2(4, 1, 4, 2, 12, 21) G2(4, 1, 6, 2, 12, 30) G2(4, 1, 6, 2, 6, 60)
+        G2(4, 1, 3, 2, 9, 21) G2(4, 1, 5, 2, 6, 48) G2(4, 1, 7, 2, 12, 36) G2(4, 1, 8, 2, 12, 42)
+        G2(4, 1, 4, 2, 6, 42) G2(4, 1, 6, 2, 18, 21)
     }
     if (!which || which == 3) {
-        C3(1, 4, 9, 1, 6, 24) C3(2, 2, 4, 2, 8, 16) C3(4, 1, 2, 4, 8, 16) C3(2, 2, 6, 2, 10, 18)
-        C3(4, 1, 3, 4, 12, 16) C3(2, 2, 8, 2, 16, 16) C3(4, 2, 4, 2, 16, 16) C3(2, 4, 8, 1, 16, 16)
-        C3(4, 1, 2, 2, 8, 16) C3(2, 2, 4, 1, 8, 16)
+        C3(4, 2, 3, 2, 10, 18) C3(4, 2, 2, 2, 5, 24) C3(4, 2, 4, 2, 16, 16)
+        G3(4, 2, 3, 2, 10, 18) G3(4, 2, 2, 2, 5, 24) G3(4, 2, 4, 2, 16, 16) G3(4, 1, 4, 4, 10, 24)
+        G3(4, 2, 4, 2, 10, 24) G3(2, 2, 8, 2, 10, 24) G3(4, 1, 2, 4, 5, 24)
     }
     if (!which || which == 4) {
-        C4(1, 4, 9, 1, 6, 24) C4(2, 2, 4, 2, 8, 16) C4(4, 1, 2, 4, 8, 16) C4(2, 2, 6, 2, 10, 18)
-        C4(4, 1, 3, 4, 12, 16) C4(2, 2, 8, 2, 16, 16) C4(4, 2, 4, 2, 16, 16) C4(2, 4, 8, 1, 16, 16)
-        C4(4, 1, 2, 2, 8, 16) C4(2, 2, 4, 1, 8, 16)
+        C4(4, 2, 3, 2, 12, 14) C4(4, 2, 4, 2, 16, 14) C4(2, 2, 7, 2, 16, 14)
+        G4(4, 2, 3, 2, 12, 14) G4(4, 2, 4, 2, 16, 14) G4(2, 2, 7, 2, 16, 14) G4(4, 1, 4, 4, 16, 14)
+        G4(4, 2, 6, 2, 24, 14) G4(4, 1, 3, 4, 12, 14) G4(4, 2, 7, 2, 16, 28)
     }
     if (!which || which == 5) {
-        C5(1, 4, 7, 1, 3, 33) C5(2, 2, 4, 2, 6, 21) C5(4, 1, 2, 4, 6, 18) C5(2, 2, 6, 2, 9, 21)
-        C5(4, 2, 3, 2, 9, 21) C5(4, 2, 2, 2, 6, 21) C5(4, 1, 2, 2, 6, 21) C5(4, 2, 3, 1, 9, 21)
-        C5(8, 1, 2, 2, 9, 21) C5(4, 1, 4, 2, 3, 60) C5(2, 2, 4, 2, 3, 42) C5(4, 1, 2, 2, 3, 33)
+        C5(5, 2, 3, 2, 39, 6) C5(2, 2, 4, 2, 3, 33) C5(4, 2, 2, 2, 3, 33)
+        G5(5, 2, 3, 2, 39, 6) G5(2, 2, 4, 2, 3, 33) G5(4, 2, 2, 2, 3, 33) G5(4, 1, 4, 4, 39, 6)
+        G5(4, 2, 4, 2, 39, 6) G5(4, 2, 4, 2, 6, 33) G5(2, 4, 8, 1, 39, 6) G5(4, 4, 4, 1, 39, 6)
+        G5(8, 2, 4, 2, 39, 12) G5(4, 2, 4, 2, 3, 66) G5(8, 2, 2, 2, 39, 6) G5(4, 1, 2, 4, 3, 33)
     }
     if (!which || which == 6) {
-        C6(2, 2, 5, 1, 6, 24) C6(2, 2, 5, 2, 6, 24) C6(4, 1, 3, 4, 7, 20) C6(2, 2, 3, 2, 4, 20)
-        C6(1, 4, 5, 1, 4, 20) C6(2, 2, 5, 1, 13, 12) C6(2, 2, 3, 1, 4, 20)
+        C6(4, 2, 3, 2, 7, 20) C6(4, 1, 3, 4, 7, 20)
+        G6(4, 2, 3, 2, 7, 20) G6(4, 1, 3, 4, 7, 20) G6(4, 2, 5, 2, 13, 20) G6(4, 4, 3, 1, 7, 20)
+        G6(2, 2, 5, 2, 13, 12)
     }
     hipError_t e = hipGetLastError();
     printf("last error: %s\n", hipGetErrorString(e));

@@ -25,8 +25,8 @@ for line in r.stderr.splitlines():
         k, v = t.split(":", 1)
         rows[cur][k.strip()] = v.strip()
 for name, d in rows.items():
-    if filt in name:
-        dm = subprocess.run(["c++filt"], input=name, capture_output=True, text=True).stdout.strip()
-        dm = re.sub(r"\(.*", "", dm)
+    dm = subprocess.run(["c++filt"], input=name, capture_output=True, text=True).stdout.strip()
+    dm = re.sub(r"\(.*", "", dm)
+    if filt in dm:
         print(f"{d.get('VGPRs','?'):>4} v {d.get('AGPRs','?'):>3} a {d.get('ScratchSize [bytes/lane]','?'):>4} scr "
               f"occ {d.get('Occupancy [waves/SIMD]','?'):>2} lds {d.get('LDS Size [bytes/block]','?'):>6}  {dm}")
