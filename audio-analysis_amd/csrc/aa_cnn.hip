@@ -118,22 +118,6 @@ __device__ __forceinline__ f32x4 mfma_chunk(const Frag<float>& a, const Frag<flo
     for (int s = 0; s < 8; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[s], b.v[s], c, 0, 0, 0);
     return c;
 }
-// split-bf16: the hi fragment at p, the lo fragment LO elements further (the
-// [hi C][lo C] row layout); hi*hi + hi*lo + lo*hi, the bf16 lane layout
-template <int LO>
-struct FragSplit {
-    bf16x8 h, l;
-    __device__ __forceinline__ void load(const bf16* p) {
-        h = *reinterpret_cast<const bf16x8*>(p);
-        l = *reinterpret_cast<const bf16x8*>(p + LO);
-    }
-};
-template <int LO>
-__device__ __forceinline__ f32x4 mfma_chunk(const FragSplit<LO>& a, const FragSplit<LO>& b, f32x4 c) {
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);
-}
 
 template <typename T>
 __device__ __forceinline__ T to_t(float x);
@@ -214,11 +198,9 @@ __global__ __launch_bounds__(256) void conv_small(const float* __restrict__ in, 
 // ds_read_b128 lane group of the fragment reads conflict-free); fp8 rows
 // padded by 16 B (48 / 80 / 144-B strides put the 16 rows of a ds_read_b64
 // half-wave on distinct 4-bank groups); f32 (parity mode) keeps a 16-B pad.
-// Split-bf16: a pixel / weight row is [hi C][lo C][16 pad], 4C + 32 bytes
-// (again 2 mod 4 16-B units for C % 32 == 0).
 template <typename T>
 __host__ __device__ constexpr int conv_cstr(int cin) {
-    return is_split<T>() ? 2 * cin + 16 : cin + (sizeof(T) == 1 ? 16 : sizeof(T) == 2 ? 16 : 4);
+    return cin + (sizeof(T) == 1 ? 16 : sizeof(T) == 2 ? 16 : 4);
 }
 
 // LDS of one conv_mfma block: [staged patch][f32 log-mel patch if FUSED]
@@ -318,11 +300,10 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
                                                  int tiles_w, int act, float alpha, FirstConv fc) {
     using LT = typename Prec<T>::L;  // LDS / fragment element
     using GT = typename Prec<T>::G;  // HBM activation element
-    constexpr bool SPLIT = is_split<T>();
     constexpr bool F8 = is_fp8<T>();
+    static_assert(!is_split<T>(), "split-bf16 runs conv_x3 (aa_conv_x3.h)");
     static_assert(TH % POOL == 0 && TW % POOL == 0, "pool-aligned tile");
     static_assert(TH * TW <= WM * MF * 16, "tile covered by the waves' fragments");
-    static_assert(!(SPLIT && EBF16), "split-bf16 keeps an f32 epilogue tile");
     constexpr int NTHR = WM * WN * 64;
     static_assert(CIN % 32 == 0, "C_in multiple of 32");
     constexpr int BN = WN * NF * 16;
@@ -370,43 +351,6 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
 
     // ---- stage the input patch ----
     if constexpr (DIAG & 1) {
-    } else if constexpr (!FUSED && SPLIT) {
-        // f32 activations, 16-B loads (4 channels), split into the hi and lo
-        // planes of the pixel's LDS row
-        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-        constexpr int VPP = CIN / 4;
-        constexpr int U = 4;
-        const int total = PH * PW * VPP;
-        const float* src = in + (size_t)n * Hin * Win * CIN;
-        for (int i0 = 0; i0 < total; i0 += U * NTHR) {
-            float4 v[U];
-            bool ok[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int idx = i0 + u * NTHR + threadIdx.x;
-                const int pix = idx / VPP, cv = idx - pix * VPP;
-                const int r = pix / PW, c = pix - r * PW;
-                const int gh = oh0 + r, gw = ow0 + c;
-                ok[u] = idx < total && gh < Hin && gw < Win;
-                const int ch = min(gh, Hin - 1), cw = min(gw, Win - 1);
-                v[u] = *reinterpret_cast<const float4*>(src + ((size_t)ch * Win + cw) * CIN + cv * 4);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int idx = i0 + u * NTHR + threadIdx.x;
-                if (idx < total) {
-                    const int pix = idx / VPP, cv = idx - pix * VPP;
-                    const float4 x = ok[u] ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
-                    bf16x4 h, l;
-                    { const float s_ = x.x; h[0] = bf_hi(s_); l[0] = bf_lo(s_); }
-                    { const float s_ = x.y; h[1] = bf_hi(s_); l[1] = bf_lo(s_); }
-                    { const float s_ = x.z; h[2] = bf_hi(s_); l[2] = bf_lo(s_); }
-                    { const float s_ = x.w; h[3] = bf_hi(s_); l[3] = bf_lo(s_); }
-                    *reinterpret_cast<bf16x4*>(patch + pix * CSTR + cv * 4) = h;
-                    *reinterpret_cast<bf16x4*>(patch + pix * CSTR + CIN + cv * 4) = l;
-                }
-            }
-        }
     } else if constexpr (!FUSED) {
         // batched, unconditional 16-B loads from clamped addresses (a
         // load-or-zero branch would serialise them); out-of-image pixels only
@@ -465,16 +409,13 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
             // B entries may hold any finite value), the bias as the C input,
             // then the activation, bf16, and 8-byte stores of 4 channels into
             // the patch.  Lane l: pixel l % 32, k-group / channel quad l / 32.
-            // Split-bf16 adds the weights' lo part (a third MFMA) and stores
-            // the activations as hi and lo planes.
             const int wave1 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
             const int l32 = threadIdx.x & 31, kg = (threadIdx.x >> 5) & 1;
-            bf16x8 wa, wal;
+            bf16x8 wa;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int tap = 8 * kg + j;
-                const float wv = tap < 9 ? fc.w[l32 * 9 + tap] : 0.f;
-                { const float s_ = wv; wa[j] = bf_hi(s_); wal[j] = bf_lo(s_); }
+                wa[j] = tap < 9 ? (bf16)fc.w[l32 * 9 + tap] : (bf16)0.f;
             }
             f32x16 cb;  // D row (channel) of register r: 8 (r / 4) + 4 kg + r % 4
 #pragma unroll
@@ -488,7 +429,7 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
             // (and their LDS reads) interleave instead of waiting out each
             // chain's latency (in-pipeline A/B: +0.7 % bench; fp8 -0.7 %, so one)
             constexpr int NG = (NPX + 31) / 32;
-            constexpr int UG = (std::is_same<T, bf16>::value || SPLIT) ? 2 : 1;
+            constexpr int UG = std::is_same<T, bf16>::value ? 2 : 1;
             for (int g0 = wave1; g0 < ((DIAG & 64) ? 0 : NG); g0 += 4 * UG) {
                 bf16x8 xh[UG], xl[UG];
                 int pix[UG];
@@ -514,24 +455,13 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
                 for (int u = 0; u < UG; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xh[u], cb, 0, 0, 0);
 #pragma unroll
                 for (int u = 0; u < UG; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xl[u], d[u], 0, 0, 0);
-                if constexpr (SPLIT) {
-#pragma unroll
-                    for (int u = 0; u < UG; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wal, xh[u], d[u], 0, 0, 0);
-                }
 #pragma unroll
                 for (int u = 0; u < UG; ++u) {
                     if ((g0 + 4 * u) * 32 + l32 < NPX) {
                         LT* dst = patch + pix[u] * CSTR + 4 * kg;
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
-                            if constexpr (SPLIT) {
-                                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                                bf16x4 h, l;
-#pragma unroll
-                                for (int e = 0; e < 4; ++e) { const float s_ = fmaxf(d[u][4 * q + e], d[u][4 * q + e] * ae); h[e] = bf_hi(s_); l[e] = bf_lo(s_); }
-                                *reinterpret_cast<bf16x4*>(dst + 8 * q) = h;
-                                *reinterpret_cast<bf16x4*>(dst + CIN + 8 * q) = l;
-                            } else if constexpr (F8) {
+                            if constexpr (F8) {
                                 float o[4];
 #pragma unroll
                                 for (int e = 0; e < 4; ++e) o[e] = fmaxf(d[u][4 * q + e], d[u][4 * q + e] * ae);
@@ -649,8 +579,7 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
     // chunk q+1's fragments are in flight.  Across a tap boundary only the A
     // fragments (from the static patch) can run ahead; the next slice's B
     // fragments follow the barrier that publishes it.
-    using FT = typename std::conditional<SPLIT, FragSplit<CIN>, Frag<LT>>::type;
-    FT fa[MF], fb[NF], na[MF], nb[NF];
+    Frag<LT> fa[MF], fb[NF], na[MF], nb[NF];
 #define AA_LOAD_A(dst, tap, cc_)                                                             \
     if (!(DIAG & 128) || (tap) == 0)                                                         \
     {                                                                                        \
@@ -1327,11 +1256,12 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         // the 1x1 head [cout_pad][C_in]
         const bool bf = (precision == AA_PREC_BF16) && s.kind != ST_SMALL;
         const bool f8 = (precision == AA_PREC_FP8) && s.kind != ST_SMALL;
-        // split-bf16: MFMA stages hold [hi C][lo C] bf16 rows; the head stays f32
+        // split-bf16: conv_x3 steps of hi/lo bf16 rows (packed below from the
+        // compact f32 [tap][cout_pad][C_in] image); the head stays f32
         const bool sp = (precision == AA_PREC_BF16X3) && s.kind == ST_MFMA;
         const int wes = (bf || sp) ? 2 : f8 ? 1 : 4;
         const int cstr = s.kind == ST_MFMA ? (bf ? conv_cstr<bf16>(s.cin) : f8 ? conv_cstr<fp8>(s.cin)
-                                              : sp ? conv_cstr<bf16x3>(s.cin) : conv_cstr<float>(s.cin))
+                                              : sp ? s.cin : conv_cstr<float>(s.cin))
                                            : s.cin;
         const int ntap = s.kh * s.kw;
         const size_t slack = s.kind == ST_MFMA ? 1024 / wes : 0;
@@ -1341,10 +1271,6 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                 const double v = kern[(size_t)k * s.cout + o] * scale[o];
                 if (s.kind == ST_SMALL) {
                     wpk[(size_t)o * K + k] = (float)v;
-                } else if (sp) {  // hi at c, the f32 value at cin + c (split below)
-                    const int t = k / s.cin, c = k - t * s.cin;
-                    wpk[((size_t)t * s.cout_pad + o) * cstr + c] = (float)v;
-                    wpk[((size_t)t * s.cout_pad + o) * cstr + s.cin + c] = (float)v;
                 } else {
                     const int t = k / s.cin, c = k - t * s.cin;
                     wpk[((size_t)t * s.cout_pad + o) * cstr + c] = (float)v;
@@ -1353,7 +1279,8 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         // fp8: [bias | per-channel dequantisation scale], both cout_pad long
         std::vector<float> bias(f8 ? 2 * s.cout_pad : s.cout_pad, 0.f);
         for (int o = 0; o < s.cout; ++o) bias[o] = (float)shift[o];
-        const size_t wbytes = wpk.size() * wes;
+        // split-bf16 stores hi + lo: twice the compact image's elements
+        const size_t wbytes = (sp ? 2 * wpk.size() : wpk.size()) * wes;
         hipError_t e = hipMalloc(&s.d_w, wbytes);
         if (e == hipSuccess) {
             if (f8) {
@@ -1382,7 +1309,7 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                 // each [cout_pad][8 units of 8 bf16]: units 0-3 hi = rn_bf16(w) of
                 // channels 32 g + 8 u .. + 7, units 4-7 lo = rn_bf16(w - hi), unit u
                 // of row o stored in slot (u + o) & 7 (aa_conv_x3.h)
-                std::vector<uint16_t> h(wpk.size(), 0);
+                std::vector<uint16_t> h(2 * wpk.size(), 0);
                 const int ng = s.cin / 32;
                 for (int g = 0; g < ng; ++g)
                     for (int t = 0; t < ntap; ++t)
