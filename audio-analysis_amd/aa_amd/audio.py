@@ -1,11 +1,16 @@
 """Recording decode (host side, outside the hot path).
 
 The reference decodes with ffmpeg through audioread + librosa.load(sr=None)
-(src/identify_tracks.py:49-62): samples as float32 in [-1, 1) (int16 / 32768)
-mixed to mono by averaging channels.  This build reads RIFF/WAVE directly
-(PCM 8/16/24/32-bit and IEEE float32/64); other containers need an external
-decoder and are rejected.  Resampling to 48 kHz (librosa soxr_hq in the
-reference) uses a polyphase FIR -- parity unpinned: soxr is not available.
+(src/identify_tracks.py:49-62): ffmpeg converts every source to interleaved
+signed 16-bit (``-f s16le``), librosa's ``buf_to_float`` scales by 1/32768 to
+float32, and channels are averaged to mono.  This build reads RIFF/WAVE
+directly (PCM 8/16/24/32-bit and IEEE float32/64) and applies the same s16
+conversion ffmpeg's libswresample performs (no dither): u8 ``(x - 128) << 8``,
+s24/s32 ``>> 16`` of the 32-bit value (truncation), float ``clip(lrint(x *
+32768))`` -- so non-16-bit files give the reference's samples, not more
+precise ones.  Other containers need an external decoder and are rejected.
+Resampling to 48 kHz (librosa soxr_hq in the reference) uses a polyphase FIR
+-- parity unpinned: soxr is not available.
 """
 from __future__ import annotations
 
@@ -34,24 +39,26 @@ def decode(path):
     if fmt is None or payload is None:
         raise ValueError(f"{path}: missing fmt/data chunk")
     tag, channels, sr, _, _, bits = fmt
-    if tag == 1:  # PCM
+    if tag == 1:  # PCM -> ffmpeg's s16
         if bits == 8:
-            x = (np.frombuffer(payload, np.uint8).astype(np.float32) - 128.0) / 128.0
+            q = (np.frombuffer(payload, np.uint8).astype(np.int32) - 128) << 8
         elif bits == 16:
-            x = np.frombuffer(payload[:len(payload) // 2 * 2], "<i2").astype(np.float32) / 32768.0
+            q = np.frombuffer(payload[:len(payload) // 2 * 2], "<i2").astype(np.int32)
         elif bits == 24:
             b = np.frombuffer(payload[:len(payload) // 3 * 3], np.uint8).reshape(-1, 3).astype(np.int32)
             v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
             v = np.where(v >= 1 << 23, v - (1 << 24), v)
-            x = v.astype(np.float32) / float(1 << 23)
+            q = v >> 8  # s24 -> s32 (<< 8) -> s16 (>> 16)
         elif bits == 32:
-            x = np.frombuffer(payload[:len(payload) // 4 * 4], "<i4").astype(np.float32) / float(1 << 31)
+            q = np.frombuffer(payload[:len(payload) // 4 * 4], "<i4") >> 16
         else:
             raise ValueError(f"{path}: {bits}-bit PCM unsupported")
-    elif tag == 3:  # IEEE float
-        x = np.frombuffer(payload, "<f4" if bits == 32 else "<f8").astype(np.float32)
+    elif tag == 3:  # IEEE float -> av_clip_int16(lrint(x * 32768))
+        f = np.frombuffer(payload[:len(payload) // (bits // 8) * (bits // 8)], "<f4" if bits == 32 else "<f8")
+        q = np.clip(np.rint(f.astype(np.float64) * 32768.0), -32768, 32767)
     else:
         raise ValueError(f"{path}: WAVE format tag {tag} unsupported")
+    x = q.astype(np.float32) / np.float32(32768.0)  # librosa.util.buf_to_float
     if channels > 1:
         x = x[: len(x) // channels * channels].reshape(-1, channels).mean(axis=1, dtype=np.float32)
     return np.ascontiguousarray(x, dtype=np.float32), int(sr)

@@ -24,7 +24,7 @@ import torch
 
 from .frontend import FeSettings, FrontEnd, pack_windows
 from .model import Model, track_mean
-from .windows import schedule
+from .windows import filtered_sources, schedule
 
 
 def fe_settings_from_meta(meta: dict, sr: int) -> FeSettings:
@@ -91,8 +91,9 @@ class Classifier:
                 logging.info("Meaning predictions as have multiple models")
             meta = group[0][1]  # IndexError on an empty group, as the reference
             s = fe_settings_from_meta(meta, sr)
-            if meta.get("filter_freq", False) or meta.get("filter_below", None):
-                raise NotImplementedError("band-pass filtered tracks (filter_freq / filter_below)")
+            if meta.get("use_mfcc", False):
+                # get_spect's MFCC branch (:269-280): librosa.feature.mfcc + tf.image.resize_with_pad
+                raise NotImplementedError("MFCC features (use_mfcc)")
             labels = meta.get("labels")
             ebird_ids = meta.get("ebird_ids")
             model_name = meta.get("name", False)
@@ -102,12 +103,18 @@ class Classifier:
             if model_name == "embeddings":
                 raise NotImplementedError("tensorflow_hub embedding models need a network fetch")
             if views is None:
-                views = schedule(len(frames), sr, tracks, s.segment_length, meta.get("segment_stride", 1.5),
-                                 s.fmin, s.fmax, meta.get("pad_short_tracks", False))
+                views, spans = schedule(len(frames), sr, tracks, s.segment_length, meta.get("segment_stride", 1.5),
+                                        s.fmin, s.fmax, meta.get("pad_short_tracks", False), return_spans=True)
+                # band-pass filtered tracks (:152-162): their windows read a
+                # filtered copy appended after the recording's samples
+                extra, views = filtered_sources(frames, sr, tracks, views, spans, meta.get("filter_freq", False),
+                                                meta.get("filter_below", None), len(frames))
+                if len(extra):
+                    pcm = torch.cat([pcm, torch.from_numpy(extra).to(dev)])
                 flat = [v for tv in views for v in tv]
                 fe = self.frontend(s)
                 if flat:
-                    rows = torch.from_numpy(pack_windows(flat, len(frames), win_len=s.win_len)).to(dev)
+                    rows = torch.from_numpy(pack_windows(flat, int(pcm.numel()), win_len=s.win_len)).to(dev)
                     status = torch.empty(len(flat), dtype=torch.int32, device=dev)
                     logmel = fe.run(pcm, rows, status=status)
                     if int(status.max().item()) != 0:

@@ -13,8 +13,10 @@ __global__ __launch_bounds__(256) void span_nonzero(const float* __restrict__ pc
                                                     int* __restrict__ flags) {
     const long long b = spans[2 * blockIdx.x], e = spans[2 * blockIdx.x + 1];
     int any = 0;
-    // 16-byte body with scalar head/tail
-    long long a4 = (b + 3) & ~3LL, e4 = e & ~3LL;
+    // 16-byte body with scalar head/tail; the body starts at the first
+    // 16-B-aligned ADDRESS (pcm may be an unaligned view)
+    const long long mis = (long long)((reinterpret_cast<uintptr_t>(pcm) >> 2) & 3);  // pcm's float offset mod 4
+    long long a4 = ((b + mis + 3) & ~3LL) - mis, e4 = ((e + mis) & ~3LL) - mis;
     if (a4 > e4) a4 = e4 = e;
     for (long long i = b + threadIdx.x; i < a4; i += 256) any |= pcm[i] != 0.f;
     const float4* q = reinterpret_cast<const float4*>(pcm + a4);

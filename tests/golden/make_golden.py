@@ -29,6 +29,12 @@ Outputs (all small, committed):
                          the ebird codes the build's label sets use (data)
 * tracks.json            get_tracks_from_signals (:795-842) on seeded random
                          signal sets (the track builder of analyse_tracks=False)
+* filtered.json          load_samples (:65-199) with filter_freqs / filter_below
+                         (:152-162, butter_bandpass_filter :1053-1056, scipy),
+                         normalize=False, on a seeded int16-quantised noise clip:
+                         per window its length, sum, sum of squares and the
+                         samples at 16 fixed positions (the windows themselves
+                         are 144,000 samples each)
 """
 from __future__ import annotations
 
@@ -298,6 +304,49 @@ def gen_tracks():
         json.dump(cases, f, indent=1)
 
 
+FILTER_POS = [0, 1, 2, 3, 100, 1000, 5000, 20000, 47999, 48000, 72000, 100000, 120000, 143997, 143998, 143999]
+
+
+def filter_clip(n, seed=11):
+    rng = np.random.default_rng(seed)
+    return (np.round(rng.standard_normal(n) * 0.1 * 32768) / 32768).astype(np.float32)
+
+
+def gen_filtered():
+    import identify_tracks as it
+    captured = []
+    it.get_spect = lambda data, *a, **k: captured.append(np.array(data)) or np.zeros(1)
+    sr = 48000
+    frames = filter_clip(20 * sr)
+    cases = [
+        # (tracks (start, end, fmin, fmax), filter_freqs, filter_below, pad_short, seed)
+        ([(0.5, 7.2, 500, 4000), (9.0, 10.0, 0, 3000), (12.0, 19.0, 1500, 9000)], True, None, False, 0),
+        ([(0.5, 7.2, 500, 4000), (9.0, 10.0, 0, 3000), (12.0, 19.0, 1500, 9000)], False, 5000, False, 1),
+        ([(1.0, 2.0, 800, 2500), (3.0, 8.5, 100, 12000)], True, None, True, 2),
+    ]
+    out = []
+    for tracks, ff, fb, pad_short, seed in cases:
+        np.random.seed(seed)
+        captured.clear()
+        res = it.load_samples(frames, sr, [it.Signal(*t) for t in tracks], 3, 1.5, 640, normalize=False,
+                              pad_short_tracks=pad_short, fmin=50, fmax=11000, filter_freqs=ff, filter_below=fb)
+        per_track, k = [], 0
+        for tr in res:
+            wins = []
+            for _ in tr:
+                d = np.asarray(captured[k], dtype=np.float64)
+                k += 1
+                wins.append({"n": int(len(d)), "sum": float(d.sum()), "sumsq": float((d * d).sum()),
+                             "at": [float(d[i]) for i in FILTER_POS]})
+            per_track.append(wins)
+        out.append({"sr": sr, "clip_seconds": 20, "clip_seed": 11, "tracks": tracks, "filter_freqs": ff,
+                    "filter_below": fb, "pad_short_tracks": pad_short, "seed": seed, "segment_length": 3,
+                    "segment_stride": 1.5, "fmin": 50, "fmax": 11000, "positions": FILTER_POS,
+                    "windows": per_track})
+    with open(OUT / "filtered.json", "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
     install_shims()
     gen_mel()
@@ -305,6 +354,7 @@ def main():
     gen_windows()
     gen_postproc()
     gen_tracks()
+    gen_filtered()
     print("wrote", sorted(p.name for p in OUT.glob("*.npz")) + sorted(p.name for p in OUT.glob("*.json")))
 
 
