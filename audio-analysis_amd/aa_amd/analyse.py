@@ -310,15 +310,21 @@ def main(argv=None):
     if args.meta_to_stdout:
         print(json.dumps(summary, sort_keys=True, indent=4))
     else:
-        meta_path = Path(args.file).with_suffix(".txt")
-        logging.info("Writing metadata to %s", meta_path)
-        metadata = {}
-        if meta_path.exists():
-            with meta_path.open("r") as f:
-                metadata = json.load(f)
-        metadata["analysis_result"] = summary
-        with meta_path.open("w") as f:
-            json.dump(metadata, f, sort_keys=True, indent=4)
+        write_metadata(args.file, summary)
+
+
+def write_metadata(file, summary):
+    """FILE.txt["analysis_result"] = summary, merged into an existing sidecar
+    (src/analyse.py:454-468)."""
+    meta_path = Path(file).with_suffix(".txt")
+    logging.info("Writing metadata to %s", meta_path)
+    metadata = {}
+    if meta_path.exists():
+        with meta_path.open("r") as f:
+            metadata = json.load(f)
+    metadata["analysis_result"] = summary
+    with meta_path.open("w") as f:
+        json.dump(metadata, f, sort_keys=True, indent=4)
 
 
 def cli():

@@ -1,0 +1,145 @@
+"""Corpus runner: many recordings over the GPUs of one node.
+
+The reference analyses one recording per process: an orchestrator runs
+``docker run ... analyse.py FILE`` per file (README.md:28), each writing
+``FILE.txt["analysis_result"]`` (src/analyse.py:434-470).  Here one process
+per GPU (``torchrun`` or ``--gpus N``) takes files ``i % world == rank``
+(shard.shard), runs the same ``examine()`` on each (classify() on its GPU),
+and the per-file result documents -- JSON, variable length -- are all-gathered
+once at the end (RCCL over xGMI with the nccl backend, gloo on CPU), so rank 0
+holds every file's result in file order and writes the reference's sidecars
+(or one JSON list on stdout).  Results do not depend on the world size: each
+file is classified by exactly the code a single process would run.
+
+    python -m aa_amd.corpus FILE... [--bird-model PATH]* [--analyse-tracks B] [-o] [--gpus N]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+from . import shard
+
+
+def gather_documents(local: dict, device=None, group=None) -> dict:
+    """All-gather {file_idx: JSON-serialisable document} across ranks as
+    UTF-8 bytes (padded to the longest rank; one collective for the sizes, one
+    for the payload).  Without an initialised process group, returns ``local``."""
+    if not dist.is_initialized():
+        return dict(sorted(local.items()))
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    payload = json.dumps(sorted(local.items()), sort_keys=True).encode()
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    world = dist.get_world_size(group)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    m = max(int(s.item()) for s in sizes)
+    buf = torch.zeros(m, dtype=torch.uint8, device=dev)
+    if payload:
+        buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    out = {}
+    for p, s in zip(parts, sizes):
+        for k, v in json.loads(bytes(p[:int(s.item())].cpu().numpy()).decode()):
+            out[int(k)] = v
+    return dict(sorted(out.items()))
+
+
+def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world=1, device=None):
+    """Classify this rank's share of ``files``; returns {file_idx: summary}
+    of ALL files on every rank (after the gather).  ``summary`` is what
+    analyse.examine returns plus ``processing_time_seconds`` (src/analyse.py:451-453)."""
+    if examine_fn is None:
+        from .analyse import examine as examine_fn
+    local = {}
+    for i, f in shard.shard(list(files), rank, world):
+        t0 = time.time()
+        summary = examine_fn(str(f), bird_models, analyse_tracks=analyse_tracks)
+        summary["processing_time_seconds"] = round(time.time() - t0, 1)
+        local[i] = summary
+    return gather_documents(local, device=device)
+
+
+def write_results(files, results, to_stdout=False):
+    """Rank 0: the reference's outputs per file -- FILE.txt["analysis_result"]
+    merged into an existing sidecar (src/analyse.py:454-468) -- or, with -o,
+    one JSON list of {"file", "analysis_result"} on stdout."""
+    if to_stdout:
+        print(json.dumps([{"file": str(files[i]), "analysis_result": r} for i, r in results.items()],
+                         sort_keys=True, indent=4))
+        return
+    from .analyse import write_metadata
+    for i, r in results.items():
+        write_metadata(files[i], r)
+
+
+def _worker(local_rank, world, args, port):
+    if port is not None:
+        os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                          MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    rank = int(os.environ.get("RANK", "0"))
+    dev = None
+    if torch.cuda.is_available():
+        # one GPU per rank; more ranks than GPUs share them round-robin
+        dev = torch.device("cuda", local_rank % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+    if world > 1:
+        backend = args.backend or ("nccl" if dev is not None else "gloo")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+    try:
+        gdev = dev if (world > 1 and dist.get_backend() == "nccl") else None
+        res = run(args.files, args.bird_model, args.analyse_tracks, rank=rank, world=world, device=gdev)
+        if rank == 0:
+            write_results(args.files, res, to_stdout=bool(args.meta_to_stdout))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def parse_args(argv=None):
+    from .analyse import none_or_str, str2bool
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("files", nargs="+", help="audio files")
+    ap.add_argument("--bird-model", type=none_or_str, action="append", help="Path to bird model")
+    ap.add_argument("--analyse-tracks", type=str2bool, default=False)
+    ap.add_argument("-o", "--meta-to-stdout", action="count")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks to spawn when not under torchrun")
+    ap.add_argument("--backend", default=None, help="process-group backend (default nccl on GPU)")
+    args = ap.parse_args(argv)
+    if not args.bird_model:
+        args.bird_model = ["/models/pre-model/audioModel.keras", "/models/bird-model-v2m/audioModel.keras"]
+    return args
+
+
+def main(argv=None):
+    from .analyse import init_logging
+    args = parse_args(argv)
+    init_logging()
+    if "WORLD_SIZE" in os.environ:
+        _worker(int(os.environ.get("LOCAL_RANK", "0")), int(os.environ["WORLD_SIZE"]), args, None)
+    elif args.gpus > 1:
+        import socket
+        import torch.multiprocessing as mp
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        mp.spawn(_worker, args=(args.gpus, args, port), nprocs=args.gpus, join=True)
+    else:
+        _worker(0, 1, args, None)
+
+
+if __name__ == "__main__":
+    try:
+        main()
+    except Exception:
+        logging.error("Terminated with error", exc_info=True)
+        sys.exit(1)

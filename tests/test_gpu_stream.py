@@ -55,3 +55,33 @@ def test_stream_matches_per_recording(gpu, model_root):
             assert np.array_equal(got[(r.key, ti)], means[row]), (r.key, ti)
             n_tracks += 1
     assert n_tracks == len(got) and n_tracks >= 14
+
+
+def test_stream_matches_oracle(gpu, model_root):
+    """BASELINE configs[2] against the CPU oracle: 8 full 60 s clips (39
+    windows each) through StreamRunner with the model1+2+3 ensemble in the
+    default (gated) split-bf16 precision; per-track means over models and
+    windows within 1e-3 of oracle.fe_oracle + oracle.cnn_oracle (fp32)."""
+    from oracle import cnn_oracle, fe_oracle
+    from aa_amd.frontend import FeSettings
+    from aa_amd.stream import Recording, StreamRunner
+    from aa_amd.windows import schedule
+    from tools import synth
+    import bench
+    s = FeSettings(htk=True, hop_length=640, n_fft=4096, n_mels=160, break_freq=1750)
+    paths = [model_root / m / "audioModel.safetensors" for m in ("model1", "model2", "model3")]
+    recs = [Recording(key=i, pcm=synth.clip(500 + i), tracks=[T(0, 60.0)]) for i in range(8)]
+    runner = StreamRunner(paths, s, device=gpu, max_windows=4 * 39, max_samples=4 * 2_880_000)
+    assert all(m.precision == "bf16x3" for m in runner.models)
+    got = {k: v for k, _, v in runner.run(recs)}
+    cfg = bench.fe_config(s)
+    worst = 0.0
+    for r in recs:
+        (views,) = schedule(len(r.pcm), 48000, r.tracks, 3, 1.5, s.fmin, s.fmax, False)
+        assert len(views) == 39
+        mel = np.stack([fe_oracle.window_logmel(bench.window_samples(r.pcm, v, s.win_len), cfg) for v in views])
+        probs = np.stack([cnn_oracle.forward(p, mel)[1] for p in paths])
+        ref = np.mean(np.mean(probs, axis=0), axis=0)
+        worst = max(worst, float(np.abs(got[r.key] - ref).max()))
+    print(f"configs[2] 8 x 60 s, 3-model ensemble: max|d track mean| = {worst:.3e}")
+    assert worst <= 1e-3
