@@ -60,8 +60,14 @@ def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world
     analyse.examine returns plus ``processing_time_seconds`` (src/analyse.py:451-453)."""
     if examine_fn is None:
         from .analyse import examine as examine_fn
+    import numpy as np
     local = {}
     for i, f in shard.shard(list(files), rank, world):
+        # short tracks draw random window offsets from the global RandomState
+        # (src/identify_tracks.py:132, :167; the reference leaves it unseeded,
+        # one process per file): seeding it per file makes every file's result
+        # independent of which rank ran it and what ran before
+        np.random.seed(i)
         t0 = time.time()
         summary = examine_fn(str(f), bird_models, analyse_tracks=analyse_tracks)
         summary["processing_time_seconds"] = round(time.time() - t0, 1)
