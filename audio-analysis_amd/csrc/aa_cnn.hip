@@ -963,14 +963,15 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
 
 // conv_x3 (split-bf16) instantiations: (kernel, C_in, pool) -> waves (WM x
 // WN), fragments per wave (MF x NF), output tile TH x TW, weight ring in LDS
-// (1) or per-wave B fragments from global (0); picked by
+// (1) or per-wave B fragments from global (0), A fragments just in time (1)
+// or a whole step ahead (0), pinned waves per SIMD (0: free); picked by
 // tools/conv_bench_x3.hip sweeps
-#define AA_X3_CFGS(X)                           \
-    X(3, 3, 32, 3, 4, 1, 3, 2, 9, 21, 0)        \
-    X(3, 3, 32, 1, 4, 2, 3, 2, 10, 18, 1)       \
-    X(3, 3, 64, 1, 4, 2, 3, 2, 12, 14, 1)       \
-    X(9, 3, 64, 3, 4, 2, 4, 2, 39, 6, 0)        \
-    X(1, 3, 128, 1, 4, 2, 3, 2, 7, 20, 1)
+#define AA_X3_CFGS(X)                                 \
+    X(3, 3, 32, 3, 4, 1, 3, 2, 9, 21, 0, 1, 4)        \
+    X(3, 3, 32, 1, 4, 2, 3, 2, 10, 18, 1, 0, 0)       \
+    X(3, 3, 64, 1, 4, 2, 3, 2, 12, 14, 1, 1, 4)       \
+    X(9, 3, 64, 3, 4, 2, 4, 4, 39, 6, 0, 1, 2)        \
+    X(1, 3, 128, 1, 4, 2, 3, 2, 7, 20, 1, 0, 0)
 
 template <typename T>
 constexpr int prec_of() {
@@ -986,16 +987,17 @@ static int mfma_bn(int prec, int kh, int kw, int cin, int pool) {
         return WN * NF * 16;
     AA_CONV_CFGS(AA_BN)
 #undef AA_BN
-#define AA_BN3(KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, RING)                                               \
+#define AA_BN3(KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, RING, AJIT, OCC)                                               \
     if (prec == AA_PREC_BF16X3 && kh == KH && kw == KW && cin == CIN && pool == POOL) return WN * NF * 16;
     AA_X3_CFGS(AA_BN3)
 #undef AA_BN3
     return 0;
 }
 
-template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool RING, bool FUSED>
+template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool RING, bool AJIT,
+          int OCC, bool FUSED>
 static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream_t st, const Stage* first) {
-    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, RING>;
+    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, RING, AJIT, OCC>;
     constexpr int BN = WN * NF * 16;
     const size_t lds = x3_lds_bytes<KH, KW, CIN, BN, TH, TW, FUSED, RING>();
     FirstConv fc{};
@@ -1058,13 +1060,13 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
                  "no fused first-layer kernel for %s", s.name.c_str());
     }
     if constexpr (is_split<T>()) {
-#define AA_LAUNCH3(KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, RING)                                        \
+#define AA_LAUNCH3(KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, RING, AJIT, OCC)                            \
         if (s.kh == KH && s.kw == KW && s.cin == CIN && s.pool == POOL) {                                  \
             if (s.fused_first) {                                                                           \
                 if constexpr (CIN == 32 && KH == 3 && KW == 3 && WM * WN == 4)                             \
-                    return launch_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, RING, true>(s, in, out, n, st, first); \
+                    return launch_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, RING, AJIT, OCC, true>(s, in, out, n, st, first); \
             } else {                                                                                       \
-                return launch_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, RING, false>(s, in, out, n, st, first); \
+                return launch_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, RING, AJIT, OCC, false>(s, in, out, n, st, first); \
             }                                                                                              \
         }
         AA_X3_CFGS(AA_LAUNCH3)

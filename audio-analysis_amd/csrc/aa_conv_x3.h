@@ -79,10 +79,14 @@ __device__ __forceinline__ int x3_addr(int R, int C, int u, int PW, int TW) {
 // its own B fragments (its NF x 16 output-channel rows of the step) straight
 // from global memory (L2-resident weights) one step ahead, so waves only
 // synchronise at the two barriers around each group's staging.
+// AJIT: A fragments read just in time inside the step (fewer VGPRs) instead
+// of a whole next-step set prefetched; OCC > 0 pins the waves per SIMD the
+// compiler must fit (its VGPR budget), 0 leaves it free up to the LDS limit.
 template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool FUSED = false,
-          int DIAG = 0, bool RING = true>
+          int DIAG = 0, bool RING = true, bool AJIT = false, int OCC = 0>
 __global__ __launch_bounds__(WM * WN * 64)
-__attribute__((amdgpu_waves_per_eu(1, x3_waves_per_simd<KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, RING>())))
+__attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1,
+                                    OCC ? OCC : x3_waves_per_simd<KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, RING>())))
 void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restrict__ wt,
              const float* __restrict__ bias, float* __restrict__ out, int Hout, int Wout, int cout_store,
              int tiles_w, int act, float alpha, FirstConv fc) {
@@ -209,15 +213,39 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             }
         }
         if (s + 1 < NSTEP) read_b(nxt, s + 1);
-        if (t + 1 < NTAP) read_a(nxt, t + 1);
+        if constexpr (!AJIT) {
+            if (t + 1 < NTAP) read_a(nxt, t + 1);
 #pragma unroll
-        for (int i = 0; i < MF; ++i)
+            for (int i = 0; i < MF; ++i)
 #pragma unroll
-            for (int j = 0; j < NF; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bh[j], cur.ah[i], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bl[j], cur.ah[i], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bh[j], cur.al[i], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < NF; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bh[j], cur.ah[i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bl[j], cur.ah[i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bh[j], cur.al[i], acc[i][j], 0, 0, 0);
+                }
+        } else {
+            // A fragments just in time, two in flight: fragment i+1's LDS read
+            // under fragment i's MFMAs (2 x 16 VGPRs instead of 2 x MF x 8)
+            const int kh = t / KW, kw = t - (t / KW) * KW;
+            const int toff = (kh * PW + kw) * 128, tv = kh * TW + kw;
+            bf16x8 h2[2], l2[2];
+            auto rd = [&](int i, int k) {
+                const int a = abase[i] + toff + (((aph[i] + tv) & 7) << 4);
+                h2[k] = *reinterpret_cast<const bf16x8*>(patch + a);
+                l2[k] = *reinterpret_cast<const bf16x8*>(patch + (a ^ 64));
+            };
+            rd(0, 0);
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                if (i + 1 < MF) rd(i + 1, (i + 1) & 1);
+#pragma unroll
+                for (int j = 0; j < NF; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bh[j], h2[i & 1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bl[j], h2[i & 1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bh[j], l2[i & 1], acc[i][j], 0, 0, 0);
+                }
             }
+        }
     };
 
     if constexpr (!RING) read_b(F0, 0);  // its latency hides behind the first staging
@@ -372,7 +400,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 F0.bl[j] = F1.bl[j];
             }
         }
-        if (!(DIAG & 2)) read_a(F0, 0);
+        if (!(DIAG & 2) && !AJIT) read_a(F0, 0);
         for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); t += 2) {
             step(F0, F1, g, t);
             if (t + 1 < NTAP) step(F1, F0, g, t + 1);

@@ -11,10 +11,10 @@
 using namespace aa;
 
 template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool FUSED,
-          int DIAG = 0, bool RING = true>
+          int DIAG = 0, bool RING = true, bool AJIT = false, int OCC = 0>
 static void time_one(const char* tag, int n, int Hin, int Win, int cout, const void* in, const void* w,
                      const float* b, void* out, FirstConv fc, int iters) {
-    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, DIAG, RING>;
+    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, DIAG, RING, AJIT, OCC>;
     constexpr int BN = WN * NF * 16;
     const size_t lds = x3_lds_bytes<KH, KW, CIN, BN, TH, TW, FUSED, RING>();
     if (lds > 160 * 1024) {
@@ -44,8 +44,8 @@ static void time_one(const char* tag, int n, int Hin, int Win, int cout, const v
     const float us = 1e3f * ms / iters;
     double fl = 2.0 * n * Hc * Wc * KH * KW * CIN * cout;
     if (FUSED) fl += 2.0 * n * (Hin) * (Win) * 9 * 32;
-    printf("%-8s%s %dx%d cin %3d WM%d WN%d MF%2d NF%d %2dx%2d  LDS %6zu  grid %6d  %7.1f us  %6.1f TF (%.3f of 833)\n",
-           tag, RING ? "" : "G", KH, KW, CIN, WM, WN, MF, NF, TH, TW, lds, grid.x * grid.y * grid.z, us, fl / us * 1e-6,
+    printf("%-8s%s%s%d %dx%d cin %3d WM%d WN%d MF%2d NF%d %2dx%2d  LDS %6zu  grid %6d  %7.1f us  %6.1f TF (%.3f of 833)\n",
+           tag, RING ? "" : "G", AJIT ? "J" : "", OCC, KH, KW, CIN, WM, WN, MF, NF, TH, TW, lds, grid.x * grid.y * grid.z, us, fl / us * 1e-6,
            fl / us * 1e-6 / 833.3);
 }
 
@@ -94,38 +94,43 @@ int main(int argc, char** argv) {
 #define G4(WM, WN, MF, NF, TH, TW) time_one<3, 3, 64, WM, WN, MF, NF, 1, TH, TW, false, 0, false>("c4", n, 50, 72, 64, in, w, b, out, fc, it);
 #define G5(WM, WN, MF, NF, TH, TW) time_one<9, 3, 64, WM, WN, MF, NF, 3, TH, TW, false, 0, false>("c5", n, 48, 70, 128, in, w, b, out, fc, it);
 #define G6(WM, WN, MF, NF, TH, TW) time_one<1, 3, 128, WM, WN, MF, NF, 1, TH, TW, false, 0, false>("c6", n, 13, 22, 256, in, w, b, out, fc, it);
+#define J2(WM, WN, MF, NF, TH, TW, R, O) time_one<3, 3, 32, WM, WN, MF, NF, 3, TH, TW, true, 0, R, true, O>("c1+c2", n, 158, 224, 32, in, w, b, out, f1, it);
+#define J3(WM, WN, MF, NF, TH, TW, R, O) time_one<3, 3, 32, WM, WN, MF, NF, 1, TH, TW, false, 0, R, true, O>("c3", n, 52, 74, 64, in, w, b, out, fc, it);
+#define J4(WM, WN, MF, NF, TH, TW, R, O) time_one<3, 3, 64, WM, WN, MF, NF, 1, TH, TW, false, 0, R, true, O>("c4", n, 50, 72, 64, in, w, b, out, fc, it);
+#define J5(WM, WN, MF, NF, TH, TW, R, O) time_one<9, 3, 64, WM, WN, MF, NF, 3, TH, TW, false, 0, R, true, O>("c5", n, 48, 70, 128, in, w, b, out, fc, it);
+#define J6(WM, WN, MF, NF, TH, TW, R, O) time_one<1, 3, 128, WM, WN, MF, NF, 1, TH, TW, false, 0, R, true, O>("c6", n, 13, 22, 256, in, w, b, out, fc, it);
 #define C6(WM, WN, MF, NF, TH, TW) time_one<1, 3, 128, WM, WN, MF, NF, 1, TH, TW, false>("c6", n, 13, 22, 256, in, w, b, out, fc, it);
     if (which == 10) {  // the shipped c5 / c2 tiles alone (PMC passes)
         C5(3, 2, 5, 2, 39, 6) C2(4, 1, 3, 2, 6, 30)
         return 0;
     }
     if (!which || which == 2) {
-        C2(4, 1, 3, 2, 6, 30) C2(4, 1, 4, 2, 12, 21) C2(4, 1, 6, 2, 12, 30) C2(4, 1, 6, 2, 6, 60)
-        C2(4, 1, 3, 2, 9, 21) C2(4, 1, 5, 2, 6, 48)
-        G2(4, 1, 3, 2, 6, 30) G2(4, 1, 4, 2, 12, 21) G2(4, 1, 6, 2, 12, 30) G2(4, 1, 6, 2, 6, 60)
-        G2(4, 1, 3, 2, 9, 21) G2(4, 1, 5, 2, 6, 48) G2(4, 1, 7, 2, 12, 36) G2(4, 1, 8, 2, 12, 42)
-        G2(4, 1, 4, 2, 6, 42) G2(4, 1, 6, 2, 18, 21)
+        G2(4, 1, 3, 2, 9, 21) G2(4, 1, 4, 2, 12, 21) G2(4, 1, 5, 2, 6, 48)
+        J2(4, 1, 3, 2, 9, 21, false, 0) J2(4, 1, 4, 2, 12, 21, false, 0) J2(4, 1, 5, 2, 6, 48, false, 0)
+        J2(4, 1, 6, 2, 12, 30, false, 0) J2(4, 1, 8, 2, 12, 42, false, 0) J2(4, 1, 6, 2, 18, 21, false, 0)
+        J2(4, 1, 3, 2, 9, 21, false, 4) J2(4, 1, 4, 2, 12, 21, false, 4) J2(4, 1, 6, 2, 12, 30, false, 3)
+        J2(4, 1, 4, 2, 12, 21, true, 0) J2(4, 1, 6, 2, 12, 30, true, 0)
     }
     if (!which || which == 3) {
-        C3(4, 2, 3, 2, 10, 18) C3(4, 2, 2, 2, 5, 24) C3(4, 2, 4, 2, 16, 16)
-        G3(4, 2, 3, 2, 10, 18) G3(4, 2, 2, 2, 5, 24) G3(4, 2, 4, 2, 16, 16) G3(4, 1, 4, 4, 10, 24)
-        G3(4, 2, 4, 2, 10, 24) G3(2, 2, 8, 2, 10, 24) G3(4, 1, 2, 4, 5, 24)
+        C3(4, 2, 3, 2, 10, 18) J3(4, 2, 3, 2, 10, 18, true, 0) J3(4, 2, 3, 2, 10, 18, true, 4)
+        J3(4, 2, 4, 2, 10, 24, true, 0) J3(4, 2, 4, 2, 10, 24, true, 4) J3(4, 2, 3, 2, 10, 18, false, 4)
+        J3(4, 2, 6, 2, 25, 12, true, 0) J3(4, 2, 5, 2, 25, 12, true, 0)
     }
     if (!which || which == 4) {
-        C4(4, 2, 3, 2, 12, 14) C4(4, 2, 4, 2, 16, 14) C4(2, 2, 7, 2, 16, 14)
-        G4(4, 2, 3, 2, 12, 14) G4(4, 2, 4, 2, 16, 14) G4(2, 2, 7, 2, 16, 14) G4(4, 1, 4, 4, 16, 14)
-        G4(4, 2, 6, 2, 24, 14) G4(4, 1, 3, 4, 12, 14) G4(4, 2, 7, 2, 16, 28)
+        C4(4, 2, 3, 2, 12, 14) J4(4, 2, 3, 2, 12, 14, true, 0) J4(4, 2, 3, 2, 12, 14, true, 4)
+        J4(4, 2, 4, 2, 16, 14, true, 0) J4(4, 2, 4, 2, 16, 14, true, 4) J4(4, 2, 4, 2, 16, 14, false, 4)
+        J4(4, 2, 6, 2, 24, 14, true, 0) J4(4, 2, 7, 2, 16, 28, true, 0) J4(2, 2, 7, 2, 16, 14, true, 0)
     }
     if (!which || which == 5) {
-        C5(5, 2, 3, 2, 39, 6) C5(2, 2, 4, 2, 3, 33) C5(4, 2, 2, 2, 3, 33)
-        G5(5, 2, 3, 2, 39, 6) G5(2, 2, 4, 2, 3, 33) G5(4, 2, 2, 2, 3, 33) G5(4, 1, 4, 4, 39, 6)
-        G5(4, 2, 4, 2, 39, 6) G5(4, 2, 4, 2, 6, 33) G5(2, 4, 8, 1, 39, 6) G5(4, 4, 4, 1, 39, 6)
-        G5(8, 2, 4, 2, 39, 12) G5(4, 2, 4, 2, 3, 66) G5(8, 2, 2, 2, 39, 6) G5(4, 1, 2, 4, 3, 33)
+        G5(4, 2, 4, 2, 39, 6) J5(4, 2, 4, 2, 39, 6, false, 0) J5(4, 2, 4, 2, 39, 6, false, 4)
+        J5(4, 2, 4, 2, 39, 6, true, 0) J5(4, 2, 4, 2, 39, 6, true, 4) J5(4, 1, 4, 4, 39, 6, false, 0)
+        J5(4, 1, 4, 4, 39, 6, false, 4) J5(8, 2, 4, 2, 39, 12, false, 0) J5(8, 2, 4, 2, 39, 12, false, 4)
+        J5(4, 2, 2, 2, 3, 33, false, 4) J5(2, 2, 4, 2, 3, 33, false, 4) J5(4, 2, 4, 2, 6, 33, false, 4)
+        J5(4, 2, 4, 4, 39, 6, false, 0) J5(4, 2, 4, 4, 39, 6, false, 2)
     }
     if (!which || which == 6) {
-        C6(4, 2, 3, 2, 7, 20) C6(4, 1, 3, 4, 7, 20)
-        G6(4, 2, 3, 2, 7, 20) G6(4, 1, 3, 4, 7, 20) G6(4, 2, 5, 2, 13, 20) G6(4, 4, 3, 1, 7, 20)
-        G6(2, 2, 5, 2, 13, 12)
+        C6(4, 2, 3, 2, 7, 20) J6(4, 2, 3, 2, 7, 20, true, 0) J6(4, 2, 3, 2, 7, 20, true, 4)
+        J6(4, 2, 5, 2, 13, 20, true, 0) J6(4, 1, 3, 4, 7, 20, true, 0)
     }
     hipError_t e = hipGetLastError();
     printf("last error: %s\n", hipGetErrorString(e));
