@@ -30,6 +30,7 @@ AA_OP = {
     "sigmoid": 6,
     "magtransform": 7,
     "relu": 8,
+    "dense": 9,
 }
 
 AA_WIN_OK = 0

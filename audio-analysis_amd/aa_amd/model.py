@@ -4,9 +4,9 @@ Model contract (reference src/identify_tracks.py:291-327, src/analyse.py:414-418
 ``--bird-model`` names ``<dir>/audioModel.keras`` (or the directory); the
 JSON ``<dir>/metadata.txt`` beside it holds labels and front-end settings.
 This build stores the network as ``<dir>/audioModel.safetensors`` (weights plus
-``__metadata__["arch"]``, a Keras-style layer list), since TF/h5py are not part
-of the MI355X stack; a ``.keras`` path resolves to the safetensors file next to
-it.  ``Model.predict`` replaces ``model.predict(np.array(d))`` (:544).
+``__metadata__["arch"]``, a Keras-style layer list); without one, the
+reference's ``audioModel.keras`` itself is read (keras_import: zip + HDF5
+through h5lite, no TF/h5py).  ``Model.predict`` replaces ``model.predict(np.array(d))`` (:544).
 """
 from __future__ import annotations
 
@@ -38,6 +38,21 @@ def weights_path(model_path) -> Path:
     if p.is_dir():
         return p / WEIGHTS_NAME
     return p.parent / WEIGHTS_NAME
+
+
+def load_network(model_path):
+    """(arch, tensors) of a model: this build's ``audioModel.safetensors`` when
+    present, else the reference's ``audioModel.keras`` (keras_import)."""
+    p = Path(model_path)
+    wp = weights_path(p)
+    if wp.exists():
+        return read_arch(wp)
+    kp = p if p.suffix == ".keras" else (p / "audioModel.keras" if p.is_dir() else p.with_name("audioModel.keras"))
+    if kp.exists():
+        from .keras_import import read_keras
+        arch, tensors, _ = read_keras(kp)
+        return arch, tensors
+    raise FileNotFoundError(f"{model_path}: neither {wp.name} nor {kp.name}")
 
 
 def read_arch(path):
@@ -98,6 +113,12 @@ def layer_table(arch, tensors):
         elif kind == "magtransform":
             off[0] = put(ly["name"] + ".a")
             op = "magtransform"
+        elif kind == "dense":
+            filters = ly["units"]
+            off[0] = put(ly["name"] + ".kernel")
+            if ly.get("use_bias", True):
+                off[1] = put(ly["name"] + ".bias")
+            op = "dense"
         else:
             raise ValueError(f"unsupported layer type {kind}")
         L = _lib.Layer(op=_lib.AA_OP[op], kh=kh, kw=kw, filters=filters, alpha=alpha, eps=eps)
@@ -120,9 +141,8 @@ class Model(_lib.StageTiming):
         self.meta = meta if meta is not None else load_model_meta(model_path)
         self.device = torch.device(device or "cuda")
         self.precision = precision
-        wp = weights_path(model_path)
         try:
-            arch, tensors = read_arch(wp)
+            arch, tensors = load_network(model_path)
         except Exception:
             logging.info("Could not load model", exc_info=True)  # :324-326
             raise

@@ -744,11 +744,12 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
 }
 
 // ---------------------------------------------------------------------------
-// conv_head: 1x1 conv (C_in % 32 == 0, C_out <= 16*NF) + global max + sigmoid.
-// One block per window; 4 waves along pixels, MF tiles each per chunk.
+// conv_head: 1x1 conv (C_in % 32 == 0) + global max + sigmoid.  Pixel ranges
+// of 64 per block (blockIdx.y), 32 labels per block (blockIdx.z: label group);
+// 4 waves along pixels, MF tiles each per chunk, NF = 2 label tiles.
 // ---------------------------------------------------------------------------
-template <typename T, int CIN, int MF, int NF>
-__global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int HW,
+template <typename T, int MF, int NF>
+__global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int HW, int cin,
                                                  const T* __restrict__ wt, const float* __restrict__ bias,
                                                  int L, int act, float alpha, int sigmoid,
                                                  float* __restrict__ logits, float* __restrict__ probs,
@@ -756,10 +757,11 @@ __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int H
     const int n = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q8 = 8 * (lane >> 4);
-    const T* src = in + (size_t)n * HW * CIN;
+    const int lg = blockIdx.z * 16 * NF;  // first label of this block's group
+    const T* src = in + (size_t)n * HW * cin;
     const T* bptr[NF];
 #pragma unroll
-    for (int j = 0; j < NF; ++j) bptr[j] = wt + (size_t)(j * 16 + (lane & 15)) * CIN + q8;
+    for (int j = 0; j < NF; ++j) bptr[j] = wt + (size_t)(lg + j * 16 + (lane & 15)) * cin + q8;
     float rmax[NF];
 #pragma unroll
     for (int j = 0; j < NF; ++j) rmax[j] = -INFINITY;
@@ -774,10 +776,10 @@ __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int H
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             const int p = p0 + (wave * MF + i) * 16 + (lane & 15);
-            arow[i] = (p < HW ? p : 0) * CIN + q8;
+            arow[i] = (p < HW ? p : 0) * cin + q8;
         }
 #pragma unroll 2
-        for (int k0 = 0; k0 < CIN; k0 += 32) {
+        for (int k0 = 0; k0 < cin; k0 += 32) {
             Frag<T> b[NF];
 #pragma unroll
             for (int j = 0; j < NF; ++j) b[j].load(bptr[j] + k0);
@@ -808,34 +810,115 @@ __global__ __launch_bounds__(256) void conv_head(const T* __restrict__ in, int H
         if (lane < 16) red[wave][j * 16 + lane] = v;
     }
     __syncthreads();
-    if (part) {  // one of gridDim.y pixel ranges: its column maxima, finished by head_final
-        if (threadIdx.x < 16 * NF)
-            part[((size_t)n * gridDim.y + blockIdx.y) * 16 * NF + threadIdx.x] =
-                fmaxf(fmaxf(red[0][threadIdx.x], red[1][threadIdx.x]), fmaxf(red[2][threadIdx.x], red[3][threadIdx.x]));
-        return;
+    if (threadIdx.x < 16 * NF) {  // one of gridDim.y pixel ranges: its column maxima, finished by head_final
+        const int lp = gridDim.z * 16 * NF;  // cout_pad
+        part[((size_t)n * gridDim.y + blockIdx.y) * lp + lg + threadIdx.x] =
+            fmaxf(fmaxf(red[0][threadIdx.x], red[1][threadIdx.x]), fmaxf(red[2][threadIdx.x], red[3][threadIdx.x]));
     }
-    if (threadIdx.x < 16 * NF && (int)threadIdx.x < L) {
-        const int c = threadIdx.x;
-        float v = fmaxf(fmaxf(red[0][c], red[1][c]), fmaxf(red[2][c], red[3][c]));
+}
+
+// global max over the head's pixel ranges, bias, activation, sigmoid
+__global__ __launch_bounds__(256) void head_final(const float* __restrict__ part, int nparts, int width,
+                                                  const float* __restrict__ bias, int L, int act, float alpha,
+                                                  int sigmoid, float* __restrict__ logits,
+                                                  float* __restrict__ probs, const float* __restrict__ wscale) {
+    const int n = blockIdx.x;
+    for (int c = threadIdx.x; c < L; c += blockDim.x) {
+        const float* p = part + (size_t)n * nparts * width + c;
+        float v = p[0];
+        for (int k = 1; k < nparts; ++k) v = fmaxf(v, p[(size_t)k * width]);
         v = apply_act(wscale ? fmaf(v, wscale[c], bias[c]) : v + bias[c], act, alpha);
         logits[(size_t)n * L + c] = v;
         if (probs) probs[(size_t)n * L + c] = sigmoid ? 1.f / (1.f + expf(-v)) : v;
     }
 }
 
-// global max over the head's pixel ranges, bias, activation, sigmoid
-__global__ __launch_bounds__(64) void head_final(const float* __restrict__ part, int nparts, int width,
-                                                 const float* __restrict__ bias, int L, int act, float alpha,
-                                                 int sigmoid, float* __restrict__ logits,
-                                                 float* __restrict__ probs, const float* __restrict__ wscale) {
-    const int n = blockIdx.x, c = threadIdx.x;
-    if (c >= L) return;
-    const float* p = part + (size_t)n * nparts * width + c;
-    float v = p[0];
-    for (int k = 1; k < nparts; ++k) v = fmaxf(v, p[(size_t)k * width]);
-    v = apply_act(wscale ? fmaf(v, wscale[c], bias[c]) : v + bias[c], act, alpha);
-    logits[(size_t)n * L + c] = v;
-    if (probs) probs[(size_t)n * L + c] = sigmoid ? 1.f / (1.f + expf(-v)) : v;
+// ---------------------------------------------------------------------------
+// Generic stages for layer shapes no tuned kernel covers (the planner's
+// fallback, exact f32 arithmetic on the VALU): any kernel size, any C_in,
+// any max-pool window, optional MagTransform prologue.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+__device__ __forceinline__ float to_f(fp8 x) {  // OCP e4m3fn
+    const int s = x.v >> 7, e = (x.v >> 3) & 15, m = x.v & 7;
+    float v = e ? ldexpf(1.f + m / 8.f, e - 7) : ldexpf(m / 8.f, -6);
+    if (e == 15 && m == 7) v = NAN;
+    return s ? -v : v;
+}
+
+// one thread = one (pooled) output pixel x 8 output channels; weights
+// [cout][kh][kw][cin] f32 (BN folded), bias f32
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void conv_generic(const TI* __restrict__ in, int Hin, int Win, int cin,
+                                                    const float* __restrict__ w, const float* __restrict__ bias,
+                                                    int kh, int kw, int cout, int ph, int pw, int Hout, int Wout,
+                                                    int act, float alpha, int has_mag, float mag_exp,
+                                                    TO* __restrict__ out) {
+    const int n = blockIdx.z;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c0 = blockIdx.y * 8;
+    if (p >= Hout * Wout) return;
+    const int oh = p / Wout, ow = p - (p / Wout) * Wout;
+    const int K = kh * kw * cin;
+    const int nc = min(8, cout - c0);
+    float best[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) best[o] = -INFINITY;
+    const TI* img = in + (size_t)n * Hin * Win * cin;
+    for (int dy = 0; dy < ph; ++dy)
+        for (int dx = 0; dx < pw; ++dx) {
+            const int h = oh * ph + dy, x = ow * pw + dx;
+            float acc[8];
+#pragma unroll
+            for (int o = 0; o < 8; ++o) acc[o] = 0.f;
+            for (int i = 0; i < kh; ++i)
+                for (int j = 0; j < kw; ++j) {
+                    const TI* src = img + ((size_t)(h + i) * Win + x + j) * cin;
+                    const float* wk = w + (size_t)c0 * K + (i * kw + j) * cin;
+                    for (int c = 0; c < cin; ++c) {
+                        float v = to_f(src[c]);
+                        if (has_mag) v = powf(v, mag_exp);
+#pragma unroll
+                        for (int o = 0; o < 8; ++o)
+                            if (o < nc) acc[o] = fmaf(v, wk[(size_t)o * K + c], acc[o]);
+                    }
+                }
+#pragma unroll
+            for (int o = 0; o < 8; ++o)
+                if (o < nc) best[o] = fmaxf(best[o], apply_act(acc[o] + bias[c0 + o], act, alpha));
+        }
+    TO* dst = out + ((size_t)(n * Hout + oh) * Wout + ow) * cout + c0;
+    for (int o = 0; o < nc; ++o) dst[o] = to_t<TO>(best[o]);
+}
+
+// GlobalMaxPool2D over a stage's output, then an optional Dense layer
+// (weights [C][U] f32, bias [U]) and sigmoid; one block per window
+template <typename TI>
+__global__ __launch_bounds__(256) void pool_dense(const TI* __restrict__ in, int HW, int C,
+                                                  const float* __restrict__ w, const float* __restrict__ b, int U,
+                                                  int sigmoid, float* __restrict__ logits, float* __restrict__ probs) {
+    extern __shared__ float mx[];
+    const int n = blockIdx.x;
+    const TI* src = in + (size_t)n * HW * C;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float m = -INFINITY;
+        for (int p = 0; p < HW; ++p) m = fmaxf(m, to_f(src[(size_t)p * C + c]));
+        mx[c] = m;
+    }
+    __syncthreads();
+    for (int u = threadIdx.x; u < U; u += blockDim.x) {
+        float v;
+        if (w) {
+            v = 0.f;
+            for (int c = 0; c < C; ++c) v = fmaf(mx[c], w[(size_t)c * U + u], v);
+            v += b[u];
+        } else {
+            v = mx[u];
+        }
+        logits[(size_t)n * U + u] = v;
+        if (probs) probs[(size_t)n * U + u] = sigmoid ? 1.f / (1.f + expf(-v)) : v;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -879,12 +962,17 @@ namespace aa {
 // ---------------------------------------------------------------------------
 // host: planner, workspace, forward, timing
 // ---------------------------------------------------------------------------
-enum StageKind { ST_SMALL = 0, ST_MFMA = 1, ST_HEAD = 2 };
+// ST_SMALL: C_in = 1 3x3 -> 32 first conv (VALU, fusable into the next
+// stage); ST_MFMA: tuned matrix-core conv; ST_HEAD: 1x1 conv + global max;
+// ST_GENERIC: any other conv shape / pool window (f32 VALU fallback);
+// ST_POOLDENSE: GlobalMaxPool2D [+ Dense] [+ sigmoid] after a conv stage
+enum StageKind { ST_SMALL = 0, ST_MFMA = 1, ST_HEAD = 2, ST_GENERIC = 3, ST_POOLDENSE = 4 };
 
 struct Stage {
     int kind = ST_MFMA;
     int kh = 1, kw = 1, cin = 0, cout = 0, cout_pad = 0;
-    int pool = 1;
+    int pool = 1;        // square pool window of the tuned kernels (1 or 3), 0 otherwise
+    int ph = 1, pw = 1;  // max-pool window (= strides)
     int act = ACT_NONE;
     float alpha = 0.f;
     int has_mag = 0;
@@ -896,6 +984,7 @@ struct Stage {
     double flops = 0, bytes = 0;  // algorithmic per window
     std::string name;
     int skipped = 0;    // first layer computed inside the next stage
+    int is_first = 0;   // reads the model input (f32 log-mel)
     int fused_first = 0;  // this stage computes the previous (first) layer itself
 };
 
@@ -1024,34 +1113,56 @@ static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream
 template <typename T>
 static int launch_stage(const Model& m, const Stage& s, const void* in, void* out, float* logits,
                         float* probs, int n, hipStream_t st, const Stage* first) {
+    using GT = typename Prec<T>::G;
     if (s.kind == ST_SMALL) {
-        AA_CHECK(s.kh == 3 && s.kw == 3 && s.cout == 32 && s.cin == 1, AA_ERR_UNSUPPORTED,
-                 "first conv %dx%d %d->%d unsupported", s.kh, s.kw, s.cin, s.cout);
         dim3 grid((s.Hc * s.Wc + 255) / 256, n);
-        using GT = typename Prec<T>::G;
         hipLaunchKernelGGL((conv_small<GT, 3, 3, 32>), grid, dim3(256), 0, st, (const float*)in, s.Hin,
                            s.Win, (const float*)s.d_w, s.d_b, s.has_mag, s.mag_exp, (GT*)out, s.Hc, s.Wc,
                            s.act, s.alpha);
         AA_LAUNCH_CHECK();
         return AA_OK;
     }
+    if (s.kind == ST_GENERIC) {
+        if constexpr (is_fp8<T>()) {
+            set_error("%s: no fp8 kernel for this shape", s.name.c_str());
+            return AA_ERR_UNSUPPORTED;
+        } else {
+            dim3 grid((s.Hout * s.Wout + 255) / 256, (s.cout + 7) / 8, n);
+            if (s.is_first) {  // reads the f32 model input (log-mel)
+                hipLaunchKernelGGL((conv_generic<float, GT>), grid, dim3(256), 0, st, (const float*)in, s.Hin,
+                                   s.Win, s.cin, (const float*)s.d_w, s.d_b, s.kh, s.kw, s.cout, s.ph, s.pw, s.Hout,
+                                   s.Wout, s.act, s.alpha, s.has_mag, s.mag_exp, (GT*)out);
+            } else {
+                hipLaunchKernelGGL((conv_generic<GT, GT>), grid, dim3(256), 0, st, (const GT*)in, s.Hin, s.Win,
+                                   s.cin, (const float*)s.d_w, s.d_b, s.kh, s.kw, s.cout, s.ph, s.pw, s.Hout,
+                                   s.Wout, s.act, s.alpha, 0, 1.f, (GT*)out);
+            }
+            AA_LAUNCH_CHECK();
+            return AA_OK;
+        }
+    }
+    if (s.kind == ST_POOLDENSE) {
+        hipLaunchKernelGGL((pool_dense<GT>), dim3(n), dim3(256), (size_t)s.cin * sizeof(float), st, (const GT*)in,
+                           s.Hin * s.Win, s.cin, (const float*)s.d_w, s.d_b, s.cout, s.sigmoid, logits, probs);
+        AA_LAUNCH_CHECK();
+        return AA_OK;
+    }
     if (s.kind == ST_HEAD) {
-        AA_CHECK(s.cin == 256 && s.cout_pad == 32, AA_ERR_UNSUPPORTED, "head %d->%d unsupported", s.cin,
-                 s.cout);
         // pixel ranges of 64 spread over blocks (a window alone is too little
-        // work for one block's dependent load chain); their column maxima go to
-        // the free ping-pong buffer `out` and head_final reduces them
+        // work for one block's dependent load chain), 32 labels per block;
+        // their column maxima go to the free ping-pong buffer `out` and
+        // head_final reduces them
         const int HW = s.Hin * s.Win, parts = (HW + 63) / 64;
         float* part = static_cast<float*>(out);
         const float* hsc = is_fp8<T>() ? s.d_b + s.cout_pad : nullptr;  // fp8 dequantisation scales
         // split-bf16: the head reads f32 activations and runs the exact f32
         // MFMA (its 1x1 contraction is <1 % of the network's FLOPs)
-        using HT = typename Prec<T>::G;
-        hipLaunchKernelGGL((conv_head<HT, 256, 1, 2>), dim3(n, parts), dim3(256), 0, st, (const HT*)in, HW,
-                           (const HT*)s.d_w, s.d_b, s.cout, s.act, s.alpha, s.sigmoid, logits, probs, part, hsc);
+        hipLaunchKernelGGL((conv_head<GT, 1, 2>), dim3(n, parts, s.cout_pad / 32), dim3(256), 0, st, (const GT*)in,
+                           HW, s.cin, (const GT*)s.d_w, s.d_b, s.cout, s.act, s.alpha, s.sigmoid, logits, probs, part,
+                           hsc);
         AA_LAUNCH_CHECK();
-        hipLaunchKernelGGL(head_final, dim3(n), dim3(64), 0, st, part, parts, 32, s.d_b, s.cout, s.act, s.alpha,
-                           s.sigmoid, logits, probs, hsc);
+        hipLaunchKernelGGL(head_final, dim3(n), dim3(s.cout <= 64 ? 64 : 256), 0, st, part, parts, s.cout_pad, s.d_b,
+                           s.cout, s.act, s.alpha, s.sigmoid, logits, probs, hsc);
         AA_LAUNCH_CHECK();
         return AA_OK;
     }
@@ -1165,6 +1276,19 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         set_error("aa_model_create: layer %d: %s", i, msg);
         rc = code;
     };
+    auto upload = [&](Stage& s, const void* w, size_t wbytes, const std::vector<float>& bias) -> bool {
+        hipError_t e = hipMalloc(&s.d_w, wbytes ? wbytes : 4);
+        if (e == hipSuccess && wbytes) e = hipMemcpy(s.d_w, w, wbytes, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc((void**)&s.d_b, sizeof(float) * std::max<size_t>(bias.size(), 1));
+        if (e == hipSuccess && !bias.empty())
+            e = hipMemcpy(s.d_b, bias.data(), sizeof(float) * bias.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            m->st.push_back(s);
+            fail(AA_ERR_HIP, hipGetErrorString(e));
+            return false;
+        }
+        return true;
+    };
     while (i < n_layers && rc == AA_OK) {
         const aa_layer& ly = layers[i];
         if (ly.op == AA_OP_MAGTRANSFORM) {
@@ -1173,6 +1297,52 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             has_mag = 1;
             mag_exp = 1.f / (1.f + expf(-a[0]));  // sigmoid(a) in f32 like tf.math.sigmoid
             ++i;
+            continue;
+        }
+        if (ly.op == AA_OP_GLOBALMAXPOOL2D) {
+            // GlobalMaxPool2D [+ Dense] [+ sigmoid] after a conv stage: one
+            // pool_dense launch (the 1x1-conv head pattern is folded below)
+            if (m->st.empty()) { fail(AA_ERR_UNSUPPORTED, "GlobalMaxPool2D before any conv"); break; }
+            Stage s;
+            s.kind = ST_POOLDENSE;
+            s.Hin = H;
+            s.Win = W;
+            s.cin = C;
+            s.cout = C;
+            ++i;
+            std::vector<float> wd, bias;
+            if (i < n_layers && layers[i].op == AA_OP_DENSE) {
+                const aa_layer& d = layers[i];
+                s.cout = d.filters;
+                const float* k = get(d.off[0], (int64_t)C * d.filters);
+                if (!k || d.filters <= 0) { fail(AA_ERR_INVALID, "dense kernel outside the blob"); break; }
+                wd.assign(k, k + (size_t)C * d.filters);
+                bias.assign(d.filters, 0.f);
+                if (d.off[1] >= 0) {
+                    const float* bb = get(d.off[1], d.filters);
+                    if (!bb) { fail(AA_ERR_INVALID, "dense bias outside the blob"); break; }
+                    bias.assign(bb, bb + d.filters);
+                }
+                ++i;
+            }
+            if (i < n_layers && layers[i].op == AA_OP_SIGMOID) {
+                s.sigmoid = 1;
+                ++i;
+            }
+            if (i != n_layers) { fail(AA_ERR_UNSUPPORTED, "layers after the global pooling / dense"); break; }
+            s.cout_pad = s.cout;
+            if (!upload(s, wd.empty() ? nullptr : wd.data(), wd.size() * sizeof(float), bias)) break;
+            if (wd.empty()) {  // no Dense: pool_dense reads a null weight pointer
+                (void)hipFree(s.d_w);
+                s.d_w = nullptr;
+            }
+            s.flops = 2.0 * C * (wd.empty() ? 0 : s.cout);
+            s.bytes = (double)prec_bytes(precision) * H * W * C + 4.0 * s.cout;
+            char nm[96];
+            snprintf(nm, sizeof nm, "globalmax%s_%d_%d", wd.empty() ? "" : "_dense", C, s.cout);
+            s.name = nm;
+            m->st.push_back(s);
+            m->L = s.cout;
             continue;
         }
         if (ly.op != AA_OP_CONV2D) { fail(AA_ERR_UNSUPPORTED, "expected Conv2D"); break; }
@@ -1185,6 +1355,7 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         s.Win = W;
         s.Hc = H - ly.kh + 1;
         s.Wc = W - ly.kw + 1;
+        s.is_first = m->st.empty();
         if (s.Hc <= 0 || s.Wc <= 0) { fail(AA_ERR_INVALID, "input smaller than the kernel"); break; }
         const int K = s.kh * s.kw * s.cin;
         const float* kern = get(ly.off[0], (int64_t)K * s.cout);
@@ -1212,52 +1383,62 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         if (i < n_layers && (layers[i].op == AA_OP_LEAKYRELU || layers[i].op == AA_OP_RELU)) {
             s.act = layers[i].op == AA_OP_LEAKYRELU ? ACT_LEAKY : ACT_RELU;
             s.alpha = layers[i].alpha;
+            if (s.act == ACT_LEAKY && s.alpha < 0.f) { fail(AA_ERR_UNSUPPORTED, "LeakyReLU with a negative slope"); break; }
             ++i;
         }
         if (i < n_layers && layers[i].op == AA_OP_MAXPOOL2D) {
-            if (layers[i].kh != 3 || layers[i].kw != 3) { fail(AA_ERR_UNSUPPORTED, "only 3x3 max-pool is fused"); break; }
-            s.pool = 3;
+            if (layers[i].kh <= 0 || layers[i].kw <= 0) { fail(AA_ERR_INVALID, "max-pool window"); break; }
+            s.ph = layers[i].kh;
+            s.pw = layers[i].kw;
             ++i;
         }
-        if (i < n_layers && layers[i].op == AA_OP_GLOBALMAXPOOL2D) {
+        s.pool = (s.ph == s.pw && (s.ph == 1 || s.ph == 3)) ? s.ph : 0;
+        s.Hout = s.Hc / s.ph;
+        s.Wout = s.Wc / s.pw;
+        if (s.Hout <= 0 || s.Wout <= 0) { fail(AA_ERR_INVALID, "pool window larger than the conv output"); break; }
+        const bool gpool = i < n_layers && layers[i].op == AA_OP_GLOBALMAXPOOL2D;
+        const bool dense_next = gpool && i + 1 < n_layers && layers[i + 1].op == AA_OP_DENSE;
+        // (the first stage reads the f32 model input: only ST_SMALL / ST_GENERIC do)
+        if (!s.is_first && gpool && !dense_next && s.kh == 1 && s.kw == 1 && s.ph == 1 && s.pw == 1 &&
+            s.cin % 32 == 0 && s.cout <= 1024) {
+            // the reference family's head: 1x1 conv, global max, sigmoid
             s.kind = ST_HEAD;
             ++i;
             if (i < n_layers && layers[i].op == AA_OP_SIGMOID) {
                 s.sigmoid = 1;
                 ++i;
             }
-            if (i != n_layers || s.pool != 1 || s.kh != 1 || s.kw != 1) {
-                fail(AA_ERR_UNSUPPORTED, "GlobalMaxPool2D must follow a final 1x1 conv");
+            if (i != n_layers) { fail(AA_ERR_UNSUPPORTED, "layers after the 1x1 head"); break; }
+        } else if (s.cin == 1 && s.kh == 3 && s.kw == 3 && s.cout == 32 && s.pool == 1) {
+            s.kind = ST_SMALL;
+        } else if (!s.is_first && s.pool && mfma_bn(precision, s.kh, s.kw, s.cin, s.pool)) {
+            s.kind = ST_MFMA;
+        } else {
+            s.kind = ST_GENERIC;
+            if (precision == AA_PREC_FP8) {
+                fail(AA_ERR_UNSUPPORTED, "no fp8 kernel for this conv shape (the f32 / bf16x3 / bf16 modes have one)");
                 break;
             }
-        } else if (s.cin <= 4) {
-            s.kind = ST_SMALL;
-        } else {
-            s.kind = ST_MFMA;
         }
-        s.Hout = s.pool > 1 ? s.Hc / s.pool : s.Hc;
-        s.Wout = s.pool > 1 ? s.Wc / s.pool : s.Wc;
-        if (s.kind == ST_SMALL) {
+        if (s.is_first) {
             s.has_mag = has_mag;
             s.mag_exp = mag_exp;
-            if (s.pool != 1) { fail(AA_ERR_UNSUPPORTED, "pool after the first conv"); break; }
-        } else if (has_mag && m->st.empty()) {
-            fail(AA_ERR_UNSUPPORTED, "MagTransform needs a C_in=1 first conv");
-            break;
+            if (has_mag && s.kind != ST_SMALL && s.kind != ST_GENERIC) {
+                fail(AA_ERR_UNSUPPORTED, "MagTransform needs a C_in=1 first conv");
+                break;
+            }
         }
         int bn_tile = 32;
-        if (s.kind == ST_MFMA) {
-            bn_tile = mfma_bn(precision, s.kh, s.kw, s.cin, s.pool);
-            if (!bn_tile) { fail(AA_ERR_UNSUPPORTED, "no conv kernel for this shape"); break; }
-        }
-        s.cout_pad = (s.kind == ST_SMALL) ? s.cout : (s.cout + bn_tile - 1) / bn_tile * bn_tile;
-        // pack weights with the BN scale folded in: conv_small [cout][K];
-        // MFMA stages tap-major with padded rows [kh*KW + kw][cout_pad][cstr]
-        // (a block's per-tap slice is one contiguous block, byte-identical to
-        // its LDS image) plus 1 KiB of slack for the last slice's rounding;
-        // the 1x1 head [cout_pad][C_in]
-        const bool bf = (precision == AA_PREC_BF16) && s.kind != ST_SMALL;
-        const bool f8 = (precision == AA_PREC_FP8) && s.kind != ST_SMALL;
+        if (s.kind == ST_MFMA) bn_tile = mfma_bn(precision, s.kh, s.kw, s.cin, s.pool);
+        const bool rowmajor = s.kind == ST_SMALL || s.kind == ST_GENERIC;  // f32 [cout][K]
+        s.cout_pad = rowmajor ? s.cout : (s.cout + bn_tile - 1) / bn_tile * bn_tile;
+        // pack weights with the BN scale folded in: conv_small / generic
+        // [cout][K] f32; MFMA stages tap-major with padded rows
+        // [kh*KW + kw][cout_pad][cstr] (a block's per-tap slice is one
+        // contiguous block, byte-identical to its LDS image) plus 1 KiB of
+        // slack for the last slice's rounding; the 1x1 head [cout_pad][C_in]
+        const bool bf = (precision == AA_PREC_BF16) && !rowmajor;
+        const bool f8 = (precision == AA_PREC_FP8) && !rowmajor;
         // split-bf16: conv_x3 steps of hi/lo bf16 rows (packed below from the
         // compact f32 [tap][cout_pad][C_in] image); the head stays f32
         const bool sp = (precision == AA_PREC_BF16X3) && s.kind == ST_MFMA;
@@ -1267,11 +1448,11 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                                            : s.cin;
         const int ntap = s.kh * s.kw;
         const size_t slack = s.kind == ST_MFMA ? 1024 / wes : 0;
-        std::vector<float> wpk(s.kind == ST_SMALL ? (size_t)s.cout * K : (size_t)ntap * s.cout_pad * cstr + slack, 0.f);
+        std::vector<float> wpk(rowmajor ? (size_t)s.cout * K : (size_t)ntap * s.cout_pad * cstr + slack, 0.f);
         for (int o = 0; o < s.cout; ++o)
             for (int k = 0; k < K; ++k) {
                 const double v = kern[(size_t)k * s.cout + o] * scale[o];
-                if (s.kind == ST_SMALL) {
+                if (rowmajor) {
                     wpk[(size_t)o * K + k] = (float)v;
                 } else {
                     const int t = k / s.cin, c = k - t * s.cin;
@@ -1283,67 +1464,61 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         for (int o = 0; o < s.cout; ++o) bias[o] = (float)shift[o];
         // split-bf16 stores hi + lo: twice the compact image's elements
         const size_t wbytes = (sp ? 2 * wpk.size() : wpk.size()) * wes;
-        hipError_t e = hipMalloc(&s.d_w, wbytes);
-        if (e == hipSuccess) {
-            if (f8) {
-                // per output channel: the largest |w| maps to 240 (e4m3fn tops
-                // out at 448), the kernel's epilogue multiplies by amax / 240
-                std::vector<uint8_t> h(wpk.size(), 0);
-                for (int o = 0; o < s.cout_pad; ++o) {
-                    float amax = 0.f;
-                    for (int t = 0; t < ntap; ++t)
-                        for (int c = 0; c < s.cin; ++c) amax = std::max(amax, std::fabs(wpk[((size_t)t * s.cout_pad + o) * cstr + c]));
-                    const float sc = amax > 0.f ? 240.f / amax : 1.f;
-                    bias[s.cout_pad + o] = 1.f / sc;
-                    for (int t = 0; t < ntap; ++t)
-                        for (int c = 0; c < s.cin; ++c) {
-                            const size_t k = ((size_t)t * s.cout_pad + o) * cstr + c;
-                            h[k] = f2fp8(wpk[k] * sc);
-                        }
-                }
-                e = hipMemcpy(s.d_w, h.data(), wbytes, hipMemcpyHostToDevice);
-            } else if (bf) {
-                std::vector<uint16_t> h(wpk.size());
-                for (size_t k = 0; k < wpk.size(); ++k) h[k] = f2bf(wpk[k]);
-                e = hipMemcpy(s.d_w, h.data(), wbytes, hipMemcpyHostToDevice);
-            } else if (sp) {
-                // conv_x3 steps (32-channel group g, tap t) in order s = g * ntap + t,
-                // each [cout_pad][8 units of 8 bf16]: units 0-3 hi = rn_bf16(w) of
-                // channels 32 g + 8 u .. + 7, units 4-7 lo = rn_bf16(w - hi), unit u
-                // of row o stored in slot (u + o) & 7 (aa_conv_x3.h)
-                std::vector<uint16_t> h(2 * wpk.size(), 0);
-                const int ng = s.cin / 32;
-                for (int g = 0; g < ng; ++g)
-                    for (int t = 0; t < ntap; ++t)
-                        for (int o = 0; o < s.cout_pad; ++o) {
-                            const size_t row = ((size_t)(g * ntap + t) * s.cout_pad + o) * 64;
-                            for (int c = 0; c < 32; ++c) {
-                                const float w = wpk[((size_t)t * s.cout_pad + o) * cstr + 32 * g + c];
-                                const uint16_t hi = f2bf(w);
-                                const int u = c / 8;
-                                h[row + ((u + o) & 7) * 8 + c % 8] = hi;
-                                h[row + ((u + 4 + o) & 7) * 8 + c % 8] = f2bf(w - bf2f(hi));
-                            }
-                        }
-                e = hipMemcpy(s.d_w, h.data(), wbytes, hipMemcpyHostToDevice);
-            } else {
-                e = hipMemcpy(s.d_w, wpk.data(), wbytes, hipMemcpyHostToDevice);
+        bool ok = true;
+        if (f8) {
+            // per output channel: the largest |w| maps to 240 (e4m3fn tops
+            // out at 448), the kernel's epilogue multiplies by amax / 240
+            std::vector<uint8_t> h(wpk.size(), 0);
+            for (int o = 0; o < s.cout_pad; ++o) {
+                float amax = 0.f;
+                for (int t = 0; t < ntap; ++t)
+                    for (int c = 0; c < s.cin; ++c) amax = std::max(amax, std::fabs(wpk[((size_t)t * s.cout_pad + o) * cstr + c]));
+                const float sc = amax > 0.f ? 240.f / amax : 1.f;
+                bias[s.cout_pad + o] = 1.f / sc;
+                for (int t = 0; t < ntap; ++t)
+                    for (int c = 0; c < s.cin; ++c) {
+                        const size_t k = ((size_t)t * s.cout_pad + o) * cstr + c;
+                        h[k] = f2fp8(wpk[k] * sc);
+                    }
             }
+            ok = upload(s, h.data(), wbytes, bias);
+        } else if (bf) {
+            std::vector<uint16_t> h(wpk.size());
+            for (size_t k = 0; k < wpk.size(); ++k) h[k] = f2bf(wpk[k]);
+            ok = upload(s, h.data(), wbytes, bias);
+        } else if (sp) {
+            // conv_x3 steps (32-channel group g, tap t) in order s = g * ntap + t,
+            // each [cout_pad][8 units of 8 bf16]: units 0-3 hi = rn_bf16(w) of
+            // channels 32 g + 8 u .. + 7, units 4-7 lo = rn_bf16(w - hi), unit u
+            // of row o stored in slot (u + o) & 7 (aa_conv_x3.h)
+            std::vector<uint16_t> h(2 * wpk.size(), 0);
+            const int ng = s.cin / 32;
+            for (int g = 0; g < ng; ++g)
+                for (int t = 0; t < ntap; ++t)
+                    for (int o = 0; o < s.cout_pad; ++o) {
+                        const size_t row = ((size_t)(g * ntap + t) * s.cout_pad + o) * 64;
+                        for (int c = 0; c < 32; ++c) {
+                            const float w = wpk[((size_t)t * s.cout_pad + o) * cstr + 32 * g + c];
+                            const uint16_t hi = f2bf(w);
+                            const int u = c / 8;
+                            h[row + ((u + o) & 7) * 8 + c % 8] = hi;
+                            h[row + ((u + 4 + o) & 7) * 8 + c % 8] = f2bf(w - bf2f(hi));
+                        }
+                    }
+            ok = upload(s, h.data(), wbytes, bias);
+        } else {
+            ok = upload(s, wpk.data(), wbytes, bias);
         }
-        if (e == hipSuccess) e = hipMalloc((void**)&s.d_b, sizeof(float) * bias.size());
-        if (e == hipSuccess) e = hipMemcpy(s.d_b, bias.data(), sizeof(float) * bias.size(), hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            m->st.push_back(s);
-            fail(AA_ERR_HIP, hipGetErrorString(e));
-            break;
-        }
+        if (!ok) break;
         s.flops = 2.0 * s.Hc * s.Wc * K * s.cout;
         const double es = (double)prec_bytes(precision);
-        s.bytes = (s.kind == ST_SMALL ? 4.0 : es) * s.Hin * s.Win * s.cin +
+        s.bytes = (s.is_first ? 4.0 : es) * s.Hin * s.Win * s.cin +
                   (s.kind == ST_HEAD ? 4.0 * s.cout : es * s.Hout * s.Wout * s.cout);
-        char nm[96];
-        snprintf(nm, sizeof nm, "%s%dx%d_%d_%d%s", s.kind == ST_SMALL ? "conv_small_" : s.kind == ST_HEAD ? "head_" : "conv_",
-                 s.kh, s.kw, s.cin, s.cout, s.pool > 1 ? "_pool3" : "");
+        char nm[96], pl[24] = "";
+        if (s.ph > 1 || s.pw > 1) snprintf(pl, sizeof pl, s.ph == s.pw ? "_pool%d" : "_pool%dx%d", s.ph, s.pw);
+        snprintf(nm, sizeof nm, "%s%dx%d_%d_%d%s",
+                 s.kind == ST_SMALL ? "conv_small_" : s.kind == ST_HEAD ? "head_" : s.kind == ST_GENERIC ? "conv_generic_" : "conv_",
+                 s.kh, s.kw, s.cin, s.cout, pl);
         s.name = nm;
         m->st.push_back(s);
         H = s.Hout;
@@ -1351,8 +1526,8 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         C = s.cout;
         if (s.kind == ST_HEAD) m->L = s.cout;
     }
-    if (rc == AA_OK && (m->st.empty() || m->st.back().kind != ST_HEAD)) {
-        set_error("aa_model_create: the model must end with conv1x1 + GlobalMaxPool2D");
+    if (rc == AA_OK && (m->st.empty() || (m->st.back().kind != ST_HEAD && m->st.back().kind != ST_POOLDENSE))) {
+        set_error("aa_model_create: the model must end with GlobalMaxPool2D (after a 1x1 conv or before a Dense)");
         rc = AA_ERR_UNSUPPORTED;
     }
     if (rc != AA_OK) {
@@ -1377,7 +1552,7 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
     // ping-pong activation buffers: stage s writes buffer s % 2
     for (size_t k = 0; k + 1 < m->st.size(); ++k) {
         const Stage& s = m->st[k];
-        if (s.skipped) continue;
+        if (s.skipped || s.kind == ST_POOLDENSE) continue;
         const size_t e = (size_t)s.Hout * s.Wout * s.cout;
         m->act_elems[k % 2] = std::max(m->act_elems[k % 2], e);
     }
@@ -1386,7 +1561,7 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         const size_t es = prec_bytes(precision);
         const size_t parts = ((size_t)h.Hin * h.Win + 63) / 64;
         const size_t k = m->st.size() - 1;
-        m->act_elems[k % 2] = std::max(m->act_elems[k % 2], (parts * 32 * sizeof(float) + es - 1) / es);
+        m->act_elems[k % 2] = std::max(m->act_elems[k % 2], (parts * h.cout_pad * sizeof(float) + es - 1) / es);
     }
     *model = m;
     return AA_OK;

@@ -101,6 +101,12 @@ int aa_fe_set_timing(void* plan, uint32_t stage_mask);
 int aa_fe_stage_time(void* plan, int32_t stage, double* total_ms, int64_t* count);
 
 /* ---------------- CNN: log-mel windows -> logits / probabilities ---------------- */
+/* Supported layer sequences: [MagTransform] then Conv2D blocks (Conv2D
+ * [BatchNormalization] [LeakyReLU|ReLU] [MaxPooling2D]) ending in either a
+ * 1x1 Conv2D + GlobalMaxPool2D [+ sigmoid] head or GlobalMaxPool2D [+ Dense]
+ * [+ sigmoid].  Tuned matrix-core kernels serve the build's model family
+ * (stage names "conv_*"); any other conv shape or pool window runs a generic
+ * f32 kernel (stage name "conv_generic_*"; not in the fp8 mode). */
 typedef enum aa_op {
     AA_OP_CONV2D = 1,       /* Keras Conv2D, padding="valid", stride 1 */
     AA_OP_BATCHNORM = 2,    /* inference BatchNormalization (moving stats) */
@@ -110,6 +116,8 @@ typedef enum aa_op {
     AA_OP_SIGMOID = 6,
     AA_OP_MAGTRANSFORM = 7, /* x ** sigmoid(a) */
     AA_OP_RELU = 8,
+    AA_OP_DENSE = 9,        /* after GlobalMaxPool2D: filters = units,
+                             * off[0] = kernel [C_in][units], off[1] = bias */
 } aa_op;
 
 typedef struct aa_layer {

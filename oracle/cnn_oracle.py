@@ -16,6 +16,8 @@ that layer list literally, un-fused, in torch-CPU float32 (or float64):
 * ``leakyrelu``     -> max(x, alpha*x)
 * ``maxpool2d``     -> Keras MaxPooling2D(pool), strides = pool, valid (floor)
 * ``globalmaxpool2d`` -> max over H, W
+* ``relu``          -> max(x, 0)
+* ``dense``         -> Keras Dense after the global pooling (x @ kernel + bias)
 * ``activation``    -> sigmoid
 
 ``logits`` are the GlobalMaxPool outputs before the final sigmoid.
@@ -65,6 +67,13 @@ def forward(path_or_arch, x_nhwc: np.ndarray, dtype=torch.float32, tensors=None)
             x = x * g[None, :, None, None] + be[None, :, None, None]
         elif kind == "leakyrelu":
             x = F.leaky_relu(x, float(layer.get("alpha", 0.3)))
+        elif kind == "relu":
+            x = F.relu(x)
+        elif kind == "dense":  # Keras Dense after the global pooling: x @ kernel + bias
+            x = x @ t(name + ".kernel")
+            if layer.get("use_bias", True):
+                x = x + t(name + ".bias")
+            logits = x
         elif kind == "maxpool2d":
             ph, pw = layer["pool"]
             x = F.max_pool2d(x, (ph, pw), (ph, pw))
