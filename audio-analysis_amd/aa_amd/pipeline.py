@@ -15,6 +15,7 @@ Models and front-end plans are cached across recordings.
 """
 from __future__ import annotations
 
+import dataclasses
 import logging
 import os
 from pathlib import Path
@@ -122,18 +123,23 @@ class Classifier:
             else:
                 logging.info("Re using track data this will cuase problems if the STFT settings are "
                              "not the same for multiple models")
-            if "efficientnet" in model_name.lower():
-                raise NotImplementedError("efficientnet (3-channel) models")
             counts = [len(tv) for tv in views]
             if sum(counts) == 0:
                 continue
+            group_mel = logmel
+            if "efficientnet" in model_name.lower():
+                # np.repeat(d, 3, -1) of the shared windows (:539-540): every
+                # channel is the same log-mel, so this is the first group's
+                # front end with three times the channels
+                fe3 = self.frontend(dataclasses.replace(fe.s, channels=fe.s.channels * 3))
+                group_mel = fe3.run(pcm, rows)
             begin = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32)
             probs = torch.empty((len(group), sum(counts), len(labels)), dtype=torch.float32, device=dev)
             for k, (path, m_meta) in enumerate(group):
-                m = self.model(path, m_meta, logmel.shape[1:])
+                m = self.model(path, m_meta, group_mel.shape[1:])
                 if m.n_labels != len(labels):
                     raise ValueError(f"{path}: {m.n_labels} outputs for {len(labels)} labels")
-                m.forward(logmel, probs=probs[k])
+                m.forward(group_mel, probs=probs[k])
             sel = [i for i, c in enumerate(counts) if c > 0]
             wb = torch.from_numpy(begin[sel]).to(dev)
             wc = torch.from_numpy(np.asarray(counts, np.int32)[sel]).to(dev)

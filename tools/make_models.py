@@ -164,8 +164,10 @@ def calibration_input(n, n_mels, T, db_scale, rng):
 
 
 def make_model(out_dir, name="model1", seed=1, widths=(32, 32, 64, 64, 128, 256),
-               labels=None, mag=None, meta_overrides=None, pre_model=False):
-    """Create ``out_dir/audioModel.safetensors`` + ``out_dir/metadata.txt``."""
+               labels=None, mag=None, meta_overrides=None, pre_model=False, in_channels=None):
+    """Create ``out_dir/audioModel.safetensors`` + ``out_dir/metadata.txt``.
+    ``in_channels`` overrides the input channels (default: meta channels),
+    e.g. 3 for an "efficientnet"-named model fed the repeated log-mel."""
     from safetensors.numpy import save_file
     labels = list(labels or LABELS)
     meta = dict(DEFAULT_META)
@@ -181,7 +183,7 @@ def make_model(out_dir, name="model1", seed=1, widths=(32, 32, 64, 64, 128, 256)
     })
     rng = np.random.default_rng(seed)
     arch = arch_layers(widths, len(labels), mag)
-    channels = int(meta.get("channels", 1))
+    channels = int(in_channels or meta.get("channels", 1))
     tensors = _init_weights(arch, channels, rng)
     T = 1 + int(meta["segment_length"] * 48000) // int(meta["hop_length"])
     x = calibration_input(6, int(meta["n_mels"]), T, bool(meta["db_scale"]), rng)
