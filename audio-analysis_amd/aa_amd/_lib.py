@@ -14,7 +14,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede loading libaa.so, see above)
 
 LIB_PATH = Path(__file__).resolve().parent / "libaa.so"
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 AA_PREC_F32 = 0
 AA_PREC_BF16 = 1
@@ -53,7 +53,7 @@ class FeConfig(C.Structure):
         ("win_len", C.c_int32), ("n_fft", C.c_int32), ("hop", C.c_int32), ("n_mels", C.c_int32),
         ("normalize", C.c_int32), ("db_scale", C.c_int32), ("power", C.c_float),
         ("amin", C.c_float), ("top_db", C.c_float), ("mean_sub", C.c_int32),
-        ("channels", C.c_int32),
+        ("channels", C.c_int32), ("out_f16", C.c_int32),
     ]
 
 
@@ -102,6 +102,7 @@ _SIGS = {
     "aa_model_stage_info": (C.c_int, [C.c_void_p, C.c_int32, C.c_char_p, C.c_int32,
                                       C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "aa_model_set_timing": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "aa_model_set_input_f16": (C.c_int, [C.c_void_p, C.c_int32]),
     "aa_model_stage_time": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double),
                                       C.POINTER(C.c_int64)]),
     "aa_track_mean": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_void_p,

@@ -59,15 +59,21 @@ class FeSettings:
 class FrontEnd(_lib.StageTiming):
     _timing_prefix = "aa_fe"
 
-    def __init__(self, s: FeSettings, device=None):
+    def __init__(self, s: FeSettings, device=None, out_dtype=torch.float32):
+        """out_dtype: torch.float32 (what get_spect returns) or torch.float16
+        (BASELINE configs[4]'s fp16 log-mel; aa_fe_config.out_f16)."""
         self.s = s
         self.device = torch.device(device or "cuda")
+        if out_dtype not in (torch.float32, torch.float16):
+            raise ValueError(f"log-mel dtype {out_dtype}: float32 or float16")
+        self.out_dtype = out_dtype
         L = _lib.lib()
         cfg = _lib.FeConfig(
             win_len=s.win_len, n_fft=int(s.n_fft), hop=int(s.hop_length), n_mels=int(s.n_mels),
             normalize=int(bool(s.normalize)), db_scale=int(bool(s.db_scale)),
             power=float(s.effective_power), amin=1e-10, top_db=80.0,
-            mean_sub=int(bool(s.mean_sub)), channels=int(s.channels))
+            mean_sub=int(bool(s.mean_sub)), channels=int(s.channels),
+            out_f16=int(out_dtype == torch.float16))
         fb = np.ascontiguousarray(s.filterbank(), dtype=np.float32)
         h = C.c_void_p()
         with torch.cuda.device(self.device):
@@ -100,11 +106,11 @@ class FrontEnd(_lib.StageTiming):
         rows (see ``pack_windows``) on device."""
         n_win = int(windows.shape[0])
         if out is None:
-            out = torch.empty(self.out_shape(n_win), dtype=torch.float32, device=self.device)
+            out = torch.empty(self.out_shape(n_win), dtype=self.out_dtype, device=self.device)
         if n_win == 0:
             return out
         assert pcm.dtype == torch.float32 and windows.dtype == torch.int64
-        assert tuple(out.shape) == self.out_shape(n_win)
+        assert tuple(out.shape) == self.out_shape(n_win) and out.dtype == self.out_dtype
         ws = workspace if workspace is not None else self._workspace(n_win)
         _lib.check(_lib.lib().aa_fe_run(
             self._h, _lib.dptr(pcm), int(pcm.numel()), _lib.dptr(windows), n_win, _lib.dptr(out),

@@ -157,6 +157,7 @@ class Model(_lib.StageTiming):
         self._h = h
         self.n_labels = _lib.lib().aa_model_n_outputs(h)
         self._ws = None
+        self._in_f16 = False
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -175,10 +176,17 @@ class Model(_lib.StageTiming):
 
     def forward(self, x: torch.Tensor, logits: torch.Tensor = None, probs: torch.Tensor = None,
                 stream=None, workspace: torch.Tensor = None):
-        """x: float32 [n, H, W, C] on device -> (logits, probs) float32 [n, L]."""
+        """x: float32 (or float16: BASELINE configs[4]) [n, H, W, C] on device ->
+        (logits, probs) float32 [n, L]."""
         n = int(x.shape[0])
         if tuple(x.shape[1:]) != self.in_shape:
             raise ValueError(f"input {tuple(x.shape)} != model input {self.in_shape}")
+        if x.dtype not in (torch.float32, torch.float16):
+            raise ValueError(f"input dtype {x.dtype}: float32 or float16")
+        f16 = x.dtype == torch.float16
+        if f16 != self._in_f16:
+            _lib.check(_lib.lib().aa_model_set_input_f16(self._h, int(f16)), "aa_model_set_input_f16")
+            self._in_f16 = f16
         if logits is None:
             logits = torch.empty((n, self.n_labels), dtype=torch.float32, device=self.device)
         if probs is None:

@@ -213,11 +213,26 @@ __host__ __device__ constexpr size_t conv_b_offset() {
     return off;
 }
 
-// One tap's weight slice [BN][CSTR] in LDS, rounded up to whole 1-KiB
+// fp8 runs the block-scaled K = 128 MFMA (v_mfma_f32_16x16x128_f8f6f4, the
+// scale operands literal 0 = unscaled, 2x the non-scaled fp8 rate): its K
+// loop walks "super-steps" of four 32-deep chunks (chunk k = tap * C_in/32 +
+// channel chunk), and its weights are packed per super-step as rows of
+// 4 x 32 B (+16 B pad) instead of per tap.
+constexpr int F8_BSTR = 144;  // bytes of one packed fp8 weight row (128 + pad)
+template <typename T>
+__host__ __device__ constexpr int conv_bstr(int cin) {  // weight-row stride (elements) of one step's slice
+    return is_fp8<T>() ? F8_BSTR : conv_cstr<T>(cin);
+}
+template <typename T>
+__host__ __device__ constexpr int conv_nstep(int ntap, int cin) {  // K-loop steps (= weight slices)
+    return is_fp8<T>() ? (ntap * (cin / 32) + 3) / 4 : ntap;
+}
+
+// One step's weight slice [BN][BSTR] in LDS, rounded up to whole 1-KiB
 // wave-instructions of global_load_lds (the tail lanes land in the rounding).
 template <typename T, int CIN, int BN>
 __host__ __device__ constexpr int conv_slice_lds_bytes() {
-    return (BN * conv_cstr<T>(CIN) * (int)sizeof(typename Prec<T>::L) + 1023) / 1024 * 1024;
+    return (BN * conv_bstr<T>(CIN) * (int)sizeof(typename Prec<T>::L) + 1023) / 1024 * 1024;
 }
 
 template <typename T, int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool EBF16>
@@ -233,10 +248,12 @@ constexpr size_t conv_lds_bytes_nb(int nb) {
 template <typename T, int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool EBF16>
 constexpr int conv_ring() {
     constexpr size_t cap = 160 * 1024;
-    const size_t base = conv_lds_bytes_nb<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>(2);
+    // fp8: the loop reads slice s+1 while s+NB-1 is issued (one-step software pipeline): >= 3
+    constexpr int NB0 = is_fp8<T>() ? 3 : 2;
+    const size_t base = conv_lds_bytes_nb<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>(NB0);
     const size_t blocks = cap / base;
-    int nb = 2;
-    while (nb < 8 && nb < KH * KW &&
+    int nb = NB0;
+    while (nb < 8 && nb < conv_nstep<T>(KH * KW, CIN) &&
            blocks * conv_lds_bytes_nb<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>(nb + 1) <= cap)
         ++nb;
     return nb;
@@ -257,6 +274,14 @@ __device__ __forceinline__ void wait_vm_lgkm(int k) {
 #undef AA_W
 }
 
+// s_waitcnt vmcnt(N) alone (LDS reads stay in flight), N = PER * k
+template <int PER>
+__device__ __forceinline__ void wait_vm(int k) {
+#define AA_W(K) case K: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * K) : "memory"); break;
+    switch (k) { AA_W(0) AA_W(1) AA_W(2) AA_W(3) AA_W(4) AA_W(5) AA_W(6) default: AA_W(7) }
+#undef AA_W
+}
+
 // First layer fused into the next conv's patch staging (FUSED = true): the
 // log-mel patch is staged in LDS and the C_in = 1, 3x3 conv (f32 VALU, folded
 // BN, activation, optional MagTransform prologue) writes the activations the
@@ -270,7 +295,13 @@ struct FirstConv {
     int has_mag;
     float mag_exp;
     int H0, W0;      // log-mel image
+    int lm_f16;      // log-mel stored as float16 (aa_model_set_input_f16)
 };
+
+// one log-mel value of the fused first conv's input (f32, or f16 when lm_f16)
+__device__ __forceinline__ float load_lm(const void* in, size_t i, int lm_f16) {
+    return lm_f16 ? (float)reinterpret_cast<const _Float16*>(in)[i] : reinterpret_cast<const float*>(in)[i];
+}
 
 // DIAG (diagnostic builds only, tools/conv_bench.hip): bit 0 skips the patch
 // staging, bit 1 the MFMA loop, bit 2 the epilogue stores, bit 3 makes every
@@ -290,10 +321,10 @@ constexpr int conv_waves_per_simd() {
 }
 
 template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW,
-          bool FUSED = false, int DIAG = 0, bool EBF16 = false, bool APF = true>
+          bool FUSED = false, int DIAG = 0, bool EBF16 = false, int OCC = 0>
 __global__ __launch_bounds__(WM * WN * 64)
-__attribute__((amdgpu_waves_per_eu(conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>(),
-                                    conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>())))
+__attribute__((amdgpu_waves_per_eu(OCC ? OCC : conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>(),
+                                    OCC ? OCC : conv_waves_per_simd<T, KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, EBF16>())))
 void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
                                                  const typename Prec<T>::L* __restrict__ wt, const float* __restrict__ bias,
                                                  typename Prec<T>::G* __restrict__ out, int Hout, int Wout, int cout_store,
@@ -329,7 +360,8 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
     constexpr int CPC = CIN / 32;
     constexpr int NW = WM * WN;
     constexpr int NB = conv_ring<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>();
-    constexpr int SLICE = BN * CSTR;                               // elements
+    constexpr int NSTEP = conv_nstep<T>(NTAP, CIN);                // K-loop steps / weight slices
+    constexpr int SLICE = BN * conv_bstr<T>(CIN);                  // elements
     constexpr int SLICE_LDS = conv_slice_lds_bytes<T, CIN, BN>();  // bytes
     constexpr int GPS = SLICE_LDS / 1024;                          // wave-instructions per slice
     constexpr int GHI = (GPS + NW - 1) / NW, GLO = GPS / NW;       // this wave's share: GHI if wave < GPS % NW
@@ -346,7 +378,8 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
     }
     if constexpr (!(DIAG & 32)) {
 #pragma unroll
-        for (int t = 0; t < NB - 1; ++t) AA_GLDS(t)
+        for (int t = 0; t < NB - 1; ++t)
+            if (t < NSTEP) { AA_GLDS(t) }
     }
 
     // ---- stage the input patch ----
@@ -387,14 +420,14 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
         constexpr int XW = PW + 2, XN = (PH + 2) * XW;
         const size_t pbytes = ((size_t)PH * PW * CSTR * sizeof(LT) + 15) & ~(size_t)15;
         float* X = reinterpret_cast<float*>(smem + pbytes);
-        const float* lm = reinterpret_cast<const float*>(in) + (size_t)n * fc.H0 * fc.W0;
+        const size_t lmo = (size_t)n * fc.H0 * fc.W0;
         for (int i0 = 0; i0 < ((DIAG & 512) ? 0 : XN); i0 += 4 * NTHR) {
             float v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int idx = min(i0 + u * NTHR + (int)threadIdx.x, XN - 1);
                 const int r = idx / XW, c = idx - r * XW;
-                v[u] = lm[(size_t)min(oh0 + r, fc.H0 - 1) * fc.W0 + min(ow0 + c, fc.W0 - 1)];
+                v[u] = load_lm(in, lmo + (size_t)min(oh0 + r, fc.H0 - 1) * fc.W0 + min(ow0 + c, fc.W0 - 1), fc.lm_f16);
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -595,6 +628,91 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
     }
     // f32 (parity mode) fragments are twice as wide: single-buffered there
     constexpr bool DB = !std::is_same<T, float>::value;
+    if constexpr (F8) {
+        // ---- fp8: K = 128 per MFMA.  Super-step s covers chunks 4s .. 4s+3
+        // (chunk k: tap k / CPC, channel chunk k % CPC); lane group q's 32
+        // fragment bytes are its 8 bytes (channels 8q .. 8q+7) of each of the
+        // four chunks, read as four ds_read_b64 from the patch (A, pixels)
+        // and from the super-step's weight slice (B, rows of 4 x 32 B), in the
+        // same order for both operands -- the instruction's k order is the
+        // same permutation for A and B (tools/mfma_scale_probe.hip), so the
+        // product is the sum over the four chunks.  Chunks past the last tap
+        // have zero weights (their A reads re-read chunk 0: finite values).
+        // Software-pipelined by one step: the barrier at the top of step s
+        // publishes slice s+1, whose B fragments are read while step s's
+        // MFMAs run; A fragments are read just in time, two in flight. ----
+        typedef __attribute__((ext_vector_type(8))) int i32x8;
+        typedef __attribute__((ext_vector_type(2))) int i32x2;
+        constexpr int NCH = NTAP * CPC;
+        const int browf = (wn * NF * 16 + (lane & 15)) * F8_BSTR + q8;
+        auto choff = [&](int k) {
+            k = k < NCH ? k : 0;
+            const int t = k / CPC, cc = k - (k / CPC) * CPC;
+            const int kh = t / KW, kw = t - (t / KW) * KW;
+            return (kh * PW + kw) * CSTR + cc * 32;
+        };
+        auto rd4 = [](i32x8& v, const char* p0, const char* p1, const char* p2, const char* p3) {
+            const i32x2 x0 = *reinterpret_cast<const i32x2*>(p0), x1 = *reinterpret_cast<const i32x2*>(p1);
+            const i32x2 x2 = *reinterpret_cast<const i32x2*>(p2), x3 = *reinterpret_cast<const i32x2*>(p3);
+            v = i32x8{x0[0], x0[1], x1[0], x1[1], x2[0], x2[1], x3[0], x3[1]};
+        };
+        auto read_b8 = [&](i32x8* b, int st) {
+            const char* bt = Bs + (st % NB) * SLICE_LDS + browf;
+#pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                const char* r = bt + j * 16 * F8_BSTR;
+                rd4(b[j], r, r + 32, r + 64, r + 96);
+            }
+        };
+        const char* pb = reinterpret_cast<const char*>(patch);
+        auto f8step = [&](i32x8* bc, i32x8* bn, int st) {
+            if (st + 1 < NSTEP && !(DIAG & 32)) {
+                // own share of slice st+1 landed (st+2 .. st+NB-2 may stay in
+                // flight); this wave's reads of slice st-1 (whose buffer the
+                // next issue overwrites) were consumed by step st-1's MFMAs
+                const int ahead = min(NB - 3, NSTEP - 2 - st);
+                if (hi_share) wait_vm<GHI>(ahead);
+                else wait_vm<GLO>(ahead);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                if (st + NB - 1 < NSTEP) { AA_GLDS(st + NB - 1) }  // into the buffer slice st-1 was read from
+            }
+            const int o0 = choff(4 * st), o1 = choff(4 * st + 1), o2 = choff(4 * st + 2), o3 = choff(4 * st + 3);
+            // A fragments three deep (fragment i+2 in flight under fragment
+            // i's MFMAs), the next step's B fragments issued after the first
+            // two A reads so the first MFMAs do not wait behind them (LDS
+            // reads retire in order)
+            i32x8 a3[3];
+            auto rda = [&](int i, int k) {
+                if ((DIAG & 128) && st > 0) return;
+                const char* a = pb + abase[i];
+                rd4(a3[k], a + o0, a + o1, a + o2, a + o3);
+            };
+            rda(0, 0);
+            if (MF > 1) rda(1, 1);
+            if (st + 1 < NSTEP && !((DIAG & 128) && st > 0)) read_b8(bn, st + 1);
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                if (i + 2 < MF) rda(i + 2, (i + 2) % 3);
+#pragma unroll
+                for (int j = 0; j < NF; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bc[j], a3[i % 3], acc[i][j], 0, 0, 0, 0,
+                                                                                 0, 0);
+            }
+        };
+        i32x8 B0[NF], B1[NF];
+        {  // slice 0: own share landed (later slices stay in flight), one barrier publishes it
+            const int ahead = min(NB - 2, NSTEP - 1);
+            if (hi_share) wait_vm_lgkm<GHI>(ahead);
+            else wait_vm_lgkm<GLO>(ahead);
+            __builtin_amdgcn_s_barrier();
+            read_b8(B0, 0);
+        }
+        for (int st = 0; st < NSTEP; st += 2) {
+            f8step(B0, B1, st);
+            if (st + 1 < NSTEP) f8step(B1, B0, st + 1);
+        }
+    } else {
     if constexpr (DB) AA_LOAD_A(fa, 0, 0)
     for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); ++t) {
         // slices t+1 .. min(t+NB-2, NTAP-1) may stay in flight
@@ -645,6 +763,7 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
             }
         }
     }
+    }  // !F8
 #undef AA_LOAD_A
 #undef AA_LOAD_B
 #undef AA_GLDS
@@ -986,6 +1105,7 @@ struct Stage {
     int skipped = 0;    // first layer computed inside the next stage
     int is_first = 0;   // reads the model input (f32 log-mel)
     int fused_first = 0;  // this stage computes the previous (first) layer itself
+    int lm_f16 = 0;       // fused_first: the model input is float16
 };
 
 struct Model {
@@ -999,17 +1119,17 @@ struct Model {
 
 
 template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW,
-          bool FUSED = false, bool EBF16 = false, bool APF = true>
+          bool FUSED = false, bool EBF16 = false, int OCC = 0>
 static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStream_t st,
                        const Stage* first = nullptr) {
-    auto k = conv_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, EBF16, APF>;
+    auto k = conv_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, EBF16, OCC>;
     constexpr int BN = WN * NF * 16;
     const size_t lds = conv_lds_bytes<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>();
     FirstConv fc{};
     if (FUSED) {
         const float slope = first->act == ACT_LEAKY ? first->alpha : first->act == ACT_RELU ? 0.f : 1.f;
         fc = FirstConv{(const float*)first->d_w, first->d_b, first->act, slope, first->has_mag,
-                       first->mag_exp, first->Hin, first->Win};
+                       first->mag_exp, first->Hin, first->Win, s.lm_f16};
     }
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
     static size_t attr = 0;
@@ -1034,21 +1154,21 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
 // output channels per block.  The f32 rows are the parity mode (smaller
 // tiles: the same LDS budget holds half the elements).
 #define AA_CONV_CFGS(X)                                     \
-    X(bf16, 3, 3, 32, 3, 4, 1, 6, 2, 18, 21, true)          \
-    X(bf16, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true)           \
-    X(bf16, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)           \
-    X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true)           \
-    X(bf16, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)         \
-    X(fp8, 3, 3, 32, 3, 4, 1, 6, 2, 12, 30, true)           \
-    X(fp8, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true)            \
-    X(fp8, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)            \
-    X(fp8, 9, 3, 64, 3, 2, 4, 11, 2, 39, 9, true)           \
-    X(fp8, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)          \
-    X(float, 3, 3, 32, 3, 2, 2, 9, 1, 6, 48, false)         \
-    X(float, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false)         \
-    X(float, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false)         \
-    X(float, 9, 3, 64, 3, 1, 4, 7, 1, 3, 33, false)         \
-    X(float, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false)
+    X(bf16, 3, 3, 32, 3, 4, 1, 6, 2, 18, 21, true, 0)          \
+    X(bf16, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true, 0)           \
+    X(bf16, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true, 0)           \
+    X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true, 0)           \
+    X(bf16, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false, 0)         \
+    X(fp8, 3, 3, 32, 3, 4, 1, 6, 2, 12, 30, true, 0)           \
+    X(fp8, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true, 0)            \
+    X(fp8, 3, 3, 64, 1, 4, 1, 3, 4, 12, 16, true, 0)           \
+    X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 21, 18, true, 0)           \
+    X(fp8, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false, 0)          \
+    X(float, 3, 3, 32, 3, 2, 2, 9, 1, 6, 48, false, 0)         \
+    X(float, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false, 0)         \
+    X(float, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false, 0)         \
+    X(float, 9, 3, 64, 3, 1, 4, 7, 1, 3, 33, false, 0)         \
+    X(float, 1, 3, 128, 1, 2, 2, 5, 1, 6, 24, false, 0)
 
 // conv_x3 (split-bf16) instantiations: (kernel, C_in, pool) -> waves (WM x
 // WN), fragments per wave (MF x NF), output tile TH x TW, weight ring in LDS
@@ -1071,7 +1191,7 @@ static size_t prec_bytes(int prec) { return prec == AA_PREC_FP8 ? 1 : prec == AA
 
 // output channels per block of the instantiation serving this stage (0: none)
 static int mfma_bn(int prec, int kh, int kw, int cin, int pool) {
-#define AA_BN(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB)                                       \
+#define AA_BN(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB, OCC)                                       \
     if (prec_of<T_>() == prec && kh == KH && kw == KW && cin == CIN && pool == POOL) \
         return WN * NF * 16;
     AA_CONV_CFGS(AA_BN)
@@ -1093,7 +1213,7 @@ static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream
     if (FUSED) {
         const float slope = first->act == ACT_LEAKY ? first->alpha : first->act == ACT_RELU ? 0.f : 1.f;
         fc = FirstConv{(const float*)first->d_w, first->d_b, first->act, slope, first->has_mag,
-                       first->mag_exp, first->Hin, first->Win};
+                       first->mag_exp, first->Hin, first->Win, s.lm_f16};
     }
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
     static size_t attr = 0;
@@ -1185,15 +1305,15 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
         set_error("conv %dx%d cin %d pool %d: no split-bf16 kernel instantiation", s.kh, s.kw, s.cin, s.pool);
         return AA_ERR_UNSUPPORTED;
     }
-#define AA_LAUNCH(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB)                                        \
+#define AA_LAUNCH(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB, OCC)                                        \
     if constexpr (std::is_same<T, T_>::value) {                                                          \
         if (s.kh == KH && s.kw == KW && s.cin == CIN && s.pool == POOL) {                                \
             if (s.fused_first) {                                                                         \
                 if constexpr (CIN == 32 && KH == 3 && KW == 3)                                           \
-                    return launch_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, true, EB>(s, in, out, \
+                    return launch_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, true, EB, OCC>(s, in, out, \
                                                                                               n, st, first); \
             } else {                                                                                     \
-                return launch_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, false, EB>(s, in, out, n, st); \
+                return launch_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, false, EB, OCC>(s, in, out, n, st); \
             }                                                                                            \
         }                                                                                                \
     }
@@ -1467,21 +1587,36 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         bool ok = true;
         if (f8) {
             // per output channel: the largest |w| maps to 240 (e4m3fn tops
-            // out at 448), the kernel's epilogue multiplies by amax / 240
-            std::vector<uint8_t> h(wpk.size(), 0);
+            // out at 448), the kernel's epilogue multiplies by amax / 240.
+            // conv stages: super-steps of four 32-channel chunks (chunk k =
+            // tap k / (C_in/32), channels 32 (k % (C_in/32)) ..), each
+            // [cout_pad][F8_BSTR] with chunk k % 4 at byte 32 (k % 4) of the
+            // row (conv_mfma's K = 128 loop); the head keeps [cout_pad][cstr]
+            const bool ss = s.kind == ST_MFMA;
+            const int cpc = s.cin / 32, nch = ntap * cpc, nss = conv_nstep<fp8>(ntap, s.cin);
+            std::vector<uint8_t> h(ss ? (size_t)nss * s.cout_pad * F8_BSTR + 1024 : wpk.size(), 0);
             for (int o = 0; o < s.cout_pad; ++o) {
                 float amax = 0.f;
                 for (int t = 0; t < ntap; ++t)
                     for (int c = 0; c < s.cin; ++c) amax = std::max(amax, std::fabs(wpk[((size_t)t * s.cout_pad + o) * cstr + c]));
                 const float sc = amax > 0.f ? 240.f / amax : 1.f;
                 bias[s.cout_pad + o] = 1.f / sc;
-                for (int t = 0; t < ntap; ++t)
-                    for (int c = 0; c < s.cin; ++c) {
-                        const size_t k = ((size_t)t * s.cout_pad + o) * cstr + c;
-                        h[k] = f2fp8(wpk[k] * sc);
-                    }
+                if (ss) {
+                    for (int k = 0; k < nch; ++k)
+                        for (int c = 0; c < 32; ++c) {
+                            const int t = k / cpc, cc = k % cpc;
+                            h[((size_t)(k / 4) * s.cout_pad + o) * F8_BSTR + 32 * (k % 4) + c] =
+                                f2fp8(wpk[((size_t)t * s.cout_pad + o) * cstr + 32 * cc + c] * sc);
+                        }
+                } else {
+                    for (int t = 0; t < ntap; ++t)
+                        for (int c = 0; c < s.cin; ++c) {
+                            const size_t k = ((size_t)t * s.cout_pad + o) * cstr + c;
+                            h[k] = f2fp8(wpk[k] * sc);
+                        }
+                }
             }
-            ok = upload(s, h.data(), wbytes, bias);
+            ok = upload(s, h.data(), h.size(), bias);
         } else if (bf) {
             std::vector<uint16_t> h(wpk.size());
             for (size_t k = 0; k < wpk.size(); ++k) h[k] = f2bf(wpk[k]);
@@ -1583,7 +1718,17 @@ extern "C" size_t aa_model_workspace_bytes(const void* model, int32_t max_batch)
     return align_up(m->act_elems[0] * es * max_batch, 256) + align_up(m->act_elems[1] * es * max_batch, 256);
 }
 
-extern "C" int aa_model_forward(void* model, const float* x, int32_t n, float* logits, float* probs,
+extern "C" int aa_model_set_input_f16(void* model, int32_t f16) {
+    Model* m = static_cast<Model*>(model);
+    AA_CHECK(m && (f16 == 0 || f16 == 1), AA_ERR_INVALID, "aa_model_set_input_f16: bad argument");
+    AA_CHECK(!f16 || (m->st.size() >= 2 && m->st[1].fused_first), AA_ERR_UNSUPPORTED,
+             "aa_model_set_input_f16: float16 input needs the fused first conv (3x3 C_in=1 -> 32 before a "
+             "pooled 3x3/32 conv)");
+    if (m->st.size() >= 2) m->st[1].lm_f16 = f16;
+    return AA_OK;
+}
+
+extern "C" int aa_model_forward(void* model, const void* x, int32_t n, float* logits, float* probs,
                                 void* workspace, size_t workspace_bytes, void* stream) {
     Model* m = static_cast<Model*>(model);
     AA_CHECK(m && x && logits, AA_ERR_INVALID, "aa_model_forward: null argument");

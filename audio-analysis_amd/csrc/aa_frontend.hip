@@ -704,11 +704,13 @@ __device__ __forceinline__ float window_ref_db(const float* __restrict__ pmax, i
     return __fmul_rn(10.0f, log10f(fmaxf(amin, mx)));
 }
 
+// TO: float, or _Float16 for the fp16 log-mel of aa_fe_config.out_f16
+template <typename TO>
 __global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melF, const float* __restrict__ pmax,
                                              int nparts, const float4* __restrict__ stats,
                                              const float* __restrict__ band_mean, int n_mels, int T, int tile_t,
                                              int db_scale, float amin, float top_db, int channels, int normalize,
-                                             float* __restrict__ out, int* __restrict__ status) {
+                                             TO* __restrict__ out, int* __restrict__ status) {
     extern __shared__ float tile[];  // [tile_t][n_mels + 1]
     __shared__ float red[4];
     const int w = blockIdx.y;
@@ -751,8 +753,8 @@ __global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melF, con
         if (tt < nt) {
             float v = tile[tt * ld + m];
             if (band_mean) v -= band_mean[(size_t)w * n_mels + m];
-            float* o = out + (((size_t)w * n_mels + m) * T + t0 + tt) * channels;
-            for (int c = 0; c < channels; ++c) o[c] = v;
+            TO* o = out + (((size_t)w * n_mels + m) * T + t0 + tt) * channels;
+            for (int c = 0; c < channels; ++c) o[c] = (TO)v;
         }
     }
 }
@@ -875,7 +877,8 @@ extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** 
     const int n = cfg->n_fft;
     AA_CHECK(n == 2048 || n == 4096 || n == 8192, AA_ERR_UNSUPPORTED,
              "aa_fe_create: n_fft %d not supported (power of two 2048..8192)", n);
-    AA_CHECK(cfg->hop > 0 && cfg->win_len > 0 && cfg->n_mels > 0 && cfg->channels >= 1,
+    AA_CHECK(cfg->hop > 0 && cfg->win_len > 0 && cfg->n_mels > 0 && cfg->channels >= 1 &&
+                 (cfg->out_f16 == 0 || cfg->out_f16 == 1),
              AA_ERR_INVALID, "aa_fe_create: bad sizes");
     FePlan* p = new FePlan();
     p->cfg = *cfg;
@@ -983,7 +986,7 @@ extern "C" size_t aa_fe_workspace_bytes(const void* plan, int32_t max_windows) {
 }
 
 extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa_window* windows,
-                         int32_t n_win, float* out, int32_t* win_status, void* workspace,
+                         int32_t n_win, void* out, int32_t* win_status, void* workspace,
                          size_t workspace_bytes, void* stream) {
     FePlan* p = static_cast<FePlan*>(plan);
     AA_CHECK(p && pcm && windows && out, AA_ERR_INVALID, "aa_fe_run: null argument");
@@ -1025,10 +1028,17 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
     }
     int tile_t = 32;  // frames per fe_db block (the [tile_t][n_mels + 1] tile within 64 KiB)
     while (tile_t > 1 && (size_t)tile_t * (p->cfg.n_mels + 1) * 4 > 65536) tile_t >>= 1;
-    hipLaunchKernelGGL(fe_db, dim3((p->T + tile_t - 1) / tile_t, n_win), dim3(256),
-                       (size_t)tile_t * (p->cfg.n_mels + 1) * 4, st, ws.melS, ws.blkmax, p->nfblk, ws.stats,
-                       p->cfg.mean_sub ? ws.band_mean : nullptr, p->cfg.n_mels, p->T, tile_t, p->cfg.db_scale,
-                       p->cfg.amin, p->cfg.top_db, p->cfg.channels, p->cfg.normalize, out, win_status);
+    if (p->cfg.out_f16) {
+        hipLaunchKernelGGL(fe_db<_Float16>, dim3((p->T + tile_t - 1) / tile_t, n_win), dim3(256),
+                           (size_t)tile_t * (p->cfg.n_mels + 1) * 4, st, ws.melS, ws.blkmax, p->nfblk, ws.stats,
+                           p->cfg.mean_sub ? ws.band_mean : nullptr, p->cfg.n_mels, p->T, tile_t, p->cfg.db_scale,
+                           p->cfg.amin, p->cfg.top_db, p->cfg.channels, p->cfg.normalize, (_Float16*)out, win_status);
+    } else {
+        hipLaunchKernelGGL(fe_db<float>, dim3((p->T + tile_t - 1) / tile_t, n_win), dim3(256),
+                           (size_t)tile_t * (p->cfg.n_mels + 1) * 4, st, ws.melS, ws.blkmax, p->nfblk, ws.stats,
+                           p->cfg.mean_sub ? ws.band_mean : nullptr, p->cfg.n_mels, p->T, tile_t, p->cfg.db_scale,
+                           p->cfg.amin, p->cfg.top_db, p->cfg.channels, p->cfg.normalize, (float*)out, win_status);
+    }
     AA_LAUNCH_CHECK();
     return p->timer.end(FE_STAGE_DB, st, e0);
 }
@@ -1053,7 +1063,7 @@ extern "C" int aa_fe_stage_info(const void* plan, int32_t stage, char* name, int
             fl = T * (2.5 * N * std::log2(N) + N + 3 * (N / 2 + 1) + 2.0 * p->nnz) + 5 * L;
             by = 4 * L + 4 * M * T;
             break;
-        default: nm = "fe_db"; fl = 3 * M * T; by = 4 * M * T * (1 + p->cfg.channels); break;
+        default: nm = "fe_db"; fl = 3 * M * T; by = M * T * (4 + (p->cfg.out_f16 ? 2 : 4) * p->cfg.channels); break;
     }
     if (name && name_len > 0) snprintf(name, name_len, "%s", nm);
     if (flops_per_item) *flops_per_item = fl;

@@ -67,7 +67,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "f32", "bf16", "fp8"],
                     help="bf16x3: split-bf16 (gated, default); fp8: OCP e4m3fn CNN (BASELINE configs[4])")
-    ap.add_argument("--secondary", default="f32,bf16,fp8,cold",
+    ap.add_argument("--logmel", default="f32", choices=["f32", "f16"],
+                    help="log-mel dtype between the front end and the CNN (f16: BASELINE configs[4])")
+    ap.add_argument("--secondary", default="f32,bf16,fp8,fp8_f16mel,cold",
                     help="N=1 only: extra modes measured into the same line ('' disables)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bound on the CPU-baseline sample (0 disables)")
@@ -182,11 +184,12 @@ class Step:
     buffers of ``pairs`` resident clip pairs (1 = the headline; COLD_POOL =
     the cold-PCM variant, one pair per step in rotation)."""
 
-    def __init__(self, dev, rank, model_path, precision, pairs=1, first=None):
+    def __init__(self, dev, rank, model_path, precision, pairs=1, first=None, lm16=False):
         from aa_amd.frontend import FrontEnd
         from aa_amd.model import Model
         self.fe_s = fe_settings()
-        self.fe = FrontEnd(self.fe_s, dev)
+        lm_dtype = torch.float16 if lm16 else torch.float32  # configs[4]: fp16 log-mel
+        self.fe = FrontEnd(self.fe_s, dev, out_dtype=lm_dtype)
         self.model = Model(model_path, (self.fe_s.n_mels, self.fe.T, 1), precision=precision, device=dev)
         batches = [first] if first is not None else []
         for k in range(len(batches), pairs):
@@ -194,7 +197,7 @@ class Step:
         self.pcm = [torch.from_numpy(b[0]).to(dev) for b in batches]
         self.rows = [torch.from_numpy(b[1]).to(dev) for b in batches]
         self.n_win = batches[0][1].shape[0]
-        self.logmel = torch.empty(self.fe.out_shape(self.n_win), dtype=torch.float32, device=dev)
+        self.logmel = torch.empty(self.fe.out_shape(self.n_win), dtype=lm_dtype, device=dev)
         self.logits = torch.empty((self.n_win, self.model.n_labels), dtype=torch.float32, device=dev)
         self.probs = torch.empty_like(self.logits)
         self.wb = torch.tensor([0, BATCH_A], dtype=torch.int32, device=dev)
@@ -248,7 +251,7 @@ def main_step(args, world, rank, dev):
     model_path = make_model(Path(tmp) / "model1", "model1", seed=1)
     first = make_batch(rank, fe_settings())
     pcm_np, _, views = first
-    step = Step(dev, rank, model_path, args.precision, first=first)
+    step = Step(dev, rank, model_path, args.precision, first=first, lm16=args.logmel == "f16")
     fe, model, n_win = step.fe, step.model, step.n_win
 
     for _ in range(args.warmup):
@@ -310,7 +313,8 @@ def main_step(args, world, rank, dev):
         "metric": METRIC, "value": round(audio_s / elapsed, 1), "unit": "audio-s/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": args.precision + (" (fp16 log-mel)" if args.logmel == "f16" else ""),
         "data": "synthetic (48 kHz int16-quantised noise+chirps, seeded), seeded random-init model1",
         "config": {"workload": WORKLOAD, "model": "model1", "global_batch": n_win * world,
                    "seq_len": step.fe_s.win_len, "parallelism": f"dp{world}"},
@@ -330,14 +334,16 @@ def main_step(args, world, rank, dev):
                     gate_fail = f"{args.precision}: max|dlogit| {d:.3e} > {LOGIT_GATE}"
         sec = {}
         for mode in [m for m in args.secondary.split(",") if m]:
-            prec = args.precision if mode == "cold" else mode
+            # "fp8_f16mel": BASELINE configs[4] (fp16 log-mel + fp8 CNN)
+            prec = args.precision if mode == "cold" else mode.split("_")[0]
             if mode == args.precision:
                 continue
-            s2 = Step(dev, rank, model_path, prec, pairs=COLD_POOL if mode == "cold" else 1, first=first)
+            s2 = Step(dev, rank, model_path, prec, pairs=COLD_POOL if mode == "cold" else 1, first=first,
+                      lm16=mode.endswith("_f16mel") or (mode == "cold" and args.logmel == "f16"))
             el = timed(s2, max(10, args.steps // 2), 5, 1)
             n2 = max(10, args.steps // 2)
             e = {"value": round(n2 * s2.n_win * SECONDS_PER_WINDOW / el, 1), "ms_per_step": round(1e3 * el / n2, 4),
-                 "steps": n2, "dtype": prec}
+                 "steps": n2, "dtype": prec + (" (fp16 log-mel)" if s2.logmel.dtype == torch.float16 else "")}
             if mode == "cold":
                 e["note"] = f"fresh clip pair per step from {COLD_POOL} resident pairs (> Infinity Cache)"
             elif ref is not None:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 1
+#define AA_ABI_VERSION 2
 
 typedef enum aa_status {
     AA_OK = 0,
@@ -69,6 +69,8 @@ typedef struct aa_fe_config {
     float top_db;      /* power_to_db top_db (80) */
     int32_t mean_sub;  /* subtract each band's mean over time */
     int32_t channels;  /* repeat the single channel this many times */
+    int32_t out_f16;   /* 1: aa_fe_run writes float16 log-mel (BASELINE configs[4]),
+                        * 0: float32 (what get_spect returns) */
 } aa_fe_config;
 
 /* Per-window status flags written by aa_fe_run (device int32 array). */
@@ -86,11 +88,12 @@ int aa_fe_destroy(void* plan);
 /* frames per window T = 1 + win_len / hop */
 int aa_fe_n_frames(const void* plan);
 size_t aa_fe_workspace_bytes(const void* plan, int32_t max_windows);
-/* out: device float32 [n_win][n_mels][T][channels] (NHWC, H = mel band,
- * W = frame), the tensor get_spect returns per window.
+/* out: device [n_win][n_mels][T][channels] (NHWC, H = mel band, W = frame),
+ * the tensor get_spect returns per window: float32, or float16 (round to
+ * nearest) when cfg.out_f16.
  * win_status: device int32 [n_win] (AA_WIN_*), may be NULL. */
 int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa_window* windows,
-              int32_t n_win, float* out, int32_t* win_status, void* workspace,
+              int32_t n_win, void* out, int32_t* win_status, void* workspace,
               size_t workspace_bytes, void* stream);
 /* Launch stages of aa_fe_run (0 fe_stats, 1 fe_stft_mel, 2 fe_db) and their
  * timing, same contract as aa_model_stage_* below. */
@@ -150,10 +153,16 @@ int aa_model_create(const aa_layer* layers, int32_t n_layers, const float* blob,
 int aa_model_destroy(void* model);
 int aa_model_n_outputs(const void* model);
 size_t aa_model_workspace_bytes(const void* model, int32_t max_batch);
-/* x: device float32 [n][in_h][in_w][in_c]; logits: device float32 [n][L]
+/* x: device [n][in_h][in_w][in_c], float32 (or float16 after
+ * aa_model_set_input_f16(model, 1)); logits: device float32 [n][L]
  * (global-max outputs before the sigmoid); probs: [n][L] or NULL. */
-int aa_model_forward(void* model, const float* x, int32_t n, float* logits, float* probs,
+int aa_model_forward(void* model, const void* x, int32_t n, float* logits, float* probs,
                      void* workspace, size_t workspace_bytes, void* stream);
+/* Model input as float16 (aa_fe_config.out_f16): served when the first
+ * conv is fused into the second (the build's model family: 3x3 C_in = 1 ->
+ * 32 before a pooled 3x3/32 conv), which converts the log-mel to f32 as it
+ * stages it; AA_ERR_UNSUPPORTED otherwise. */
+int aa_model_set_input_f16(void* model, int32_t f16);
 
 /* Per-stage timing of aa_model_forward (HIP events around each stage whose
  * bit is set in stage_mask, on the launch stream; 0 disables).  Used by

@@ -29,7 +29,7 @@ def test_abi_version_and_struct_sizes():
     assert _lib.lib().aa_abi_version() == _lib.ABI_VERSION
     assert C.sizeof(_lib.Window) == 16
     assert C.sizeof(_lib.Layer) == 6 * 4 + 4 * 8
-    assert C.sizeof(_lib.FeConfig) == 11 * 4
+    assert C.sizeof(_lib.FeConfig) == 12 * 4
     assert C.sizeof(_lib.SnConfig) == 32 and C.sizeof(_lib.SnComponent) == 24
 
 

@@ -56,3 +56,89 @@ def test_config1_logits(step, gpu, precision):
     print(f"configs[1] {precision}: max|dlogit| = {d.max():.3e} (mean {d.mean():.3e})")
     assert np.isfinite(d).all()
     assert d.max() <= LOOSE.get(precision, LOGIT_TOL)
+
+
+# ---- BASELINE configs[4]: fp16 log-mel + fp8 CNN (throughput-ceiling mode) ----
+
+def test_config4_logmel_f16_is_rounded_f32(step, gpu):
+    """aa_fe_config.out_f16: fe_db rounds the same f32 dB values to float16
+    (round to nearest), so the fp16 log-mel is bit-identical to the f32 one
+    cast to half."""
+    import bench
+    from aa_amd.frontend import FeSettings, FrontEnd
+    fe_s = FeSettings(htk=True, hop_length=640, n_fft=4096, n_mels=160, break_freq=1750)
+    pcm_np, rows_np, _ = bench.make_batch(0, fe_s)
+    fe16 = FrontEnd(fe_s, gpu, out_dtype=torch.float16)
+    lm16 = fe16.run(torch.from_numpy(pcm_np).to(gpu), torch.from_numpy(rows_np).to(gpu))
+    torch.cuda.synchronize()
+    assert lm16.dtype == torch.float16
+    assert torch.equal(lm16, step["logmel"].half())
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp8"])
+def test_config4_f16_input_equals_f32_of_same_values(step, gpu, precision):
+    """A float16 model input is widened to f32 exactly where the fused first
+    conv stages it: logits equal those of the f32 tensor holding the same
+    (half-rounded) values, bit for bit."""
+    from aa_amd.model import Model
+    lm16 = step["logmel"].half()
+    m = Model(step["path"], lm16.shape[1:], precision=precision, device=gpu)
+    a, _ = m.forward(lm16)
+    b, _ = m.forward(lm16.float())
+    c, _ = m.forward(lm16)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(a, c)
+
+
+def test_config4_step(step, gpu):
+    """configs[4]'s step: fp16 log-mel -> fp8 CNN.  Against the fp8 CPU
+    emulation fed the same half-rounded log-mel (gate: the fp8 bounds of
+    test_gpu_cnn.py), and the delta to the fp32 oracle reported."""
+    from aa_amd.model import Model
+    from oracle import cnn_oracle
+    from tests.test_gpu_cnn import FP8_EMU_MAX, FP8_EMU_MEAN
+    lm16 = step["logmel"].half()
+    m = Model(step["path"], lm16.shape[1:], precision="fp8", device=gpu)
+    lg, _ = m.forward(lm16)
+    torch.cuda.synchronize()
+    lg = lg.cpu().numpy()
+    elg, _ = cnn_oracle.forward_fp8_emulated(step["path"], lm16.float().cpu().numpy())
+    d_emu = np.abs(lg - elg)
+    d_ref = np.abs(lg - step["ref_logits"])
+    print(f"configs[4] fp16 log-mel + fp8: max|dlogit| vs emulation {d_emu.max():.3e} (mean {d_emu.mean():.3e}), "
+          f"vs fp32 oracle {d_ref.max():.3e} (mean {d_ref.mean():.3e})")
+    assert np.isfinite(lg).all()
+    assert d_emu.max() <= FP8_EMU_MAX and d_emu.mean() <= FP8_EMU_MEAN
+    assert d_ref.max() <= LOOSE["fp8"]
+
+
+def test_f16_input_needs_fused_first_conv(gpu, tmp_path):
+    """Only the fused first conv reads a float16 input: another first layer
+    refuses it (AA_ERR_UNSUPPORTED) instead of misreading the buffer."""
+    from aa_amd import _lib
+    from aa_amd.model import Model
+    from tools.make_models import make_model
+    path = make_model(tmp_path / "m2", "model2", seed=2)  # C_in = 1 first conv, then a pooled 3x3/32: fused
+    Model(path, (160, 226, 1), precision="fp8", device=gpu).forward(torch.zeros(1, 160, 226, 1, dtype=torch.float16,
+                                                                             device=gpu))
+    import json
+    from safetensors.numpy import load_file, save_file
+    from safetensors import safe_open
+    with safe_open(str(path), "np") as f:
+        meta = f.metadata()
+    arch = json.loads(meta["arch"])
+    # drop the fusing pattern: make the second conv unpooled
+    for i, ly in enumerate(arch):
+        if ly["type"] == "maxpool2d":
+            del arch[i]
+            break
+    meta["arch"] = json.dumps(arch)
+    p2 = tmp_path / "m3" / "audioModel.safetensors"
+    p2.parent.mkdir()
+    save_file(load_file(str(path)), str(p2), metadata=meta)
+    for fn in ("metadata.txt",):
+        if (path.parent / fn).exists():
+            (p2.parent / fn).write_text((path.parent / fn).read_text())
+    m = Model(p2, (160, 226, 1), precision="bf16x3", device=gpu)
+    with pytest.raises(_lib.AAError):
+        m.forward(torch.zeros(1, 160, 226, 1, dtype=torch.float16, device=gpu))

@@ -11,10 +11,10 @@
 using namespace aa;
 
 template <typename T, int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int DIAG,
-          bool EBF16 = false, bool APF = true, bool FUSED = false>
+          bool EBF16 = false, int OCC = 0, bool FUSED = false>
 static float time_one(int n, int Hin, int Win, int cout, void* in, void* w, float* b, void* out, FirstConv fc,
                       int iters) {
-    auto k = conv_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, DIAG, EBF16, APF>;
+    auto k = conv_mfma<T, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, DIAG, EBF16, OCC>;
     constexpr int BN = WN * NF * 16;
     const size_t lds = conv_lds_bytes<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>();
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -66,17 +66,17 @@ int main(int argc, char** argv) {
         else if (kh == 9) { H = 48; W = 70; C = 128; }
         else { H = 13; W = 22; C = 256; }
     };
-#define AA_BENCH(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB)                                         \
+#define AA_BENCH(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB, OCC)                                         \
     {                                                                                                     \
         int H, W, C;                                                                                      \
         dims(KH, KW, CIN, POOL, H, W, C);                                                                 \
-        const float full = time_one<T_, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, 0, EB>(n, H, W, C, in, w, b, \
+        const float full = time_one<T_, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, 0, EB, OCC>(n, H, W, C, in, w, b, \
                                                                                           out, fc, it);   \
-        const float mf = pmc ? 0.f : time_one<T_, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, 5, EB>(n, H, W, C, in, w, b, \
+        const float mf = pmc ? 0.f : time_one<T_, KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, 5, EB, OCC>(n, H, W, C, in, w, b, \
                                                                                         out, fc, it);     \
         const double fl = 2.0 * n * (H - KH + 1) * (W - KW + 1) * KH * KW * CIN * C;                      \
-        printf("%-6s %dx%d cin %3d pool %d  WM%d WN%d MF%d NF%d %2dx%2d  full %7.1f us (%6.1f TF)  only-mfma %7.1f us\n", \
-               sizeof(T_) == 1 ? "fp8" : sizeof(T_) == 2 ? "bf16" : "f32", KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, full,        \
+        printf("%-6s %dx%d cin %3d pool %d  WM%d WN%d MF%d NF%d %2dx%2d occ%d  full %7.1f us (%6.1f TF)  only-mfma %7.1f us\n", \
+               sizeof(T_) == 1 ? "fp8" : sizeof(T_) == 2 ? "bf16" : "f32", KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, full,        \
                fl / full * 1e-6, mf);                                                                     \
     }
     if (fp8mode) {
@@ -84,33 +84,42 @@ int main(int argc, char** argv) {
         (void)hipMemcpy(in, h.data(), h.size() * 2, hipMemcpyHostToDevice);
         (void)hipMemcpy(w, h.data(), 8u << 20, hipMemcpyHostToDevice);
         (void)hipMemset(b, 0, 4096);
-#define AA_TRY8(X)                                        \
-        X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true)      \
-        X(fp8, 9, 3, 64, 3, 4, 2, 7, 4, 12, 33, true)     \
-        X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 21, 18, true)     \
-        X(fp8, 9, 3, 64, 3, 4, 2, 5, 4, 15, 21, true)     \
-        X(fp8, 9, 3, 64, 3, 4, 2, 8, 4, 51, 9, true)      \
-        X(fp8, 9, 3, 64, 3, 2, 4, 12, 2, 39, 9, true)     \
-        X(fp8, 9, 3, 64, 3, 2, 4, 12, 2, 21, 18, true)    \
-        X(fp8, 9, 3, 64, 3, 2, 4, 12, 2, 42, 9, true)     \
-        X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 42, 9, true)      \
-        X(fp8, 9, 3, 64, 3, 2, 4, 11, 2, 39, 9, true)     \
-        X(bf16, 9, 3, 64, 3, 2, 4, 11, 2, 39, 9, true)    \
-        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 42, 9, true)     \
-        X(bf16, 9, 3, 64, 3, 2, 4, 12, 2, 21, 18, true)   \
-        X(bf16, 9, 3, 64, 3, 2, 4, 12, 2, 39, 9, true)    \
-        X(fp8, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true)      \
-        X(fp8, 3, 3, 32, 1, 2, 2, 6, 2, 10, 18, true)     \
-        X(fp8, 3, 3, 32, 1, 4, 2, 6, 2, 10, 36, true)     \
-        X(fp8, 3, 3, 32, 1, 2, 2, 8, 2, 10, 24, true)     \
-        X(fp8, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)      \
-        X(fp8, 3, 3, 64, 1, 2, 2, 6, 2, 10, 18, true)     \
-        X(fp8, 3, 3, 64, 1, 4, 2, 6, 2, 10, 36, true)     \
-        X(fp8, 3, 3, 64, 1, 2, 2, 8, 2, 10, 24, true)     \
-        X(fp8, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)    \
-        X(fp8, 1, 3, 128, 1, 1, 4, 5, 2, 4, 20, false)    \
-        X(fp8, 1, 3, 128, 1, 2, 2, 9, 2, 13, 20, true)
+#define AA_TRY8(X)                                           \
+        X(fp8, 9, 3, 64, 3, 2, 4, 11, 2, 39, 9, true, 0)     \
+        X(fp8, 9, 3, 64, 3, 2, 4, 11, 2, 39, 9, true, 1)     \
+        X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true, 0)      \
+        X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true, 2)      \
+        X(fp8, 9, 3, 64, 3, 4, 2, 4, 4, 39, 6, true, 0)      \
+        X(fp8, 9, 3, 64, 3, 4, 2, 4, 4, 39, 6, true, 2)      \
+        X(fp8, 9, 3, 64, 3, 2, 4, 8, 2, 39, 6, true, 0)      \
+        X(fp8, 9, 3, 64, 3, 2, 2, 8, 4, 39, 6, true, 0)      \
+        X(fp8, 9, 3, 64, 3, 2, 2, 8, 4, 39, 6, true, 1)      \
+        X(fp8, 9, 3, 64, 3, 4, 1, 4, 8, 39, 6, true, 0)      \
+        X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 21, 18, true, 0)     \
+        X(fp8, 9, 3, 64, 3, 4, 2, 8, 4, 51, 9, true, 0)      \
+        X(fp8, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true, 0)      \
+        X(fp8, 3, 3, 32, 1, 2, 2, 6, 2, 10, 18, true, 0)     \
+        X(fp8, 3, 3, 32, 1, 4, 1, 3, 4, 12, 16, true, 0)     \
+        X(fp8, 3, 3, 32, 1, 4, 2, 6, 2, 10, 36, true, 0)     \
+        X(fp8, 3, 3, 32, 1, 2, 2, 8, 2, 10, 24, true, 0)     \
+        X(fp8, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true, 0)      \
+        X(fp8, 3, 3, 64, 1, 2, 2, 6, 2, 10, 18, true, 0)     \
+        X(fp8, 3, 3, 64, 1, 4, 1, 3, 4, 12, 16, true, 0)     \
+        X(fp8, 3, 3, 64, 1, 4, 2, 6, 2, 10, 36, true, 0)     \
+        X(fp8, 3, 3, 64, 1, 2, 2, 8, 2, 10, 24, true, 0)     \
+        X(fp8, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false, 0)    \
+        X(fp8, 1, 3, 128, 1, 1, 4, 5, 2, 4, 20, false, 0)    \
+        X(fp8, 1, 3, 128, 1, 2, 2, 9, 2, 13, 20, true, 0)    \
+        X(fp8, 1, 3, 128, 1, 4, 1, 5, 4, 13, 20, true, 0)
         AA_TRY8(AA_BENCH)
+        {  // ablations of the K = 128 loop: 32 no barriers / weight stream, 128 no fragment reads
+            int H, W, C;
+            dims(9, 3, 64, 3, H, W, C);
+#define AA_D8(D) printf("fp8 9x3 39x9 MF6 NF4 DIAG %3d: %7.1f us\n", D, \
+                        time_one<fp8, 9, 3, 64, 4, 2, 6, 4, 3, 39, 9, D, true, 2>(n, H, W, C, in, w, b, out, fc, it));
+            AA_D8(0) AA_D8(1) AA_D8(5) AA_D8(32) AA_D8(128) AA_D8(160) AA_D8(165)
+#undef AA_D8
+        }
 #undef AA_TRY8
         float* w1;
         float* b1;
@@ -121,71 +130,56 @@ int main(int argc, char** argv) {
         (void)hipMemcpy(b1, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
         FirstConv f1{w1, b1, 1, 0.3f, 0, 1.f, 160, 226};
         const int H = 158, W = 224;
-#define AA_FT8(MF, TH, TW)                                                                                 \
-    printf("fp8 fused c1+c2 MF%2d %2dx%2d: %7.1f us\n", MF, TH, TW,                                        \
-           time_one<fp8, 3, 3, 32, 4, 1, MF, 2, 3, TH, TW, 0, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
-        AA_FT8(9, 12, 48) AA_FT8(7, 9, 48) AA_FT8(6, 9, 42) AA_FT8(8, 9, 54) AA_FT8(5, 6, 51) AA_FT8(8, 12, 42)
-        AA_FT8(6, 6, 63) AA_FT8(7, 6, 72) AA_FT8(7, 12, 36) AA_FT8(9, 15, 36) AA_FT8(10, 15, 42) AA_FT8(8, 15, 33)
-        AA_FT8(6, 12, 30) AA_FT8(8, 12, 39) AA_FT8(5, 12, 24) AA_FT8(4, 12, 18) AA_FT8(5, 9, 33) AA_FT8(6, 9, 39)
-        AA_FT8(6, 15, 24) AA_FT8(5, 15, 21) AA_FT8(6, 18, 21) AA_FT8(6, 21, 18) AA_FT8(7, 24, 18) AA_FT8(5, 21, 15)
-        AA_FT8(6, 24, 15) AA_FT8(7, 27, 15) AA_FT8(7, 36, 12) AA_FT8(7, 39, 9) AA_FT8(5, 24, 12) AA_FT8(4, 18, 12)
+#define AA_FT8(MF, TH, TW, OCC)                                                                            \
+    printf("fp8 fused c1+c2 MF%2d %2dx%2d occ%d: %7.1f us\n", MF, TH, TW, OCC,                              \
+           time_one<fp8, 3, 3, 32, 4, 1, MF, 2, 3, TH, TW, 0, true, OCC, true>(n, H, W, 32, in, w, b, out, f1, it));
+        AA_FT8(6, 12, 30, 0) AA_FT8(6, 12, 30, 2) AA_FT8(6, 12, 30, 3) AA_FT8(9, 12, 48, 2) AA_FT8(7, 9, 48, 2)
+        AA_FT8(5, 12, 24, 0) AA_FT8(5, 12, 24, 3) AA_FT8(4, 12, 18, 0) AA_FT8(6, 18, 21, 2) AA_FT8(6, 18, 21, 3)
+        AA_FT8(6, 21, 18, 2) AA_FT8(5, 15, 21, 0) AA_FT8(5, 15, 21, 3) AA_FT8(7, 36, 12, 2) AA_FT8(7, 39, 9, 2)
+        AA_FT8(5, 24, 12, 3) AA_FT8(4, 18, 12, 0) AA_FT8(3, 6, 24, 0) AA_FT8(8, 15, 33, 2) AA_FT8(8, 12, 39, 2)
 #undef AA_FT8
-        // the same fused candidates in bf16 (the LDS image is larger there)
-        for (auto& x : h) x = 0x3c00 + (rand() & 0x3ff);
-        (void)hipMemcpy(in, h.data(), h.size() * 2, hipMemcpyHostToDevice);
-        (void)hipMemcpy(w, h.data(), 8u << 20, hipMemcpyHostToDevice);
-#define AA_FTB(MF, TH, TW)                                                                                 \
-    printf("bf16 fused c1+c2 MF%2d %2dx%2d: %7.1f us\n", MF, TH, TW,                                       \
-           time_one<bf16, 3, 3, 32, 4, 1, MF, 2, 3, TH, TW, 0, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
-        AA_FTB(9, 12, 48) AA_FTB(7, 9, 48) AA_FTB(6, 9, 42) AA_FTB(8, 9, 54) AA_FTB(5, 6, 51) AA_FTB(8, 12, 42)
-        AA_FTB(6, 6, 63) AA_FTB(7, 6, 72) AA_FTB(6, 12, 30) AA_FTB(8, 12, 39) AA_FTB(8, 15, 33) AA_FTB(7, 12, 36)
-        AA_FTB(5, 12, 24) AA_FTB(4, 12, 18) AA_FTB(5, 15, 21) AA_FTB(5, 9, 33) AA_FTB(4, 9, 24) AA_FTB(3, 6, 24)
-        AA_FTB(6, 18, 21) AA_FTB(6, 21, 18) AA_FTB(7, 24, 18) AA_FTB(6, 18, 18) AA_FTB(8, 24, 21) AA_FTB(4, 18, 12)
-        AA_FTB(5, 21, 15) AA_FTB(6, 24, 15) AA_FTB(7, 27, 15) AA_FTB(6, 30, 12) AA_FTB(7, 36, 12) AA_FTB(7, 39, 9)
-        AA_FTB(5, 39, 6) AA_FTB(8, 39, 12) AA_FTB(5, 24, 12)
-#undef AA_FTB
         printf("last error: %s\n", hipGetErrorString(hipGetLastError()));
         return 0;
     }
     AA_CONV_CFGS(AA_BENCH)
     if (!pmc && argc == 1) {  // candidate tilings of the 9x3 layer
 #define AA_TRY(X)                                          \
-        X(bf16, 9, 3, 64, 3, 4, 2, 7, 4, 12, 33, true)     \
-        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 15, 24, true)     \
-        X(bf16, 9, 3, 64, 3, 4, 2, 4, 4, 6, 33, true)      \
-        X(bf16, 9, 3, 64, 3, 4, 1, 5, 8, 9, 33, true)      \
-        X(bf16, 9, 3, 64, 3, 2, 2, 10, 4, 9, 33, true)     \
-        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true)      \
-        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 21, 18, true)     \
-        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 18, 21, true)     \
-        X(bf16, 9, 3, 64, 3, 4, 2, 5, 4, 15, 21, true)
+        X(bf16, 9, 3, 64, 3, 4, 2, 7, 4, 12, 33, true, 0)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 15, 24, true, 0)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 4, 4, 6, 33, true, 0)      \
+        X(bf16, 9, 3, 64, 3, 4, 1, 5, 8, 9, 33, true, 0)      \
+        X(bf16, 9, 3, 64, 3, 2, 2, 10, 4, 9, 33, true, 0)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 39, 9, true, 0)      \
+        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 21, 18, true, 0)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 6, 4, 18, 21, true, 0)     \
+        X(bf16, 9, 3, 64, 3, 4, 2, 5, 4, 15, 21, true, 0)
         AA_TRY(AA_BENCH)
 #undef AA_TRY
         // candidate tilings of the small-K layers (c3: 3x3 32->64, c4: 3x3
         // 64->64, c6: 1x3 128->256)
 #define AA_TRY2(X)                                         \
-        X(bf16, 3, 3, 32, 1, 4, 1, 2, 4, 8, 16, true)      \
-        X(bf16, 3, 3, 32, 1, 8, 1, 2, 4, 8, 32, true)      \
-        X(bf16, 3, 3, 32, 1, 4, 2, 4, 2, 8, 32, true)      \
-        X(bf16, 3, 3, 32, 1, 4, 1, 6, 4, 12, 32, true)     \
-        X(bf16, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true)      \
-        X(bf16, 3, 3, 64, 1, 4, 1, 2, 4, 8, 16, true)      \
-        X(bf16, 3, 3, 64, 1, 8, 1, 2, 4, 8, 32, true)      \
-        X(bf16, 3, 3, 64, 1, 4, 2, 4, 2, 8, 32, true)      \
-        X(bf16, 3, 3, 64, 1, 4, 1, 6, 4, 12, 32, true)     \
-        X(bf16, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true)      \
-        X(bf16, 3, 3, 64, 1, 4, 1, 3, 4, 6, 32, true)      \
-        X(bf16, 3, 3, 32, 1, 2, 2, 6, 2, 10, 18, true)     \
-        X(bf16, 3, 3, 64, 1, 2, 2, 6, 2, 10, 18, true)     \
-        X(bf16, 3, 3, 32, 1, 2, 2, 8, 2, 10, 24, true)     \
-        X(bf16, 3, 3, 64, 1, 2, 2, 8, 2, 10, 24, true)     \
-        X(bf16, 3, 3, 32, 1, 4, 2, 6, 2, 10, 36, true)     \
-        X(bf16, 3, 3, 64, 1, 4, 2, 6, 2, 10, 36, true)     \
-        X(bf16, 3, 3, 64, 1, 2, 2, 6, 2, 25, 6, true)      \
-        X(bf16, 1, 3, 128, 1, 1, 4, 9, 2, 6, 24, true)     \
-        X(bf16, 1, 3, 128, 1, 2, 2, 9, 2, 13, 20, true)    \
-        X(bf16, 1, 3, 128, 1, 1, 4, 5, 2, 4, 20, false)    \
-        X(bf16, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false)
+        X(bf16, 3, 3, 32, 1, 4, 1, 2, 4, 8, 16, true, 0)      \
+        X(bf16, 3, 3, 32, 1, 8, 1, 2, 4, 8, 32, true, 0)      \
+        X(bf16, 3, 3, 32, 1, 4, 2, 4, 2, 8, 32, true, 0)      \
+        X(bf16, 3, 3, 32, 1, 4, 1, 6, 4, 12, 32, true, 0)     \
+        X(bf16, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true, 0)      \
+        X(bf16, 3, 3, 64, 1, 4, 1, 2, 4, 8, 16, true, 0)      \
+        X(bf16, 3, 3, 64, 1, 8, 1, 2, 4, 8, 32, true, 0)      \
+        X(bf16, 3, 3, 64, 1, 4, 2, 4, 2, 8, 32, true, 0)      \
+        X(bf16, 3, 3, 64, 1, 4, 1, 6, 4, 12, 32, true, 0)     \
+        X(bf16, 3, 3, 64, 1, 2, 2, 4, 2, 8, 16, true, 0)      \
+        X(bf16, 3, 3, 64, 1, 4, 1, 3, 4, 6, 32, true, 0)      \
+        X(bf16, 3, 3, 32, 1, 2, 2, 6, 2, 10, 18, true, 0)     \
+        X(bf16, 3, 3, 64, 1, 2, 2, 6, 2, 10, 18, true, 0)     \
+        X(bf16, 3, 3, 32, 1, 2, 2, 8, 2, 10, 24, true, 0)     \
+        X(bf16, 3, 3, 64, 1, 2, 2, 8, 2, 10, 24, true, 0)     \
+        X(bf16, 3, 3, 32, 1, 4, 2, 6, 2, 10, 36, true, 0)     \
+        X(bf16, 3, 3, 64, 1, 4, 2, 6, 2, 10, 36, true, 0)     \
+        X(bf16, 3, 3, 64, 1, 2, 2, 6, 2, 25, 6, true, 0)      \
+        X(bf16, 1, 3, 128, 1, 1, 4, 9, 2, 6, 24, true, 0)     \
+        X(bf16, 1, 3, 128, 1, 2, 2, 9, 2, 13, 20, true, 0)    \
+        X(bf16, 1, 3, 128, 1, 1, 4, 5, 2, 4, 20, false, 0)    \
+        X(bf16, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false, 0)
         AA_TRY2(AA_BENCH)
 #undef AA_TRY2
         {  // the 3x3/32 layer with the weight ring instead of register-resident weights
@@ -217,7 +211,7 @@ int main(int argc, char** argv) {
 #undef AA_FUSED
 #define AA_FT(MF, TH, TW)                                                                                  \
     printf("fused c1+c2 MF%2d %2dx%2d: %7.1f us\n", MF, TH, TW,                                            \
-           time_one<bf16, 3, 3, 32, 4, 1, MF, 2, 3, TH, TW, 0, true, true, true>(n, H, W, 32, in, w, b, out, f1, it));
+           time_one<bf16, 3, 3, 32, 4, 1, MF, 2, 3, TH, TW, 0, true, 0, true>(n, H, W, 32, in, w, b, out, f1, it));
         AA_FT(9, 12, 45) AA_FT(6, 6, 60) AA_FT(9, 9, 60) AA_FT(7, 9, 48) AA_FT(5, 6, 48) AA_FT(11, 12, 57)
 #undef AA_FT
     }
