@@ -218,14 +218,21 @@ __host__ __device__ constexpr size_t conv_b_offset() {
 // loop walks "super-steps" of four 32-deep chunks (chunk k = tap * C_in/32 +
 // channel chunk), and its weights are packed per super-step as rows of
 // 4 x 32 B (+16 B pad) instead of per tap.
+// C_in = 32 layers keep the non-scaled K = 32 form: 9 taps are 9 chunks, and
+// packed into K = 128 they would waste a quarter of the MFMA work (measured
+// in the pipeline: fused first conv 64 -> 75 us, 3x3/32 19 -> 22 us).
 constexpr int F8_BSTR = 144;  // bytes of one packed fp8 weight row (128 + pad)
 template <typename T>
+__host__ __device__ constexpr bool conv_k128(int cin) {
+    return is_fp8<T>() && cin >= 64;
+}
+template <typename T>
 __host__ __device__ constexpr int conv_bstr(int cin) {  // weight-row stride (elements) of one step's slice
-    return is_fp8<T>() ? F8_BSTR : conv_cstr<T>(cin);
+    return conv_k128<T>(cin) ? F8_BSTR : conv_cstr<T>(cin);
 }
 template <typename T>
 __host__ __device__ constexpr int conv_nstep(int ntap, int cin) {  // K-loop steps (= weight slices)
-    return is_fp8<T>() ? (ntap * (cin / 32) + 3) / 4 : ntap;
+    return conv_k128<T>(cin) ? (ntap * (cin / 32) + 3) / 4 : ntap;
 }
 
 // One step's weight slice [BN][BSTR] in LDS, rounded up to whole 1-KiB
@@ -249,7 +256,7 @@ template <typename T, int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSE
 constexpr int conv_ring() {
     constexpr size_t cap = 160 * 1024;
     // fp8: the loop reads slice s+1 while s+NB-1 is issued (one-step software pipeline): >= 3
-    constexpr int NB0 = is_fp8<T>() ? 3 : 2;
+    constexpr int NB0 = conv_k128<T>(CIN) ? 3 : 2;
     const size_t base = conv_lds_bytes_nb<T, KH, KW, CIN, BN, TH, TW, FUSED, EBF16>(NB0);
     const size_t blocks = cap / base;
     int nb = NB0;
@@ -628,8 +635,8 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
     }
     // f32 (parity mode) fragments are twice as wide: single-buffered there
     constexpr bool DB = !std::is_same<T, float>::value;
-    if constexpr (F8) {
-        // ---- fp8: K = 128 per MFMA.  Super-step s covers chunks 4s .. 4s+3
+    if constexpr (conv_k128<T>(CIN)) {
+        // ---- fp8, C_in >= 64: K = 128 per MFMA.  Super-step s covers chunks 4s .. 4s+3
         // (chunk k: tap k / CPC, channel chunk k % CPC); lane group q's 32
         // fragment bytes are its 8 bytes (channels 8q .. 8q+7) of each of the
         // four chunks, read as four ds_read_b64 from the patch (A, pixels)
@@ -763,7 +770,7 @@ void conv_mfma(const typename Prec<T>::G* __restrict__ in, int Hin, int Win,
             }
         }
     }
-    }  // !F8
+    }  // !K128
 #undef AA_LOAD_A
 #undef AA_LOAD_B
 #undef AA_GLDS
@@ -1592,7 +1599,7 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             // tap k / (C_in/32), channels 32 (k % (C_in/32)) ..), each
             // [cout_pad][F8_BSTR] with chunk k % 4 at byte 32 (k % 4) of the
             // row (conv_mfma's K = 128 loop); the head keeps [cout_pad][cstr]
-            const bool ss = s.kind == ST_MFMA;
+            const bool ss = s.kind == ST_MFMA && conv_k128<fp8>(s.cin);
             const int cpc = s.cin / 32, nch = ntap * cpc, nss = conv_nstep<fp8>(ntap, s.cin);
             std::vector<uint8_t> h(ss ? (size_t)nss * s.cout_pad * F8_BSTR + 1024 : wpk.size(), 0);
             for (int o = 0; o < s.cout_pad; ++o) {
