@@ -9,11 +9,13 @@ raises.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 import torch  # noqa: F401  (must precede loading libaa.so, see above)
 
-LIB_PATH = Path(__file__).resolve().parent / "libaa.so"
+# AA_LIB: an alternative build of the same library (tools/ab_build.py variants)
+LIB_PATH = Path(os.environ.get("AA_LIB") or Path(__file__).resolve().parent / "libaa.so")
 ABI_VERSION = 2
 
 AA_PREC_F32 = 0

@@ -1113,6 +1113,8 @@ struct Stage {
     int is_first = 0;   // reads the model input (f32 log-mel)
     int fused_first = 0;  // this stage computes the previous (first) layer itself
     int lm_f16 = 0;       // fused_first: the model input is float16
+    int in_split = 0;     // split-bf16: input / output in the grouped-split layout (aa_conv_x3.h)
+    int out_split = 0;
 };
 
 struct Model {
@@ -1182,12 +1184,16 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
 // (1) or per-wave B fragments from global (0), A fragments just in time (1)
 // or a whole step ahead (0), pinned waves per SIMD (0: free); picked by
 // tools/conv_bench_x3.hip sweeps
+#ifdef AA_X3_ALT  // tools/ab_build.py: an alternative tile table for in-pipeline A/B runs
+#define AA_X3_CFGS(X) AA_X3_ALT(X)
+#else
 #define AA_X3_CFGS(X)                                 \
     X(3, 3, 32, 3, 4, 1, 3, 2, 9, 21, 0, 1, 4)        \
-    X(3, 3, 32, 1, 4, 2, 3, 2, 10, 18, 1, 0, 0)       \
-    X(3, 3, 64, 1, 4, 2, 3, 2, 12, 14, 1, 1, 4)       \
-    X(9, 3, 64, 3, 4, 2, 4, 4, 39, 6, 0, 1, 2)        \
-    X(1, 3, 128, 1, 4, 2, 3, 2, 7, 20, 1, 0, 0)
+    X(3, 3, 32, 1, 4, 2, 3, 2, 10, 18, 1, 0, 4)       \
+    X(3, 3, 64, 1, 2, 2, 3, 2, 12, 8, 1, 1, 4)        \
+    X(9, 3, 64, 3, 2, 2, 4, 2, 21, 6, 0, 1, 4)        \
+    X(1, 3, 128, 1, 2, 2, 3, 2, 7, 12, 1, 1, 4)
+#endif
 
 template <typename T>
 constexpr int prec_of() {
@@ -1211,9 +1217,9 @@ static int mfma_bn(int prec, int kh, int kw, int cin, int pool) {
 }
 
 template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool RING, bool AJIT,
-          int OCC, bool FUSED>
+          int OCC, bool FUSED, bool IN_SPLIT, bool OUT_SPLIT>
 static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream_t st, const Stage* first) {
-    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, RING, AJIT, OCC>;
+    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, RING, AJIT, OCC, IN_SPLIT, OUT_SPLIT>;
     constexpr int BN = WN * NF * 16;
     const size_t lds = x3_lds_bytes<KH, KW, CIN, BN, TH, TW, FUSED, RING>();
     FirstConv fc{};
@@ -1298,17 +1304,24 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
                  "no fused first-layer kernel for %s", s.name.c_str());
     }
     if constexpr (is_split<T>()) {
+#define AA_X3L(FU, IS, OS) launch_x3<KH_, KW_, CIN_, WM_, WN_, MF_, NF_, POOL_, TH_, TW_, RING_, AJIT_, OCC_, FU, IS, OS>(s, in, out, n, st, first)
 #define AA_LAUNCH3(KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, RING, AJIT, OCC)                            \
         if (s.kh == KH && s.kw == KW && s.cin == CIN && s.pool == POOL) {                                  \
+            constexpr int KH_ = KH, KW_ = KW, CIN_ = CIN, WM_ = WM, WN_ = WN, MF_ = MF, NF_ = NF, POOL_ = POOL;  \
+            constexpr int TH_ = TH, TW_ = TW, OCC_ = OCC;                                                  \
+            constexpr bool RING_ = RING, AJIT_ = AJIT;                                                     \
             if (s.fused_first) {                                                                           \
                 if constexpr (CIN == 32 && KH == 3 && KW == 3 && WM * WN == 4)                             \
-                    return launch_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, RING, AJIT, OCC, true>(s, in, out, n, st, first); \
+                    return s.out_split ? AA_X3L(true, false, true) : AA_X3L(true, false, false);          \
+            } else if (s.in_split) {                                                                       \
+                return s.out_split ? AA_X3L(false, true, true) : AA_X3L(false, true, false);              \
             } else {                                                                                       \
-                return launch_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, RING, AJIT, OCC, false>(s, in, out, n, st, first); \
+                return s.out_split ? AA_X3L(false, false, true) : AA_X3L(false, false, false);            \
             }                                                                                              \
         }
         AA_X3_CFGS(AA_LAUNCH3)
 #undef AA_LAUNCH3
+#undef AA_X3L
         set_error("conv %dx%d cin %d pool %d: no split-bf16 kernel instantiation", s.kh, s.kw, s.cin, s.pool);
         return AA_ERR_UNSUPPORTED;
     }
@@ -1690,6 +1703,19 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         m->st[1].bytes = 4.0 * m->st[0].Hin * m->st[0].Win * m->st[0].cin +
                          (m->st[1].bytes - es1 * m->st[1].Hin * m->st[1].Win * m->st[1].cin);
         m->st[1].name = m->st[0].name + "+" + m->st[1].name;
+    }
+    // split-bf16: a conv_x3 stage whose consumer is another conv_x3 stage
+    // writes the grouped-split layout, and that consumer stages it by
+    // global_load_lds alone (aa_conv_x3.h); heads / generic stages keep f32
+    if (precision == AA_PREC_BF16X3) {
+        for (size_t k = 0; k + 1 < m->st.size(); ++k) {
+            Stage& a = m->st[k];
+            Stage& b = m->st[k + 1];
+            if (a.skipped || a.kind != ST_MFMA || b.kind != ST_MFMA || b.fused_first) continue;
+            if (a.cout % 32 != 0 || b.cin != a.cout) continue;
+            a.out_split = 1;
+            b.in_split = 1;
+        }
     }
     // ping-pong activation buffers: stage s writes buffer s % 2
     for (size_t k = 0; k + 1 < m->st.size(); ++k) {

@@ -24,6 +24,14 @@
 //    row o in slot (u + o) & 7: the same conflict-free read for B fragments;
 //    a block's slice of a step is BN * 128 contiguous bytes, streamed by
 //    global_load_lds through the LDS ring as in conv_mfma.
+//  * Pre-split activations between conv_x3 stages (IN_SPLIT / OUT_SPLIT).
+//    A stage whose consumer is another conv_x3 stage writes its output
+//    already split, as the "grouped split" HBM layout: per pixel, per
+//    32-channel group, 64 B of bf16 hi then 64 B of bf16 lo (the same 4 B per
+//    element as f32).  The consumer then stages a group's patch with
+//    global_load_lds alone -- lane i of a wave-instruction lands at LDS byte
+//    16 i, and the per-lane GLOBAL address picks the unit that belongs in
+//    that swizzled slot -- no VALU split, no ds_write, no register round trip.
 #pragma once
 
 namespace aa {
@@ -83,7 +91,8 @@ __device__ __forceinline__ int x3_addr(int R, int C, int u, int PW, int TW) {
 // of a whole next-step set prefetched; OCC > 0 pins the waves per SIMD the
 // compiler must fit (its VGPR budget), 0 leaves it free up to the LDS limit.
 template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool FUSED = false,
-          int DIAG = 0, bool RING = true, bool AJIT = false, int OCC = 0>
+          int DIAG = 0, bool RING = true, bool AJIT = false, int OCC = 0, bool IN_SPLIT = false,
+          bool OUT_SPLIT = false>
 __global__ __launch_bounds__(WM * WN * 64)
 __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1,
                                     OCC ? OCC : x3_waves_per_simd<KH, KW, CIN, WM, WN, NF, TH, TW, FUSED, RING>())))
@@ -96,6 +105,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     static_assert(CIN % X3_CG == 0, "C_in multiple of 32");
     static_assert((KW - 1) % 2 == 0, "odd kernel width (the swizzle needs even row jumps)");
     static_assert(!FUSED || (CIN == 32 && WM * WN == 4), "fused first layer: 32 channels, 4 waves");
+    static_assert(!(FUSED && IN_SPLIT), "the fused first layer reads the f32 log-mel");
     constexpr int NTHR = WM * WN * 64;
     constexpr int BN = WN * NF * 16;
     constexpr int PH = TH + KH - 1, PW = TW + KW - 1;
@@ -253,6 +263,26 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         // ---- stage channel group g of the patch (hi / lo planes, swizzled) ----
         if (g > 0) __syncthreads();  // every wave is done with group g-1's patch
         if constexpr (DIAG & 1) {
+        } else if constexpr (IN_SPLIT) {
+            // group g of the patch straight from the pre-split activations:
+            // LDS unit index i = pixel * 8 + slot; slot holds unit
+            // (slot - R*TW - C) & 7 of pixel (R, C).  Out-of-image pixels read a
+            // clamped (finite) pixel: they only feed discarded outputs.
+            constexpr int UNITS = PH * PW * 8;
+            const char* src = reinterpret_cast<const char*>(in) + (size_t)n * Hin * Win * CIN * 4 + g * 128;
+            for (int i0 = wave0 * 64; i0 < UNITS; i0 += NW * 64) {
+                const int idx = i0 + lane;
+                if (idx < UNITS) {
+                    const int pix = idx >> 3, slot = idx & 7;
+                    const int R = pix / PW, C = pix - R * PW;
+                    const int u = (slot - R * TW - C) & 7;
+                    const int gh = min(oh0 + R, Hin - 1), gw = min(ow0 + C, Win - 1);
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(src + ((size_t)gh * Win + gw) * (CIN * 4) + u * 16),
+                        (__attribute__((address_space(3))) void*)(patch + i0 * 16), 16, 0, 0);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if constexpr (!FUSED) {
             constexpr int ITEMS = (PH * PW + 7) / 8 * 64;  // (pixel, channel quad), pixels in 8s
             constexpr int U = 4;
@@ -456,12 +486,29 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         if constexpr ((DIAG & 4) != 0) {
             if (v[0] != 12345.f) continue;  // keep the values live, store (almost) never
         }
-        float* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
-        if (ch0 + 8 <= cout_store) {
-            reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
-            reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+        if constexpr (OUT_SPLIT) {
+            // grouped split: 8 channels of group ch0 / 32 -> one 16-B hi unit and
+            // one 16-B lo unit (cout_store % 32 == 0, planner-checked)
+            if (ch0 < cout_store) {
+                char* o = reinterpret_cast<char*>(out) + ((size_t)n * Hout * Wout + (size_t)gh * Wout + gw) * cout_store * 4 +
+                          (ch0 >> 5) * 128 + (ch0 & 31) * 2;
+                bf16x8 h, l;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    h[c] = bf_hi(v[c]);
+                    l[c] = bf_lo(v[c]);
+                }
+                *reinterpret_cast<bf16x8*>(o) = h;
+                *reinterpret_cast<bf16x8*>(o + 64) = l;
+            }
         } else {
-            for (int c = 0; c < 8 && ch0 + c < cout_store; ++c) o[c] = v[c];
+            float* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
+            if (ch0 + 8 <= cout_store) {
+                reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
+                reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+                for (int c = 0; c < 8 && ch0 + c < cout_store; ++c) o[c] = v[c];
+            }
         }
     }
 }

@@ -6,15 +6,16 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 using namespace aa;
 
 template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, bool FUSED,
-          int DIAG = 0, bool RING = true, bool AJIT = false, int OCC = 0>
+          int DIAG = 0, bool RING = true, bool AJIT = false, int OCC = 0, bool IS = false, bool OS = false>
 static void time_one(const char* tag, int n, int Hin, int Win, int cout, const void* in, const void* w,
                      const float* b, void* out, FirstConv fc, int iters) {
-    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, DIAG, RING, AJIT, OCC>;
+    auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, DIAG, RING, AJIT, OCC, IS, OS>;
     constexpr int BN = WN * NF * 16;
     const size_t lds = x3_lds_bytes<KH, KW, CIN, BN, TH, TW, FUSED, RING>();
     if (lds > 160 * 1024) {
@@ -44,8 +45,8 @@ static void time_one(const char* tag, int n, int Hin, int Win, int cout, const v
     const float us = 1e3f * ms / iters;
     double fl = 2.0 * n * Hc * Wc * KH * KW * CIN * cout;
     if (FUSED) fl += 2.0 * n * (Hin) * (Win) * 9 * 32;
-    printf("%-8s%s%s%d %dx%d cin %3d WM%d WN%d MF%2d NF%d %2dx%2d  LDS %6zu  grid %6d  %7.1f us  %6.1f TF (%.3f of 833)\n",
-           tag, RING ? "" : "G", AJIT ? "J" : "", OCC, KH, KW, CIN, WM, WN, MF, NF, TH, TW, lds, grid.x * grid.y * grid.z, us, fl / us * 1e-6,
+    printf("%-8s%s%s%s%d %dx%d cin %3d WM%d WN%d MF%2d NF%d %2dx%2d  LDS %6zu  grid %6d  %7.1f us  %6.1f TF (%.3f of 833)\n",
+           tag, IS ? "S" : "", RING ? "" : "G", AJIT ? "J" : "", OCC, KH, KW, CIN, WM, WN, MF, NF, TH, TW, lds, grid.x * grid.y * grid.z, us, fl / us * 1e-6,
            fl / us * 1e-6 / 833.3);
 }
 
@@ -76,12 +77,14 @@ int main(int argc, char** argv) {
     if (which == 9) {
         // DIAG bits (aa_cnn.hip): 1 no staging, 4 no stores, 32 no weight stream,
         // 128 no fragment reads after the first, 2 no MFMA loop
-#define ABL5(D) time_one<9, 3, 64, 3, 2, 5, 2, 3, 39, 6, false, D>("c5 d" #D, n, 48, 70, 128, in, w, b, out, fc, it);
-#define ABL2(D) time_one<3, 3, 32, 4, 1, 3, 2, 3, 6, 30, true, D>("c2 d" #D, n, 158, 224, 32, in, w, b, out, f1, it);
-#define ABL4(D) time_one<3, 3, 64, 4, 2, 4, 2, 1, 16, 16, false, D>("c4 d" #D, n, 50, 72, 64, in, w, b, out, fc, it);
-        ABL5(0) ABL5(1) ABL5(2) ABL5(4) ABL5(33) ABL5(161) ABL5(165) ABL5(37)
-        ABL2(0) ABL2(2) ABL2(64) ABL2(4) ABL2(32) ABL2(160) ABL2(96)
-        ABL4(0) ABL4(1) ABL4(2) ABL4(33) ABL4(161) ABL4(165)
+#define ABL5(D) time_one<9, 3, 64, 4, 2, 4, 4, 3, 39, 6, false, D, false, true, 2>("c5 d" #D, n, 48, 70, 128, in, w, b, out, fc, it);
+#define ABL2(D) time_one<3, 3, 32, 4, 1, 3, 2, 3, 9, 21, true, D, false, true, 4>("c2 d" #D, n, 158, 224, 32, in, w, b, out, f1, it);
+#define ABL4(D) time_one<3, 3, 64, 4, 2, 3, 2, 1, 12, 14, false, D, true, true, 4>("c4 d" #D, n, 50, 72, 64, in, w, b, out, fc, it);
+#define ABL3(D) time_one<3, 3, 32, 4, 2, 3, 2, 1, 10, 18, false, D, true, false, 0>("c3 d" #D, n, 52, 74, 64, in, w, b, out, fc, it);
+        ABL5(0) ABL5(1) ABL5(2) ABL5(4) ABL5(5) ABL5(33) ABL5(161) ABL5(165) ABL5(37)
+        ABL2(0) ABL2(2) ABL2(64) ABL2(512) ABL2(576) ABL2(4) ABL2(1) ABL2(5)
+        ABL4(0) ABL4(1) ABL4(2) ABL4(4) ABL4(5) ABL4(33) ABL4(161) ABL4(165)
+        ABL3(0) ABL3(1) ABL3(2) ABL3(5) ABL3(165)
         return 0;
     }
     // model1 at T = 226: (Hin, Win) of each conv's input
@@ -100,6 +103,76 @@ int main(int argc, char** argv) {
 #define J5(WM, WN, MF, NF, TH, TW, R, O) time_one<9, 3, 64, WM, WN, MF, NF, 3, TH, TW, false, 0, R, true, O>("c5", n, 48, 70, 128, in, w, b, out, fc, it);
 #define J6(WM, WN, MF, NF, TH, TW, R, O) time_one<1, 3, 128, WM, WN, MF, NF, 1, TH, TW, false, 0, R, true, O>("c6", n, 13, 22, 256, in, w, b, out, fc, it);
 #define C6(WM, WN, MF, NF, TH, TW) time_one<1, 3, 128, WM, WN, MF, NF, 1, TH, TW, false>("c6", n, 13, 22, 256, in, w, b, out, fc, it);
+    // pre-split input / output (IN_SPLIT, OUT_SPLIT): the shipped pipeline's c3..c6
+#define S3(WM, WN, MF, NF, TH, TW, R, J, O) time_one<3, 3, 32, WM, WN, MF, NF, 1, TH, TW, false, 0, R, J, O, true, true>("c3", n, 52, 74, 64, in, w, b, out, fc, it);
+#define S4(WM, WN, MF, NF, TH, TW, R, J, O) time_one<3, 3, 64, WM, WN, MF, NF, 1, TH, TW, false, 0, R, J, O, true, true>("c4", n, 50, 72, 64, in, w, b, out, fc, it);
+#define S5(WM, WN, MF, NF, TH, TW, R, J, O) time_one<9, 3, 64, WM, WN, MF, NF, 3, TH, TW, false, 0, R, J, O, true, true>("c5", n, 48, 70, 128, in, w, b, out, fc, it);
+#define S6(WM, WN, MF, NF, TH, TW, R, J, O) time_one<1, 3, 128, WM, WN, MF, NF, 1, TH, TW, false, 0, R, J, O, true, false>("c6", n, 13, 22, 256, in, w, b, out, fc, it);
+    if (which == 11) {
+        S5(4, 2, 4, 4, 39, 6, false, true, 2) S5(4, 1, 4, 4, 39, 6, false, true, 2) S5(4, 1, 4, 4, 39, 6, false, true, 0)
+        S5(4, 1, 4, 4, 39, 6, true, true, 2) S5(4, 2, 4, 4, 39, 6, true, true, 2) S5(4, 2, 4, 2, 39, 6, false, true, 4)
+        S5(4, 2, 4, 2, 39, 6, true, true, 4) S5(4, 1, 4, 2, 39, 6, false, true, 4) S5(2, 2, 4, 4, 21, 6, false, true, 2)
+        S5(8, 2, 2, 4, 39, 6, false, true, 2) S5(4, 2, 4, 4, 42, 6, false, true, 2) S5(4, 2, 6, 4, 39, 9, false, true, 2)
+        S4(4, 2, 3, 2, 12, 14, true, true, 4) S4(4, 2, 3, 2, 12, 14, false, true, 4) S4(4, 2, 4, 2, 16, 14, true, true, 4)
+        S4(4, 2, 4, 2, 16, 14, true, true, 0) S4(4, 1, 3, 4, 12, 14, true, true, 4) S4(4, 2, 6, 2, 24, 14, true, true, 0)
+        S4(4, 2, 3, 2, 8, 24, true, true, 4) S4(2, 2, 3, 2, 8, 12, true, true, 4)
+        S3(4, 2, 3, 2, 10, 18, true, false, 0) S3(4, 2, 3, 2, 10, 18, true, true, 4) S3(4, 2, 4, 2, 10, 24, true, true, 4)
+        S3(4, 2, 3, 2, 12, 16, true, true, 4) S3(4, 1, 3, 4, 12, 16, true, true, 4) S3(2, 2, 3, 2, 8, 12, true, true, 4)
+        S6(4, 2, 3, 2, 7, 20, true, false, 0) S6(4, 2, 3, 2, 7, 20, true, true, 4) S6(4, 2, 5, 2, 13, 20, true, true, 0)
+        S6(4, 1, 3, 4, 7, 20, true, false, 0) S6(2, 2, 3, 2, 7, 12, true, true, 4) S6(4, 2, 3, 2, 7, 20, false, true, 4)
+        return 0;
+    }
+#define F2(WM, WN, MF, NF, TH, TW, R, O) time_one<3, 3, 32, WM, WN, MF, NF, 3, TH, TW, true, 0, R, true, O, false, true>("c1+c2", n, 158, 224, 32, in, w, b, out, f1, it);
+    if (which == 13) {
+        // data dependence: the same tiles on random bit patterns (the default
+        // fill) and on properly split N(0,1) activations / N(0,0.05) weights
+        S5(2, 2, 4, 2, 21, 6, false, true, 4) S5(4, 2, 4, 4, 39, 6, false, true, 2) S4(2, 2, 3, 2, 12, 8, true, true, 4)
+        F2(4, 1, 3, 2, 9, 21, false, 4)
+        std::vector<uint16_t> hs(h.size() * 2), ws(hw.size());
+        unsigned st = 1;
+        auto gauss = [&]() {
+            float a = 0;
+            for (int k = 0; k < 4; ++k) { st = st * 1664525u + 1013904223u; a += (st >> 8) * (1.f / 16777216.f) - 0.5f; }
+            return a * 1.7f;
+        };
+        auto split = [](float x, uint16_t& hi, uint16_t& lo) {
+            uint32_t u; memcpy(&u, &x, 4);
+            uint32_t r = (u + 0x7fff + ((u >> 16) & 1)) & 0xffff0000u;
+            float hf; memcpy(&hf, &r, 4);
+            float l = x - hf; uint32_t v; memcpy(&v, &l, 4);
+            v = (v + 0x7fff + ((v >> 16) & 1)) >> 16;
+            hi = (uint16_t)(r >> 16); lo = (uint16_t)v;
+        };
+        // grouped split: per 32 channels 32 hi then 32 lo
+        for (size_t px = 0; px < hs.size() / 64; ++px)
+            for (int c = 0; c < 32; ++c) split(gauss(), hs[px * 64 + c], hs[px * 64 + 32 + c]);
+        for (size_t r = 0; r < ws.size() / 64; ++r)
+            for (int c = 0; c < 32; ++c) split(0.05f * gauss(), ws[r * 64 + c], ws[r * 64 + 32 + c]);
+        (void)hipMemcpy(in, hs.data(), std::min(hs.size() * 2, h.size() * 4), hipMemcpyHostToDevice);
+        (void)hipMemcpy(w, ws.data(), ws.size() * 2, hipMemcpyHostToDevice);
+        printf("-- split N(0,1) data --\n");
+        S5(2, 2, 4, 2, 21, 6, false, true, 4) S5(4, 2, 4, 4, 39, 6, false, true, 2) S4(2, 2, 3, 2, 12, 8, true, true, 4)
+        F2(4, 1, 3, 2, 9, 21, false, 4)
+        return 0;
+    }
+    if (which == 12) {
+        S5(2, 2, 4, 4, 21, 6, false, true, 2) S5(2, 2, 4, 4, 21, 6, false, true, 0) S5(2, 2, 4, 4, 21, 6, false, true, 3)
+        S5(2, 2, 4, 4, 21, 6, true, true, 2) S5(2, 2, 5, 4, 24, 6, false, true, 2) S5(2, 2, 3, 4, 15, 6, false, true, 2)
+        S5(2, 2, 4, 2, 21, 6, false, true, 4) S5(4, 1, 2, 4, 21, 6, false, true, 4) S5(2, 1, 4, 8, 21, 6, false, true, 2)
+        S5(2, 2, 8, 4, 39, 6, false, true, 2) S5(2, 2, 8, 4, 39, 6, false, true, 1) S5(2, 1, 4, 4, 21, 6, false, true, 4)
+        S5(1, 2, 8, 4, 21, 6, false, true, 2) S5(2, 2, 4, 4, 21, 6, false, false, 2) S5(2, 4, 4, 2, 21, 6, false, true, 2)
+        S4(2, 2, 3, 2, 8, 12, true, true, 4) S4(2, 2, 3, 2, 8, 12, true, true, 0) S4(2, 2, 3, 2, 8, 12, false, true, 4)
+        S4(2, 2, 4, 2, 8, 16, true, true, 4) S4(2, 2, 3, 2, 6, 16, true, true, 4) S4(2, 2, 2, 2, 4, 16, true, true, 4)
+        S4(2, 1, 3, 4, 8, 12, true, true, 4) S4(2, 2, 3, 2, 12, 8, true, true, 4) S4(2, 2, 4, 2, 10, 12, true, true, 4)
+        S3(2, 2, 3, 2, 8, 12, true, true, 0) S3(2, 2, 3, 2, 8, 12, true, false, 0) S3(2, 2, 4, 2, 8, 16, true, false, 0)
+        S3(2, 2, 3, 2, 6, 16, true, false, 0) S3(2, 2, 2, 2, 4, 16, true, false, 0) S3(4, 2, 3, 2, 10, 18, true, false, 4)
+        S3(2, 2, 4, 2, 10, 12, true, false, 0) S3(2, 1, 3, 4, 8, 12, true, false, 0)
+        S6(2, 2, 3, 2, 7, 12, true, true, 4) S6(2, 2, 3, 2, 7, 12, true, false, 0) S6(2, 2, 2, 2, 4, 16, true, true, 4)
+        S6(2, 1, 3, 4, 7, 12, true, true, 4) S6(2, 2, 3, 2, 7, 12, false, true, 4)
+        F2(4, 1, 3, 2, 9, 21, false, 4) F2(4, 1, 3, 2, 9, 21, false, 0) F2(4, 1, 4, 2, 12, 21, false, 4)
+        F2(4, 1, 6, 2, 12, 30, false, 3) F2(4, 1, 3, 2, 9, 21, true, 4) F2(4, 1, 2, 2, 6, 21, false, 4)
+        return 0;
+    }
     if (which == 10) {  // the shipped c5 / c2 tiles alone (PMC passes)
         C5(3, 2, 5, 2, 39, 6) C2(4, 1, 3, 2, 6, 30)
         return 0;
