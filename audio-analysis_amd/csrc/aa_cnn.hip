@@ -1082,6 +1082,7 @@ __global__ void track_mean(const float* __restrict__ probs, int n_models, long l
 }  // namespace aa
 
 #include "aa_conv_x3.h"
+#include "aa_conv_wg.h"
 
 namespace aa {
 
@@ -1115,6 +1116,7 @@ struct Stage {
     int lm_f16 = 0;       // fused_first: the model input is float16
     int in_split = 0;     // split-bf16: input / output in the grouped-split layout (aa_conv_x3.h)
     int out_split = 0;
+    int wg = 0;           // split-bf16 Winograd F(2,3)-along-W kernel (aa_conv_wg.h) and its weight packing
 };
 
 struct Model {
@@ -1195,6 +1197,28 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     X(1, 3, 128, 1, 2, 2, 3, 2, 7, 12, 1, 1, 4)
 #endif
 
+// conv_wg (split-bf16, Winograd F(2,3) along W) instantiations: (kh, C_in,
+// pool) of kernel-width-3 convs -> waves (WM x WN), fragments per wave (MF x
+// NF, each with 4 accumulator sets), output tile TH x TW (TW even), pinned
+// waves per SIMD (0: free).  Preferred over conv_x3 where a row exists (the
+// fused first-layer stage always runs conv_x3).  In-pipeline A/B (tools/ab.sh,
+// same box): the 9x3 layer 187 -> 160 us, step 180k -> 193k audio-s/s; the
+// small 3x3 / 1x3 layers lose on it (their transform-heavy staging outweighs
+// the saved MFMAs: 3x3/32 36 -> 55 us, 3x3/64 52 -> 76 us, 1x3 22 -> 28 us).
+#ifdef AA_WG_ALT
+#define AA_WG_CFGS(X) AA_WG_ALT(X)
+#else
+#define AA_WG_CFGS(X) X(9, 64, 3, 2, 2, 4, 2, 39, 6, 2)
+#endif
+
+static int wg_bn(int kh, int kw, int cin, int pool) {
+#define AA_WBN(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC) \
+    if (kw == 3 && kh == KH && cin == CIN && pool == POOL) return WN * NF * 16;
+    AA_WG_CFGS(AA_WBN)
+#undef AA_WBN
+    return 0;
+}
+
 template <typename T>
 constexpr int prec_of() {
     return is_split<T>() ? AA_PREC_BF16X3 : sizeof(T) == 1 ? AA_PREC_FP8 : sizeof(T) == 2 ? AA_PREC_BF16 : AA_PREC_F32;
@@ -1204,6 +1228,7 @@ static size_t prec_bytes(int prec) { return prec == AA_PREC_FP8 ? 1 : prec == AA
 
 // output channels per block of the instantiation serving this stage (0: none)
 static int mfma_bn(int prec, int kh, int kw, int cin, int pool) {
+    if (prec == AA_PREC_BF16X3 && wg_bn(kh, kw, cin, pool)) return wg_bn(kh, kw, cin, pool);
 #define AA_BN(T_, KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, EB, OCC)                                       \
     if (prec_of<T_>() == prec && kh == KH && kw == KW && cin == CIN && pool == POOL) \
         return WN * NF * 16;
@@ -1239,6 +1264,27 @@ static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream
     dim3 grid(tiles_h * tiles_w, s.cout_pad / BN, n);
     hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, st, (const float*)in, s.Hin, s.Win, (const bf16*)s.d_w,
                        s.d_b, (float*)out, s.Hout, s.Wout, s.cout, tiles_w, s.act, s.alpha, fc);
+    AA_LAUNCH_CHECK();
+    return AA_OK;
+}
+
+template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int OCC, bool IN_SPLIT,
+          bool OUT_SPLIT>
+static int launch_wg(const Stage& s, const void* in, void* out, int n, hipStream_t st) {
+    auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IN_SPLIT, OUT_SPLIT>;
+    constexpr int BN = WN * NF * 16;
+    const size_t lds = wg_lds_bytes<KH, BN, TH, TW>();
+    AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
+    static size_t attr = 0;
+    if (lds > attr) {
+        AA_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = lds;
+    }
+    const int tiles_h = (s.Hout * POOL + TH - 1) / TH;
+    const int tiles_w = (s.Wout * POOL + TW - 1) / TW;
+    dim3 grid(tiles_h * tiles_w, s.cout_pad / BN, n);
+    hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, st, (const float*)in, s.Hin, s.Win, (const bf16*)s.d_w,
+                       s.d_b, (float*)out, s.Hout, s.Wout, s.cout, tiles_w, s.act, s.alpha);
     AA_LAUNCH_CHECK();
     return AA_OK;
 }
@@ -1304,6 +1350,20 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
                  "no fused first-layer kernel for %s", s.name.c_str());
     }
     if constexpr (is_split<T>()) {
+        if (s.wg) {
+#define AA_LAUNCHW(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC)                                                   \
+            if (s.kh == KH && s.cin == CIN && s.pool == POOL) {                                                   \
+                if (s.in_split)                                                                                   \
+                    return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, true, true>(s, in, out, n, st) \
+                                       : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, true, false>(s, in, out, n, st); \
+                return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, false, true>(s, in, out, n, st) \
+                                   : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, false, false>(s, in, out, n, st); \
+            }
+            AA_WG_CFGS(AA_LAUNCHW)
+#undef AA_LAUNCHW
+            set_error("conv %dx%d cin %d pool %d: no Winograd kernel instantiation", s.kh, s.kw, s.cin, s.pool);
+            return AA_ERR_UNSUPPORTED;
+        }
 #define AA_X3L(FU, IS, OS) launch_x3<KH_, KW_, CIN_, WM_, WN_, MF_, NF_, POOL_, TH_, TW_, RING_, AJIT_, OCC_, FU, IS, OS>(s, in, out, n, st, first)
 #define AA_LAUNCH3(KH, KW, CIN, POOL, WM, WN, MF, NF, TH, TW, RING, AJIT, OCC)                            \
         if (s.kh == KH && s.kw == KW && s.cin == CIN && s.pool == POOL) {                                  \
@@ -1570,6 +1630,7 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         }
         int bn_tile = 32;
         if (s.kind == ST_MFMA) bn_tile = mfma_bn(precision, s.kh, s.kw, s.cin, s.pool);
+        s.wg = precision == AA_PREC_BF16X3 && s.kind == ST_MFMA && wg_bn(s.kh, s.kw, s.cin, s.pool) > 0;
         const bool rowmajor = s.kind == ST_SMALL || s.kind == ST_GENERIC;  // f32 [cout][K]
         s.cout_pad = rowmajor ? s.cout : (s.cout + bn_tile - 1) / bn_tile * bn_tile;
         // pack weights with the BN scale folded in: conv_small / generic
@@ -1648,6 +1709,31 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             // of row o stored in slot (u + o) & 7 (aa_conv_x3.h)
             std::vector<uint16_t> h(2 * wpk.size(), 0);
             const int ng = s.cin / 32;
+            if (s.wg) {
+                // conv_wg steps (group g, row kh, e) in order ((g * kh + kh) * 4 + e), each
+                // [cout_pad][8 units] as above, holding the transformed weights
+                // v0 = w0, v1 = (w0 + w1 + w2) / 2, v2 = (w0 - w1 + w2) / 2, v3 = w2
+                // (w_kw = the folded kernel at (kh, kw)), computed in double
+                h.assign((size_t)ng * s.kh * 4 * s.cout_pad * 64 * 2 + 1024, 0);
+                for (int g = 0; g < ng; ++g)
+                    for (int kh = 0; kh < s.kh; ++kh)
+                        for (int o = 0; o < s.cout_pad; ++o)
+                            for (int c = 0; c < 32; ++c) {
+                                double w3[3];
+                                for (int kw = 0; kw < 3; ++kw)
+                                    w3[kw] = o < s.cout ? (double)kern[((size_t)(kh * 3 + kw) * s.cin + 32 * g + c) * s.cout + o] * scale[o] : 0.0;
+                                const double v[4] = {w3[0], 0.5 * (w3[0] + w3[1] + w3[2]), 0.5 * (w3[0] - w3[1] + w3[2]), w3[2]};
+                                for (int e = 0; e < 4; ++e) {
+                                    const size_t row = ((size_t)((g * s.kh + kh) * 4 + e) * s.cout_pad + o) * 64;
+                                    const float w = (float)v[e];
+                                    const uint16_t hi = f2bf(w);
+                                    const int u = c / 8;
+                                    h[row + ((u + o) & 7) * 8 + c % 8] = hi;
+                                    h[row + ((u + 4 + o) & 7) * 8 + c % 8] = f2bf(w - bf2f(hi));
+                                }
+                            }
+                ok = upload(s, h.data(), h.size() * 2, bias);
+            } else {
             for (int g = 0; g < ng; ++g)
                 for (int t = 0; t < ntap; ++t)
                     for (int o = 0; o < s.cout_pad; ++o) {
@@ -1661,6 +1747,7 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                         }
                     }
             ok = upload(s, h.data(), wbytes, bias);
+            }
         } else {
             ok = upload(s, wpk.data(), wbytes, bias);
         }

@@ -83,6 +83,72 @@ __device__ __forceinline__ int x3_addr(int R, int C, int u, int PW, int TW) {
     return (R * PW + C) * 128 + (((u + R * TW + C) & 7) << 4);
 }
 
+// Epilogue shared by the split-bf16 kernels: the f32 tile E [TH*TW][BN+4]
+// (bias not yet added) -> POOL x POOL max, bias, activation, and the NHWC
+// store (f32, or the grouped-split layout when OUT_SPLIT).  One thread per
+// (pooled pixel, 8-channel group).
+template <int TH, int TW, int POOL, int BN, int NTHR, bool OUT_SPLIT, bool NOSTORE>
+__device__ __forceinline__ void x3_store(const float* E, const float* __restrict__ bias, float* __restrict__ out, int n,
+                                         int oh0, int ow0, int Hout, int Wout, int cout_store, int act, float alpha) {
+    constexpr int ESTR = BN + 4;
+    constexpr int PHo = TH / POOL, PWo = TW / POOL;
+    constexpr int G = BN / 8;
+    static_assert(NTHR % G == 0, "fixed channel group per thread");
+    const int oh0s = oh0 / POOL, ow0s = ow0 / POOL;
+    const int col = (threadIdx.x % G) * 8;
+    const int ch0 = blockIdx.y * BN + col;
+    float bv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bv[c] = bias[ch0 + c];  // bias is padded to cout_pad
+    float* dst = out + (size_t)n * Hout * Wout * cout_store;
+    for (int qo = threadIdx.x / G; qo < PHo * PWo; qo += NTHR / G) {
+        const int pr = qo / PWo, pc = qo - (qo / PWo) * PWo;
+        const int gh = oh0s + pr, gw = ow0s + pc;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = -INFINITY;
+#pragma unroll
+        for (int dy = 0; dy < POOL; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < POOL; ++dx) {
+                const float* e = E + ((pr * POOL + dy) * TW + pc * POOL + dx) * ESTR + col;
+                const float4 a = reinterpret_cast<const float4*>(e)[0], b = reinterpret_cast<const float4*>(e)[1];
+                v[0] = fmaxf(v[0], a.x); v[1] = fmaxf(v[1], a.y); v[2] = fmaxf(v[2], a.z); v[3] = fmaxf(v[3], a.w);
+                v[4] = fmaxf(v[4], b.x); v[5] = fmaxf(v[5], b.y); v[6] = fmaxf(v[6], b.z); v[7] = fmaxf(v[7], b.w);
+            }
+        if (gh >= Hout || gw >= Wout) continue;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = apply_act(v[c] + bv[c], act, alpha);
+        if constexpr (NOSTORE) {
+            if (v[0] != 12345.f) continue;  // keep the values live, store (almost) never
+        }
+        if constexpr (OUT_SPLIT) {
+            // grouped split: 8 channels of group ch0 / 32 -> one 16-B hi unit and
+            // one 16-B lo unit (cout_store % 32 == 0, planner-checked)
+            if (ch0 < cout_store) {
+                char* o = reinterpret_cast<char*>(out) + ((size_t)n * Hout * Wout + (size_t)gh * Wout + gw) * cout_store * 4 +
+                          (ch0 >> 5) * 128 + (ch0 & 31) * 2;
+                bf16x8 h, l;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    h[c] = bf_hi(v[c]);
+                    l[c] = bf_lo(v[c]);
+                }
+                *reinterpret_cast<bf16x8*>(o) = h;
+                *reinterpret_cast<bf16x8*>(o + 64) = l;
+            }
+        } else {
+            float* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
+            if (ch0 + 8 <= cout_store) {
+                reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
+                reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+                for (int c = 0; c < 8 && ch0 + c < cout_store; ++c) o[c] = v[c];
+            }
+        }
+    }
+}
+
 // RING = false: no weight ring and no per-step barrier -- every wave loads
 // its own B fragments (its NF x 16 output-channel rows of the step) straight
 // from global memory (L2-resident weights) one step ahead, so waves only
@@ -455,62 +521,8 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         }
     }
     __syncthreads();
-    constexpr int PHo = TH / POOL, PWo = TW / POOL;
-    constexpr int G = BN / 8;
-    static_assert(NTHR % G == 0, "fixed channel group per thread");
-    const int oh0s = oh0 / POOL, ow0s = ow0 / POOL;
-    const int col = (threadIdx.x % G) * 8;
-    const int ch0 = blockIdx.y * BN + col;
-    float bv[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) bv[c] = bias[ch0 + c];  // bias is padded to cout_pad
-    float* dst = out + (size_t)n * Hout * Wout * cout_store;
-    for (int qo = threadIdx.x / G; qo < PHo * PWo; qo += NTHR / G) {
-        const int pr = qo / PWo, pc = qo - (qo / PWo) * PWo;
-        const int gh = oh0s + pr, gw = ow0s + pc;
-        float v[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = -INFINITY;
-#pragma unroll
-        for (int dy = 0; dy < POOL; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < POOL; ++dx) {
-                const float* e = E + ((pr * POOL + dy) * TW + pc * POOL + dx) * ESTR + col;
-                const float4 a = reinterpret_cast<const float4*>(e)[0], b = reinterpret_cast<const float4*>(e)[1];
-                v[0] = fmaxf(v[0], a.x); v[1] = fmaxf(v[1], a.y); v[2] = fmaxf(v[2], a.z); v[3] = fmaxf(v[3], a.w);
-                v[4] = fmaxf(v[4], b.x); v[5] = fmaxf(v[5], b.y); v[6] = fmaxf(v[6], b.z); v[7] = fmaxf(v[7], b.w);
-            }
-        if (gh >= Hout || gw >= Wout) continue;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = apply_act(v[c] + bv[c], act, alpha);
-        if constexpr ((DIAG & 4) != 0) {
-            if (v[0] != 12345.f) continue;  // keep the values live, store (almost) never
-        }
-        if constexpr (OUT_SPLIT) {
-            // grouped split: 8 channels of group ch0 / 32 -> one 16-B hi unit and
-            // one 16-B lo unit (cout_store % 32 == 0, planner-checked)
-            if (ch0 < cout_store) {
-                char* o = reinterpret_cast<char*>(out) + ((size_t)n * Hout * Wout + (size_t)gh * Wout + gw) * cout_store * 4 +
-                          (ch0 >> 5) * 128 + (ch0 & 31) * 2;
-                bf16x8 h, l;
-#pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    h[c] = bf_hi(v[c]);
-                    l[c] = bf_lo(v[c]);
-                }
-                *reinterpret_cast<bf16x8*>(o) = h;
-                *reinterpret_cast<bf16x8*>(o + 64) = l;
-            }
-        } else {
-            float* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
-            if (ch0 + 8 <= cout_store) {
-                reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
-                reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
-            } else {
-                for (int c = 0; c < 8 && ch0 + c < cout_store; ++c) o[c] = v[c];
-            }
-        }
-    }
+    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, (DIAG & 4) != 0>(E, bias, out, n, oh0, ow0, Hout, Wout, cout_store, act,
+                                                               alpha);
 }
 
 }  // namespace aa

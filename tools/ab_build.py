@@ -4,7 +4,9 @@ kernel times differ by +-5-25 % between boxes and with the data's toggle
 rate (the MI355X runs power-limited), so tile choices are compared in the
 real pipeline, alternating runs on the same box.
 
-usage: python tools/ab_build.py NAME 'X(...) X(...) ...' [NAME 'table' ...]
+usage: python tools/ab_build.py NAME X3TABLE WGTABLE [NAME X3TABLE WGTABLE ...]
+  X3TABLE / WGTABLE: 'X(...) X(...) ...' for AA_X3_CFGS / AA_WG_CFGS, '-' keeps
+  the in-tree table, '' an empty one
 writes tools/ab/libaa_NAME.so (the other objects come from the main build)."""
 import subprocess
 import sys
@@ -15,14 +17,15 @@ sys.path.insert(0, str(ROOT / "audio-analysis_amd"))
 from aa_amd import _build  # noqa: E402
 
 
-def build(name, table):
+def build(name, table, wg="-"):
     _build.build()
     out = ROOT / "tools" / "ab"
     out.mkdir(exist_ok=True)
     cc = _build.hipcc()
     obj = out / f"aa_cnn_{name}.o"
     cmd = [cc, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={_build.ARCH}", f"-I{_build.INCLUDE}",
-           f"-DAA_X3_ALT(X)={table}", "-c", str(_build.CSRC / "aa_cnn.hip"), "-o", str(obj)]
+           *([f"-DAA_X3_ALT(X)={table}"] if table != "-" else []),
+           *([f"-DAA_WG_ALT(X)={wg}"] if wg != "-" else []), "-c", str(_build.CSRC / "aa_cnn.hip"), "-o", str(obj)]
     subprocess.run(cmd, check=True)
     objs = [_build.PKG.parent / "build" / (s.rsplit(".", 1)[0] + ".o") for s in _build.SOURCES if s != "aa_cnn.hip"]
     lib = out / f"libaa_{name}.so"
@@ -34,5 +37,5 @@ def build(name, table):
 
 if __name__ == "__main__":
     a = sys.argv[1:]
-    for i in range(0, len(a), 2):
-        build(a[i], a[i + 1])
+    for i in range(0, len(a), 3):
+        build(a[i], a[i + 1], a[i + 2])

@@ -50,6 +50,40 @@ static void time_one(const char* tag, int n, int Hin, int Win, int cout, const v
            fl / us * 1e-6 / 833.3);
 }
 
+template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int OCC, bool IS, bool OS,
+          int DIAG = 0>
+static void time_wg(const char* tag, int n, int Hin, int Win, int cout, const void* in, const void* w, const float* b,
+                    void* out, int iters) {
+    auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IS, OS, DIAG>;
+    constexpr int BN = WN * NF * 16;
+    const size_t lds = wg_lds_bytes<KH, BN, TH, TW>();
+    if (lds > 160 * 1024) { printf("%s LDS %zu: skip\n", tag, lds); return; }
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const int Hc = Hin - KH + 1, Wc = Win - 3 + 1;
+    const int Hout = Hc / POOL, Wout = Wc / POOL;
+    const int tiles_h = (Hout * POOL + TH - 1) / TH, tiles_w = (Wout * POOL + TW - 1) / TW;
+    dim3 grid(tiles_h * tiles_w, cout / BN, n);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int i = 0; i < 3; ++i)
+        hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, 0, (const float*)in, Hin, Win, (const bf16*)w, b,
+                           (float*)out, Hout, Wout, cout, tiles_w, 1, 0.3f);
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < iters; ++i)
+        hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, 0, (const float*)in, Hin, Win, (const bf16*)w, b,
+                           (float*)out, Hout, Wout, cout, tiles_w, 1, 0.3f);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const float us = 1e3f * ms / iters;
+    const double fl = 2.0 * n * Hc * Wc * KH * 3 * CIN * cout;
+    printf("%-6s wg d%d %dx3 cin %3d WM%d WN%d MF%d NF%d %2dx%2d occ%d LDS %6zu grid %6d  %7.1f us  %6.1f TF (%.3f of 833)\n",
+           tag, DIAG, KH, CIN, WM, WN, MF, NF, TH, TW, OCC, lds, grid.x * grid.y * grid.z, us, fl / us * 1e-6,
+           fl / us * 1e-6 / 833.3);
+}
+
 int main(int argc, char** argv) {
     const int n = 64, it = 20;
     std::vector<float> h(100u << 20);  // 400 MB of f32 activations: larger than every layer's input
@@ -123,6 +157,22 @@ int main(int argc, char** argv) {
         return 0;
     }
 #define F2(WM, WN, MF, NF, TH, TW, R, O) time_one<3, 3, 32, WM, WN, MF, NF, 3, TH, TW, true, 0, R, true, O, false, true>("c1+c2", n, 158, 224, 32, in, w, b, out, f1, it);
+#define W5(WM, WN, MF, NF, TH, TW, O, D) time_wg<9, 64, WM, WN, MF, NF, 3, TH, TW, O, true, true, D>("c5", n, 48, 70, 128, in, w, b, out, it);
+#define W4(WM, WN, MF, NF, TH, TW, O, D) time_wg<3, 64, WM, WN, MF, NF, 1, TH, TW, O, true, true, D>("c4", n, 50, 72, 64, in, w, b, out, it);
+#define W3(WM, WN, MF, NF, TH, TW, O, D) time_wg<3, 32, WM, WN, MF, NF, 1, TH, TW, O, true, true, D>("c3", n, 52, 74, 64, in, w, b, out, it);
+#define W6(WM, WN, MF, NF, TH, TW, O, D) time_wg<1, 128, WM, WN, MF, NF, 1, TH, TW, O, true, false, D>("c6", n, 13, 22, 256, in, w, b, out, it);
+    if (which == 14) {
+        W5(2, 2, 2, 2, 21, 6, 0, 0) W5(2, 2, 2, 2, 21, 6, 0, 1) W5(2, 2, 2, 2, 21, 6, 0, 2) W5(2, 2, 2, 2, 21, 6, 0, 3)
+        W5(2, 2, 4, 2, 39, 6, 0, 0) W5(2, 2, 4, 2, 39, 6, 2, 0) W5(4, 1, 2, 4, 21, 6, 0, 0) W5(2, 2, 2, 4, 21, 6, 0, 0)
+        W5(1, 2, 4, 2, 21, 6, 0, 0) W5(2, 1, 2, 4, 21, 6, 0, 0) W5(2, 2, 2, 2, 21, 6, 2, 0) W5(2, 2, 2, 2, 21, 6, 4, 0)
+        W5(4, 2, 2, 2, 39, 6, 0, 0) W5(2, 2, 3, 2, 15, 12, 0, 0)
+        W4(2, 2, 2, 2, 8, 16, 0, 0) W4(2, 2, 2, 2, 8, 16, 0, 1) W4(2, 2, 2, 2, 8, 16, 0, 2) W4(2, 2, 3, 2, 12, 16, 0, 0)
+        W4(2, 2, 4, 2, 16, 16, 0, 0) W4(2, 2, 2, 2, 4, 32, 0, 0) W4(4, 2, 2, 2, 16, 16, 0, 0) W4(2, 2, 4, 2, 8, 32, 0, 0)
+        W3(2, 2, 2, 2, 8, 16, 0, 0) W3(2, 2, 2, 2, 8, 16, 0, 1) W3(2, 2, 2, 2, 8, 16, 0, 2) W3(2, 2, 3, 2, 12, 16, 0, 0)
+        W3(2, 2, 4, 2, 16, 16, 0, 0) W3(4, 2, 2, 2, 16, 16, 0, 0) W3(2, 2, 4, 2, 8, 32, 0, 0)
+        W6(2, 2, 2, 2, 13, 8, 0, 0) W6(2, 2, 5, 2, 13, 20, 0, 0) W6(2, 2, 3, 2, 13, 12, 0, 0) W6(1, 2, 4, 2, 13, 8, 0, 0)
+        return 0;
+    }
     if (which == 13) {
         // data dependence: the same tiles on random bit patterns (the default
         // fill) and on properly split N(0,1) activations / N(0,0.05) weights
