@@ -222,6 +222,22 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         abase[i] = (r * PW + c) * 128;
         aph[i] = p + q;  // v = r*TW + c = p
     }
+    // AOFF (the fused first-layer kernel, which has VGPRs to spare): the
+    // lane's fragment addresses for all 8 swizzle residues precomputed, so a
+    // tap's A reads are a register plus an immediate offset (no per-read
+    // address arithmetic in the fully unrolled tap loop)
+#ifdef AA_NO_AOFF
+    constexpr bool AOFF = false;
+#else
+    constexpr bool AOFF = FUSED;
+#endif
+    int aoff[AOFF ? MF : 1][8];
+    if constexpr (AOFF) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) aoff[i][r] = abase[i] + (((aph[i] + r) & 7) << 4);
+    }
     int bofs[NF];  // byte offset of the lane's hi unit in a slice (lo: ^ 64)
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
@@ -306,9 +322,14 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             const int toff = (kh * PW + kw) * 128, tv = kh * TW + kw;
             bf16x8 h2[2], l2[2];
             auto rd = [&](int i, int k) {
-                const int a = abase[i] + toff + (((aph[i] + tv) & 7) << 4);
-                h2[k] = *reinterpret_cast<const bf16x8*>(patch + a);
-                l2[k] = *reinterpret_cast<const bf16x8*>(patch + (a ^ 64));
+                if constexpr (AOFF) {
+                    h2[k] = *reinterpret_cast<const bf16x8*>(patch + toff + aoff[i][tv & 7]);
+                    l2[k] = *reinterpret_cast<const bf16x8*>(patch + toff + aoff[i][(tv + 4) & 7]);
+                } else {
+                    const int a = abase[i] + toff + (((aph[i] + tv) & 7) << 4);
+                    h2[k] = *reinterpret_cast<const bf16x8*>(patch + a);
+                    l2[k] = *reinterpret_cast<const bf16x8*>(patch + (a ^ 64));
+                }
             };
             rd(0, 0);
 #pragma unroll
@@ -498,6 +519,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             }
         }
         if (!(DIAG & 2) && !AJIT) read_a(F0, 0);
+#pragma unroll
         for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); t += 2) {
             step(F0, F1, g, t);
             if (t + 1 < NTAP) step(F1, F0, g, t + 1);

@@ -8,6 +8,7 @@ usage: python tools/ab_build.py NAME X3TABLE WGTABLE [NAME X3TABLE WGTABLE ...]
   X3TABLE / WGTABLE: 'X(...) X(...) ...' for AA_X3_CFGS / AA_WG_CFGS, '-' keeps
   the in-tree table, '' an empty one
 writes tools/ab/libaa_NAME.so (the other objects come from the main build)."""
+import os
 import subprocess
 import sys
 from pathlib import Path
@@ -25,7 +26,8 @@ def build(name, table, wg="-"):
     obj = out / f"aa_cnn_{name}.o"
     cmd = [cc, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={_build.ARCH}", f"-I{_build.INCLUDE}",
            *([f"-DAA_X3_ALT(X)={table}"] if table != "-" else []),
-           *([f"-DAA_WG_ALT(X)={wg}"] if wg != "-" else []), "-c", str(_build.CSRC / "aa_cnn.hip"), "-o", str(obj)]
+           *([f"-DAA_WG_ALT(X)={wg}"] if wg != "-" else []),
+           *os.environ.get("AB_DEFS", "").split(), "-c", str(_build.CSRC / "aa_cnn.hip"), "-o", str(obj)]
     subprocess.run(cmd, check=True)
     objs = [_build.PKG.parent / "build" / (s.rsplit(".", 1)[0] + ".o") for s in _build.SOURCES if s != "aa_cnn.hip"]
     lib = out / f"libaa_{name}.so"

@@ -161,6 +161,11 @@ int main(int argc, char** argv) {
 #define W4(WM, WN, MF, NF, TH, TW, O, D) time_wg<3, 64, WM, WN, MF, NF, 1, TH, TW, O, true, true, D>("c4", n, 50, 72, 64, in, w, b, out, it);
 #define W3(WM, WN, MF, NF, TH, TW, O, D) time_wg<3, 32, WM, WN, MF, NF, 1, TH, TW, O, true, true, D>("c3", n, 52, 74, 64, in, w, b, out, it);
 #define W6(WM, WN, MF, NF, TH, TW, O, D) time_wg<1, 128, WM, WN, MF, NF, 1, TH, TW, O, true, false, D>("c6", n, 13, 22, 256, in, w, b, out, it);
+    if (which == 15) {  // the shipped 9x3 Winograd tile: staging / MFMA ablations
+        W5(2, 2, 4, 2, 39, 6, 2, 0) W5(2, 2, 4, 2, 39, 6, 2, 1) W5(2, 2, 4, 2, 39, 6, 2, 2) W5(2, 2, 4, 2, 39, 6, 2, 3)
+        C5(2, 2, 4, 2, 21, 6)
+        return 0;
+    }
     if (which == 14) {
         W5(2, 2, 2, 2, 21, 6, 0, 0) W5(2, 2, 2, 2, 21, 6, 0, 1) W5(2, 2, 2, 2, 21, 6, 0, 2) W5(2, 2, 2, 2, 21, 6, 0, 3)
         W5(2, 2, 4, 2, 39, 6, 0, 0) W5(2, 2, 4, 2, 39, 6, 2, 0) W5(4, 1, 2, 4, 21, 6, 0, 0) W5(2, 2, 2, 4, 21, 6, 0, 0)
