@@ -1174,7 +1174,7 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     X(fp8, 3, 3, 32, 1, 2, 2, 4, 2, 8, 16, true, 0)            \
     X(fp8, 3, 3, 64, 1, 4, 1, 3, 4, 12, 16, true, 0)           \
     X(fp8, 9, 3, 64, 3, 4, 2, 6, 4, 21, 18, true, 0)           \
-    X(fp8, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, false, 0)          \
+    X(fp8, 1, 3, 128, 1, 2, 4, 5, 2, 7, 20, true, 0)           \
     X(float, 3, 3, 32, 3, 2, 2, 9, 1, 6, 48, false, 0)         \
     X(float, 3, 3, 32, 1, 1, 4, 9, 1, 6, 24, false, 0)         \
     X(float, 3, 3, 64, 1, 1, 4, 9, 1, 6, 24, false, 0)         \

@@ -96,14 +96,18 @@ def _fp8(x):
 
 
 @torch.no_grad()
-def forward_fp8_emulated(path, x_nhwc: np.ndarray):
+def forward_fp8_emulated(path, x_nhwc: np.ndarray, first_bf16=True):
     """CPU emulation of libaa's AA_PREC_FP8 numerics (the checker of that mode,
     not a reference result): BN folded into the conv (per output channel), a
-    C_in = 1 first conv with bf16 weights on the f32 input, every later conv's
-    folded weights quantised per output channel to e4m3fn with the largest |w|
-    at 240 and dequantised after the f32 accumulation, pre-pool values rounded
-    to bf16 (the epilogue tile), every stored activation rounded to e4m3fn, f32
-    logits.  Returns (logits, probs)."""
+    C_in = 1 first conv with bf16 weights on the f32 input (first_bf16: the
+    fused first layer; False: f32 weights, the stand-alone conv_small), every
+    later conv's folded weights quantised per output channel to e4m3fn with
+    the largest |w| at 240 and dequantised after the f32 accumulation,
+    pre-pool values rounded to bf16 (the epilogue tile), every stored
+    activation rounded to e4m3fn.  A 1x1 conv followed by GlobalMaxPool2D is
+    the head kernel (max of the f32 values); any other conv followed by it
+    stores e4m3fn activations that the global max then reads.  Returns
+    (logits, probs)."""
     arch, tensors = load_arch(path)
     t = lambda k: torch.from_numpy(np.asarray(tensors[k])).to(torch.float64)
     x = torch.from_numpy(np.ascontiguousarray(x_nhwc)).to(torch.float32).permute(0, 3, 1, 2)
@@ -128,8 +132,12 @@ def forward_fp8_emulated(path, x_nhwc: np.ndarray):
             i += 1
         w, b = w.float(), b.float()
         first = w.shape[1] == 1
-        if first:
-            y = F.conv2d(x, w.to(torch.bfloat16).float(), b)
+        if first and first_bf16:
+            # the fused first layer: bf16 weights times the input as bf16 hi + lo
+            xh = x.to(torch.bfloat16).float()
+            y = F.conv2d(xh + (x - xh).to(torch.bfloat16).float(), w.to(torch.bfloat16).float(), b)
+        elif first:
+            y = F.conv2d(x, w, b)
         else:
             amax = w.abs().amax(dim=(1, 2, 3))
             s = torch.where(amax > 0, 240.0 / amax, torch.ones_like(amax))
@@ -145,7 +153,7 @@ def forward_fp8_emulated(path, x_nhwc: np.ndarray):
             elif k == "globalmaxpool2d":
                 head = True
             i += 1
-        if head:
+        if head and w.shape[2:] == (1, 1):
             logits = torch.amax(y, dim=(2, 3))
             if act is not None:
                 logits = F.leaky_relu(logits, act)
@@ -158,6 +166,12 @@ def forward_fp8_emulated(path, x_nhwc: np.ndarray):
         if act is not None:
             y = F.leaky_relu(y, act)
         x = _fp8(y)
+        if head:  # GlobalMaxPool2D over the stored e4m3fn activations
+            logits = torch.amax(x, dim=(2, 3))
+            if i < len(arch) and arch[i]["type"] == "activation":
+                i += 1
+            x = torch.sigmoid(logits)
+            break
     return logits.numpy(), x.numpy()
 
 

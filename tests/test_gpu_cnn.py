@@ -18,14 +18,14 @@ from tools.make_models import calibration_input, make_model
 pytestmark = pytest.mark.gpu
 
 LOGIT_TOL = 1e-3
-# fp8 vs its emulation: e4m3 rounding ties flip where the f32 summation
-# orders differ (one e4m3 step is 6 % of the value) and the flips compound
-# through six layers: 3e-8 relative noise on each layer's pre-rounding values
-# (the scale of f32 summation-order differences) moves the emulation's own
-# logits by up to 0.40 (mean 0.096) on this input, so the gate is the mean
-# at that floor with a loose cap on the max
-FP8_EMU_MAX = 0.6
-FP8_EMU_MEAN = 0.15
+# fp8 vs its emulation, whole network: e4m3 rounding ties flip where the f32
+# summation orders differ (one e4m3 step is 6-12 % of the value) and the flips
+# compound through six layers (measured: max 0.18-0.27, mean 0.045-0.054 on
+# model1/model2/MagTransform).  Each kernel alone is gated tightly below
+# (test_fp8_kernel_chains_match_emulation: >= 97 % of logits bit-equal, the
+# rest one e4m3 step).
+FP8_EMU_MAX = 0.45
+FP8_EMU_MEAN = 0.08
 
 
 def _run(path, x, precision):
@@ -138,3 +138,34 @@ def test_track_mean_matches_numpy(gpu):
         seg = probs[:, begin[t]:begin[t] + count[t]]
         ref = np.mean(np.mean(list(seg), axis=0), axis=0)
         assert np.array_equal(out[t], ref), t
+
+
+# ---- fp8, one conv kernel at a time (tight gate) ----
+# Short chains ending in GlobalMaxPool2D over the stored e4m3fn activations:
+# the logits ARE e4m3fn values, so GPU and emulation agree exactly unless a
+# rounding tie (e4m3 or the bf16 epilogue tile) falls differently under the
+# two summation orders -- rare, and then one e4m3 step (<= 1/8 relative) at
+# the maximum.  Each chain adds one tuned fp8 kernel to the previous one.
+FP8_CHAINS = {
+    "3x3_32_k32": [(32, (3, 3), None), (64, (3, 3), None)],
+    "3x3_64_k128": [(32, (3, 3), None), (64, (3, 3), None), (64, (3, 3), None)],
+    "9x3_64_k128": [(32, (3, 3), None), (64, (3, 3), None), (128, (9, 3), (3, 3))],
+    "fused_first": [(32, (3, 3), None), (32, (3, 3), (3, 3)), (64, (3, 3), None)],
+    "1x3_128_k128": [(32, (3, 3), None), (128, (3, 3), None), (256, (1, 3), None)],
+}
+
+
+@pytest.mark.parametrize("chain", sorted(FP8_CHAINS))
+def test_fp8_kernel_chains_match_emulation(gpu, tmp_path, chain):
+    from tools.make_models import make_chain
+    path = make_chain(tmp_path / chain, FP8_CHAINS[chain], seed=5)
+    x = calibration_input(6, 160, 226, True, np.random.default_rng(8))
+    lg, _ = _run(path, x, "fp8")
+    elg, _ = cnn_oracle.forward_fp8_emulated(path, x, first_bf16=(chain == "fused_first"))
+    d = np.abs(lg - elg)
+    rel = d / np.maximum(np.abs(elg), 2.0 ** -6)  # (e4m3 subnormals below 2^-6 have absolute steps)
+    exact = float((lg == elg).mean())
+    print(f"{chain}: fp8 logits equal to the emulation {100 * exact:.1f} %, max rel diff {rel.max():.3e} "
+          f"(max abs {d.max():.3e}, logit range {elg.min():.2f}..{elg.max():.2f})")
+    assert np.isfinite(lg).all()
+    assert exact >= 0.97 and rel.max() <= 0.135

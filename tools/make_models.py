@@ -163,6 +163,35 @@ def calibration_input(n, n_mels, T, db_scale, rng):
     return x.astype(np.float32)
 
 
+def make_chain(out_dir, blocks, seed=1, n_mels=160, T=226, alpha=0.3):
+    """A conv chain ending in GlobalMaxPool2D (no 1x1 head): ``blocks`` =
+    [(filters, (kh, kw), pool or None), ...], each conv + BN + LeakyReLU
+    [+ MaxPooling2D]; the last conv carries the bias the calibration centres.
+    For layer-by-layer checks of single conv kernels (tests/)."""
+    from safetensors.numpy import save_file
+    arch = []
+    for i, (f, k, pool) in enumerate(blocks, 1):
+        arch.append({"type": "conv2d", "name": f"conv{i}", "filters": f, "kernel": list(k),
+                     "use_bias": i == len(blocks)})
+        arch.append({"type": "batchnorm", "name": f"bn{i}", "eps": 1e-3})
+        arch.append({"type": "leakyrelu", "alpha": alpha})
+        if pool:
+            arch.append({"type": "maxpool2d", "pool": list(pool)})
+    arch.append({"type": "globalmaxpool2d"})
+    rng = np.random.default_rng(seed)
+    tensors = _init_weights(arch, 1, rng)
+    tensors = _calibrate(arch, tensors, calibration_input(4, n_mels, T, True, rng), rng)
+    out = Path(out_dir)
+    out.mkdir(parents=True, exist_ok=True)
+    save_file({k: np.ascontiguousarray(v) for k, v in tensors.items()},
+              str(out / "audioModel.safetensors"), metadata={"arch": json.dumps(arch)})
+    meta = dict(DEFAULT_META)
+    meta.update({"name": "chain", "labels": [f"c{i}" for i in range(blocks[-1][0])]})
+    with open(out / "metadata.txt", "w") as f:
+        json.dump(meta, f, indent=2)
+    return out / "audioModel.safetensors"
+
+
 def make_model(out_dir, name="model1", seed=1, widths=(32, 32, 64, 64, 128, 256),
                labels=None, mag=None, meta_overrides=None, pre_model=False, in_channels=None):
     """Create ``out_dir/audioModel.safetensors`` + ``out_dir/metadata.txt``.
