@@ -65,8 +65,9 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* patch = smem;
 
-    const int n = blockIdx.z;
-    const int th = blockIdx.x / tiles_w, tw = blockIdx.x - (blockIdx.x / tiles_w) * tiles_w;
+    const BlockPos bp = x3_block<true>();
+    const int n = bp.n, cb = bp.cb;
+    const int th = bp.tile / tiles_w, tw = bp.tile - (bp.tile / tiles_w) * tiles_w;
     const int oh0 = th * TH, ow0 = tw * TW;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -88,7 +89,7 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         bofs[j] = row * 128 + (((q + row) & 7) << 4);
     }
     const size_t step_stride = (size_t)gridDim.y * SLICE;
-    const bf16* wblk = wt + (size_t)blockIdx.y * SLICE;
+    const bf16* wblk = wt + (size_t)cb * SLICE;
 
     f32x4 acc[4][MF][NF];
 #pragma unroll
@@ -211,7 +212,8 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         }
     }
     __syncthreads();
-    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, false>(E, bias, out, n, oh0, ow0, Hout, Wout, cout_store, act, alpha);
+    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, false>(E, bias, out, n, cb, oh0, ow0, Hout, Wout, cout_store, act,
+                                                      alpha);
 }
 
 }  // namespace aa

@@ -83,20 +83,46 @@ __device__ __forceinline__ int x3_addr(int R, int C, int u, int PW, int TW) {
     return (R * PW + C) * 128 + (((u + R * TW + C) & 7) << 4);
 }
 
+// XCD-aware block order (split-bf16 kernels): the dispatcher places block L
+// (linear id) on XCD L % 8, so consecutive linear ids land on different L2s.
+// Renumber so each XCD works through a contiguous range of (window, tile,
+// channel block) with the channel block fastest: the blocks that stage the
+// same input patch (all channel blocks of a tile) and its neighbours (the
+// next tiles, which share the halo) meet in the same L2.  In-pipeline A/B:
+// the Winograd 9x3 kernel (two channel blocks per tile) gains a little, the
+// conv_x3 kernels lose a little (-0.8 % on the step when all remap), so only
+// conv_wg remaps.
+struct BlockPos {
+    int tile, cb, n;
+};
+template <bool REMAP>
+__device__ __forceinline__ BlockPos x3_block() {
+    const int gx = gridDim.x, gy = gridDim.y, G = gx * gy * gridDim.z;
+    int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    if (REMAP && (G & 7) == 0) L = (L & 7) * (G >> 3) + (L >> 3);
+    BlockPos b;
+    b.cb = L % gy;
+    const int r = L / gy;
+    b.tile = r % gx;
+    b.n = r / gx;
+    return b;
+}
+
 // Epilogue shared by the split-bf16 kernels: the f32 tile E [TH*TW][BN+4]
 // (bias not yet added) -> POOL x POOL max, bias, activation, and the NHWC
 // store (f32, or the grouped-split layout when OUT_SPLIT).  One thread per
 // (pooled pixel, 8-channel group).
 template <int TH, int TW, int POOL, int BN, int NTHR, bool OUT_SPLIT, bool NOSTORE>
 __device__ __forceinline__ void x3_store(const float* E, const float* __restrict__ bias, float* __restrict__ out, int n,
-                                         int oh0, int ow0, int Hout, int Wout, int cout_store, int act, float alpha) {
+                                         int cb, int oh0, int ow0, int Hout, int Wout, int cout_store, int act,
+                                         float alpha) {
     constexpr int ESTR = BN + 4;
     constexpr int PHo = TH / POOL, PWo = TW / POOL;
     constexpr int G = BN / 8;
     static_assert(NTHR % G == 0, "fixed channel group per thread");
     const int oh0s = oh0 / POOL, ow0s = ow0 / POOL;
     const int col = (threadIdx.x % G) * 8;
-    const int ch0 = blockIdx.y * BN + col;
+    const int ch0 = cb * BN + col;
     float bv[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) bv[c] = bias[ch0 + c];  // bias is padded to cout_pad
@@ -186,15 +212,16 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     char* patch = smem;
     char* Bs = smem + x3_patch_bytes<KH, KW, TH, TW, FUSED>();
 
-    const int n = blockIdx.z;
-    const int th = blockIdx.x / tiles_w, tw = blockIdx.x - (blockIdx.x / tiles_w) * tiles_w;
+    const BlockPos bp = x3_block<false>();
+    const int n = bp.n, cb = bp.cb;
+    const int th = bp.tile / tiles_w, tw = bp.tile - (bp.tile / tiles_w) * tiles_w;
     const int oh0 = th * TH, ow0 = tw * TW;
     const int wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
 
     // weight ring: slice of step s = wt[s][cout_pad][64] rows of this block
     const size_t step_stride = (size_t)gridDim.y * SLICE;
-    const bf16* wsl = wt + (size_t)blockIdx.y * SLICE + lane * 8;
+    const bf16* wsl = wt + (size_t)cb * SLICE + lane * 8;
 #define X3_GLDS(s)                                                                                       \
     _Pragma("unroll") for (int u_ = 0; u_ < GHI; ++u_) {                                               \
         const int g_ = u_ * NW + wave0;                                                                  \
@@ -244,7 +271,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         const int row = wn * NF * 16 + j * 16 + (lane & 15);
         bofs[j] = row * 128 + (((q + row) & 7) << 4);
     }
-    const bf16* wblk = wt + (size_t)blockIdx.y * SLICE;  // RING = false: this block's rows of step 0
+    const bf16* wblk = wt + (size_t)cb * SLICE;  // RING = false: this block's rows of step 0
     const bool hi_share = (GPS % NW == 0) || wave < GPS % NW;
 
     f32x4 acc[MF][NF];
@@ -543,7 +570,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         }
     }
     __syncthreads();
-    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, (DIAG & 4) != 0>(E, bias, out, n, oh0, ow0, Hout, Wout, cout_store, act,
+    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, (DIAG & 4) != 0>(E, bias, out, n, cb, oh0, ow0, Hout, Wout, cout_store, act,
                                                                alpha);
 }
 
