@@ -25,20 +25,26 @@ def decode(path):
         data = f.read()
     if len(data) < 12 or data[:4] not in (b"RIFF", b"RF64") or data[8:12] != b"WAVE":
         raise ValueError(f"{path}: not a RIFF/WAVE file")
+    mv = memoryview(data)  # chunk bodies as views: no copy of the sample payload
     pos, fmt, payload = 12, None, None
     while pos + 8 <= len(data):
         cid, size = data[pos:pos + 4], struct.unpack("<I", data[pos + 4:pos + 8])[0]
-        body = data[pos + 8:pos + 8 + size]
+        body = mv[pos + 8:pos + 8 + size]
         if cid == b"fmt ":
-            fmt = struct.unpack("<HHIIHH", body[:16])
+            fmt = struct.unpack("<HHIIHH", bytes(body[:16]))
             if fmt[0] == 0xFFFE and len(body) >= 26:  # WAVE_FORMAT_EXTENSIBLE: real tag in the GUID
-                fmt = (struct.unpack("<H", body[24:26])[0],) + fmt[1:]
+                fmt = (struct.unpack("<H", bytes(body[24:26]))[0],) + fmt[1:]
         elif cid == b"data":
             payload = body
         pos += 8 + size + (size & 1)
     if fmt is None or payload is None:
         raise ValueError(f"{path}: missing fmt/data chunk")
     tag, channels, sr, _, _, bits = fmt
+    if tag == 1 and bits == 16:  # the common case in one pass: x = s16 * 2^-15 (== s16 / 32768 exactly)
+        x = np.frombuffer(payload, "<i2", count=len(payload) // 2).astype(np.float32) * np.float32(1.0 / 32768.0)
+        if channels > 1:
+            x = x[: len(x) // channels * channels].reshape(-1, channels).mean(axis=1, dtype=np.float32)
+        return np.ascontiguousarray(x, dtype=np.float32), int(sr)
     if tag == 1:  # PCM -> ffmpeg's s16
         if bits == 8:
             q = (np.frombuffer(payload, np.uint8).astype(np.int32) - 128) << 8

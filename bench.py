@@ -76,10 +76,12 @@ def parse(argv=None):
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="CPU-baseline processes for the numpy front end (the GPU box's CPU share is 16)")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4],
                     help="2: the 64-window step (BASELINE configs[1], the headline); 3: streamed 60 s clips "
-                         "through the model1+2+3 ensemble (configs[2]), PCM uploaded from pinned host memory")
+                         "through the model1+2+3 ensemble (configs[2]), PCM uploaded from pinned host memory; "
+                         "4: a corpus of 60 s WAV files through the whole analyse path (configs[3])")
     ap.add_argument("--clips", type=int, default=1000, help="--config 3: clips per rank")
+    ap.add_argument("--files", type=int, default=32, help="--config 4: files per rank")
     return ap.parse_args(argv)
 
 
@@ -430,6 +432,55 @@ def main_stream(args, world, rank, dev):
         print(json.dumps(out), flush=True)
 
 
+def main_corpus(args, world, rank, dev):
+    """configs[3]: a corpus of 60 s WAV files through the whole analyse path
+    (aa_amd.corpus: decode, signal_noise, tracks, classify() with model1,
+    post-processing to the reference's per-file JSON), files sharded one per
+    stream across ranks and the JSON documents all-gathered (RCCL) at the end.
+    value = files x 60 s over all ranks / max-over-ranks wall time, including
+    the file reads and the host-side steps the reference runs on the CPU."""
+    from aa_amd import corpus
+    from tools import synth
+    from tools.make_models import make_model
+    root = Path(tempfile.mkdtemp(prefix="aa_bench4_"))
+    model = make_model(root / "model1", "model1", seed=1)
+    n = args.files
+    files = []
+    for i in range(n * world):  # every rank writes the whole (small) corpus into its own temp dir
+        p = root / f"clip{i:05d}.wav"
+        if i % world == rank or i == 0:
+            synth.write_wav(p, synth.clip(5000 + i))
+        files.append(p)
+    models = [str(model)]
+    corpus.run([files[0]], models, rank=0, world=1)  # warm-up: plans, kernels, model upload (untimed)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    res = corpus.run(files, models, rank=rank, world=world, device=dev if world > 1 else None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    assert len(res) == n * world
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    n_pred = sum(len(r.get("species_identify", [])) for r in res.values())
+    out = {"metric": METRIC, "value": round(n * world * 60.0 / elapsed, 1), "unit": "audio-s/s", "n_gpus": world,
+           "steps": n, "warmup": 1, "ms_per_step": round(1e3 * elapsed / n, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "bf16x3",
+           "data": "synthetic 60 s 48 kHz int16 WAV files (noise+chirps, seeded), seeded random-init model1",
+           "config": {"workload": "config4: corpus of 60 s WAV files through analyse.examine (decode, "
+                                  "signal_noise, tracks, classify, species JSON), one file per stream, "
+                                  "JSON all-gathered", "model": "model1", "global_batch": world,
+                      "seq_len": 48000 * 60, "parallelism": f"dp{world}", "files_per_rank": n,
+                      "documents_gathered": len(res), "tracks_classified": n_pred}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def worker(local, world, args, port=None):
     """One rank.  ``port`` set: spawned by ``--gpus N`` (no torchrun env)."""
     if port is not None:
@@ -445,6 +496,8 @@ def worker(local, world, args, port=None):
     try:
         if args.config == 3:
             main_stream(args, world, rank, dev)
+        elif args.config == 4:
+            main_corpus(args, world, rank, dev)
         else:
             main_step(args, world, rank, dev)
     finally:
