@@ -1026,7 +1026,10 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
                            p->cfg.n_mels, p->T, p->cfg.db_scale, p->cfg.amin, p->cfg.top_db, ws.band_mean);
         AA_LAUNCH_CHECK();
     }
-    int tile_t = 32;  // frames per fe_db block (the [tile_t][n_mels + 1] tile within 64 KiB)
+#ifndef AA_FE_DB_TILE
+#define AA_FE_DB_TILE 16
+#endif
+    int tile_t = AA_FE_DB_TILE;  // frames per fe_db block (the [tile_t][n_mels + 1] tile within 64 KiB)
     while (tile_t > 1 && (size_t)tile_t * (p->cfg.n_mels + 1) * 4 > 65536) tile_t >>= 1;
     if (p->cfg.out_f16) {
         hipLaunchKernelGGL(fe_db<_Float16>, dim3((p->T + tile_t - 1) / tile_t, n_win), dim3(256),

@@ -29,7 +29,14 @@ def build(name, table, wg="-"):
            *([f"-DAA_WG_ALT(X)={wg}"] if wg != "-" else []),
            *os.environ.get("AB_DEFS", "").split(), "-c", str(_build.CSRC / "aa_cnn.hip"), "-o", str(obj)]
     subprocess.run(cmd, check=True)
-    objs = [_build.PKG.parent / "build" / (s.rsplit(".", 1)[0] + ".o") for s in _build.SOURCES if s != "aa_cnn.hip"]
+    objs = [_build.PKG.parent / "build" / (s.rsplit(".", 1)[0] + ".o") for s in _build.SOURCES
+            if s != "aa_cnn.hip" and not (s == "aa_frontend.hip" and os.environ.get("AB_FE_DEFS"))]
+    if os.environ.get("AB_FE_DEFS"):  # a front-end variant too
+        fo = out / f"aa_frontend_{name}.o"
+        subprocess.run([cc, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={_build.ARCH}", f"-I{_build.INCLUDE}",
+                        *_build.EXTRA_FLAGS.get("aa_frontend.hip", []), *os.environ["AB_FE_DEFS"].split(), "-c",
+                        str(_build.CSRC / "aa_frontend.hip"), "-o", str(fo)], check=True)
+        objs.append(fo)
     lib = out / f"libaa_{name}.so"
     subprocess.run([cc, f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", str(obj), *map(str, objs), "-o",
                     str(lib)], check=True)

@@ -161,6 +161,19 @@ int main(int argc, char** argv) {
 #define W4(WM, WN, MF, NF, TH, TW, O, D) time_wg<3, 64, WM, WN, MF, NF, 1, TH, TW, O, true, true, D>("c4", n, 50, 72, 64, in, w, b, out, it);
 #define W3(WM, WN, MF, NF, TH, TW, O, D) time_wg<3, 32, WM, WN, MF, NF, 1, TH, TW, O, true, true, D>("c3", n, 52, 74, 64, in, w, b, out, it);
 #define W6(WM, WN, MF, NF, TH, TW, O, D) time_wg<1, 128, WM, WN, MF, NF, 1, TH, TW, O, true, false, D>("c6", n, 13, 22, 256, in, w, b, out, it);
+    if (which == 18) {  // LDS bank conflicts of the fused kernel by phase (PMC): full, no conv1 compute, no MFMA loop
+        ABL2(66) ABL2(70) ABL2(578) ABL2(582)
+        return 0;
+    }
+    if (which == 17) {  // the shipped fused first conv and Winograd 9x3 once each (PMC passes)
+        time_one<3, 3, 32, 4, 1, 3, 2, 3, 9, 21, true, 0, false, true, 4, false, true>("c2", n, 158, 224, 32, in, w, b, out, f1, 1);
+        W5(2, 2, 4, 2, 39, 6, 2, 0)
+        return 0;
+    }
+    if (which == 16) {  // the fused first conv: B latency (16: weights of step 0 re-read, L1-resident)
+        ABL2(0) ABL2(16) ABL2(128) ABL2(144) ABL2(1) ABL2(17) ABL2(2)
+        return 0;
+    }
     if (which == 15) {  // the shipped 9x3 Winograd tile: staging / MFMA ablations
         W5(2, 2, 4, 2, 39, 6, 2, 0) W5(2, 2, 4, 2, 39, 6, 2, 1) W5(2, 2, 4, 2, 39, 6, 2, 2) W5(2, 2, 4, 2, 39, 6, 2, 3)
         C5(2, 2, 4, 2, 21, 6)

@@ -11,7 +11,7 @@ for path in sys.argv[1:]:
         meta = {}
         for r in rows:
             agg[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-            meta[r["Dispatch_Id"]] = (r["Kernel_Name"][:50], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            meta[r["Dispatch_Id"]] = (r["Kernel_Name"][:110], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         last = {}
         for d, (k, _) in meta.items():
             if k not in last or int(d) > int(last[k]):
