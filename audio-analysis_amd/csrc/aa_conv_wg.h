@@ -89,7 +89,7 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         bofs[j] = row * 128 + (((q + row) & 7) << 4);
     }
     const size_t step_stride = (size_t)gridDim.y * SLICE;
-    const bf16* wblk = wt + (size_t)cb * SLICE;
+    const __amdgpu_buffer_rsrc_t wrs = x3_wrsrc(wt);
 
     f32x4 acc[4][MF][NF];
 #pragma unroll
@@ -104,11 +104,11 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     };
     BSet B0, B1;
     auto read_b = [&](BSet& b, int s) {
-        const char* bsl = reinterpret_cast<const char*>(wblk + (size_t)s * step_stride);
+        const int soff = __builtin_amdgcn_readfirstlane((int)((cb * SLICE + s * step_stride) * 2));
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
-            b.h[j] = *reinterpret_cast<const bf16x8*>(bsl + bofs[j]);
-            b.l[j] = *reinterpret_cast<const bf16x8*>(bsl + (bofs[j] ^ 64));
+            b.h[j] = x3_wload(wrs, bofs[j], soff);
+            b.l[j] = x3_wload(wrs, bofs[j] ^ 64, soff);
         }
     };
     // one step: plane e at row offset kh, B of this step in `cur`, the next

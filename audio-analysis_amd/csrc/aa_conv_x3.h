@@ -108,6 +108,17 @@ __device__ __forceinline__ BlockPos x3_block() {
     return b;
 }
 
+// A weight fragment (16 B) through a buffer resource over the packed weights:
+// the per-lane part of the address (row, swizzled unit) is a VGPR that stays
+// fixed across steps, the step's slice base a wave-uniform SGPR offset -- no
+// 64-bit address arithmetic per load in the unrolled step loop.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t x3_wrsrc(const void* wt) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(wt), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ bf16x8 x3_wload(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
 // Epilogue shared by the split-bf16 kernels: the f32 tile E [TH*TW][BN+4]
 // (bias not yet added) -> POOL x POOL max, bias, activation, and the NHWC
 // store (f32, or the grouped-split layout when OUT_SPLIT).  One thread per
@@ -271,7 +282,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         const int row = wn * NF * 16 + j * 16 + (lane & 15);
         bofs[j] = row * 128 + (((q + row) & 7) << 4);
     }
-    const bf16* wblk = wt + (size_t)cb * SLICE;  // RING = false: this block's rows of step 0
+    const __amdgpu_buffer_rsrc_t wrs = x3_wrsrc(wt);  // RING = false: B fragments by buffer loads
     const bool hi_share = (GPS % NW == 0) || wave < GPS % NW;
 
     f32x4 acc[MF][NF];
@@ -298,11 +309,11 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     auto read_b = [&](FragSet& f, int s) {
         if (DIAG & 128) return;
         if constexpr (!RING) {
-            const char* bsl = reinterpret_cast<const char*>(wblk + (size_t)((DIAG & 16) ? 0 : s) * step_stride);
+            const int soff = __builtin_amdgcn_readfirstlane((int)((cb * SLICE + ((DIAG & 16) ? 0 : s) * step_stride) * 2));
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
-                f.bh[j] = *reinterpret_cast<const bf16x8*>(bsl + bofs[j]);
-                f.bl[j] = *reinterpret_cast<const bf16x8*>(bsl + (bofs[j] ^ 64));
+                f.bh[j] = x3_wload(wrs, bofs[j], soff);
+                f.bl[j] = x3_wload(wrs, bofs[j] ^ 64, soff);
             }
             return;
         }
