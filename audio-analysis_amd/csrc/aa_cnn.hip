@@ -1246,6 +1246,9 @@ template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int
 static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream_t st, const Stage* first) {
     auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, RING, AJIT, OCC, IN_SPLIT, OUT_SPLIT>;
     constexpr int BN = WN * NF * 16;
+    // buffer-resource addressing (32-bit byte offsets) of activations and weights
+    AA_CHECK((double)n * s.Hin * s.Win * s.cin * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
+             "conv %s: batch %d too large for one launch", s.name.c_str(), n);
     const size_t lds = x3_lds_bytes<KH, KW, CIN, BN, TH, TW, FUSED, RING>();
     FirstConv fc{};
     if (FUSED) {
@@ -1273,6 +1276,8 @@ template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int
 static int launch_wg(const Stage& s, const void* in, void* out, int n, hipStream_t st) {
     auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IN_SPLIT, OUT_SPLIT>;
     constexpr int BN = WN * NF * 16;
+    AA_CHECK((double)n * s.Hin * s.Win * s.cin * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
+             "conv %s: batch %d too large for one launch", s.name.c_str(), n);
     const size_t lds = wg_lds_bytes<KH, BN, TH, TW>();
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
     static size_t attr = 0;

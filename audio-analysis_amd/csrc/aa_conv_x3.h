@@ -232,14 +232,14 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
 
     // weight ring: slice of step s = wt[s][cout_pad][64] rows of this block
     const size_t step_stride = (size_t)gridDim.y * SLICE;
-    const bf16* wsl = wt + (size_t)cb * SLICE + lane * 8;
+    const __amdgpu_buffer_rsrc_t wrs = x3_wrsrc(wt);  // weight slices / fragments by buffer loads
 #define X3_GLDS(s)                                                                                       \
     _Pragma("unroll") for (int u_ = 0; u_ < GHI; ++u_) {                                               \
         const int g_ = u_ * NW + wave0;                                                                  \
         if (GPS % NW == 0 || g_ < GPS)                                                                  \
-            __builtin_amdgcn_global_load_lds(                                                           \
-                (const __attribute__((address_space(1))) void*)(wsl + (size_t)(s) * step_stride + g_ * 512), \
-                (__attribute__((address_space(3))) void*)(Bs + ((s) % NB) * SLICE_LDS + g_ * 1024), 16, 0, 0); \
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                   \
+                wrs, (__attribute__((address_space(3))) void*)(Bs + ((s) % NB) * SLICE_LDS + g_ * 1024), 16,   \
+                lane * 16, __builtin_amdgcn_readfirstlane((int)((cb * SLICE + (s) * step_stride + g_ * 512) * 2)), 0, 0); \
     }
     if constexpr (RING && !(DIAG & 32)) {
 #pragma unroll
@@ -282,7 +282,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         const int row = wn * NF * 16 + j * 16 + (lane & 15);
         bofs[j] = row * 128 + (((q + row) & 7) << 4);
     }
-    const __amdgpu_buffer_rsrc_t wrs = x3_wrsrc(wt);  // RING = false: B fragments by buffer loads
+
     const bool hi_share = (GPS % NW == 0) || wave < GPS % NW;
 
     f32x4 acc[MF][NF];
@@ -394,7 +394,10 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             // (slot - R*TW - C) & 7 of pixel (R, C).  Out-of-image pixels read a
             // clamped (finite) pixel: they only feed discarded outputs.
             constexpr int UNITS = PH * PW * 8;
-            const char* src = reinterpret_cast<const char*>(in) + (size_t)n * Hin * Win * CIN * 4 + g * 128;
+            // buffer loads: the window's and group's base in the SGPR offset,
+            // the pixel / unit in the lane's VGPR offset
+            const __amdgpu_buffer_rsrc_t ars = x3_wrsrc(in);
+            const int abase_s = __builtin_amdgcn_readfirstlane(n * Hin * Win * CIN * 4 + g * 128);
             for (int i0 = wave0 * 64; i0 < UNITS; i0 += NW * 64) {
                 const int idx = i0 + lane;
                 if (idx < UNITS) {
@@ -402,9 +405,8 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                     const int R = pix / PW, C = pix - R * PW;
                     const int u = (slot - R * TW - C) & 7;
                     const int gh = min(oh0 + R, Hin - 1), gw = min(ow0 + C, Win - 1);
-                    __builtin_amdgcn_global_load_lds(
-                        (const __attribute__((address_space(1))) void*)(src + ((size_t)gh * Win + gw) * (CIN * 4) + u * 16),
-                        (__attribute__((address_space(3))) void*)(patch + i0 * 16), 16, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)(patch + i0 * 16),
+                                                             16, (gh * Win + gw) * (CIN * 4) + u * 16, abase_s, 0, 0);
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
