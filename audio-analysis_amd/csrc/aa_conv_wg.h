@@ -138,15 +138,21 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     };
 
     // one input value quad (4 channels of group g) of pixel (gh, gw), in f32
+    // (buffer loads: the window's base in an SGPR offset, the pixel in the lane's 32-bit offset)
+    const __amdgpu_buffer_rsrc_t ars = x3_wrsrc(in);
+    const int wbase = __builtin_amdgcn_readfirstlane(n * Hin * Win * CIN * 4);
     auto load4 = [&](int gh, int gw, int g, int cq) -> float4 {
-        const size_t pix = ((size_t)n * Hin + gh) * Win + gw;
+        const int pix = gh * Win + gw;
         if constexpr (IN_SPLIT) {
-            const char* b = reinterpret_cast<const char*>(in) + pix * (CIN * 4) + g * 128 + cq * 8;
-            const bf16x4 h = *reinterpret_cast<const bf16x4*>(b), l = *reinterpret_cast<const bf16x4*>(b + 64);
+            const int o = pix * (CIN * 4) + g * 128 + cq * 8;
+            typedef __attribute__((ext_vector_type(2))) int i32x2;
+            const bf16x4 h = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(ars, o, wbase, 0));
+            const bf16x4 l = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(ars, o + 64, wbase, 0));
             return make_float4((float)h[0] + (float)l[0], (float)h[1] + (float)l[1], (float)h[2] + (float)l[2],
                                (float)h[3] + (float)l[3]);
         } else {
-            return *reinterpret_cast<const float4*>(in + pix * CIN + g * 32 + cq * 4);
+            return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ars, (pix * CIN + g * 32 + cq * 4) * 4,
+                                                                                     wbase, 0));
         }
     };
 

@@ -456,15 +456,19 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             // in k, the bias as C), activation, hi/lo into the swizzled patch
             constexpr int XW = PW + 2, XN = (PH + 2) * XW;
             float* X = reinterpret_cast<float*>(smem + (size_t)PH * PW * 128);
-            const size_t lmo = (size_t)n * fc.H0 * fc.W0;
+            // buffer loads: the window's base in an SGPR offset, the element in the lane's offset
+            const __amdgpu_buffer_rsrc_t lrs = x3_wrsrc(in);
+            const int esz = fc.lm_f16 ? 2 : 4;
+            const int lbase = __builtin_amdgcn_readfirstlane(n * fc.H0 * fc.W0 * esz);
             for (int i0 = 0; i0 < ((DIAG & 512) ? 0 : XN); i0 += 4 * NTHR) {
                 float v[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int idx = min(i0 + u * NTHR + (int)threadIdx.x, XN - 1);
                     const int r = idx / XW, c = idx - r * XW;
-                    v[u] = load_lm(in, lmo + (size_t)min(oh0 + r, fc.H0 - 1) * fc.W0 + min(ow0 + c, fc.W0 - 1),
-                                   fc.lm_f16);
+                    const int e = min(oh0 + r, fc.H0 - 1) * fc.W0 + min(ow0 + c, fc.W0 - 1);
+                    v[u] = fc.lm_f16 ? (float)__builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(lrs, e * 2, lbase, 0))
+                                     : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lrs, e * 4, lbase, 0));
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
