@@ -177,14 +177,12 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             const int unit = (((cq >> 1) + v) & 7) << 4;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                bf16x4 h, l;
-                h[0] = bf_hi(u[e].x); l[0] = bf_lo(u[e].x);
-                h[1] = bf_hi(u[e].y); l[1] = bf_lo(u[e].y);
-                h[2] = bf_hi(u[e].z); l[2] = bf_lo(u[e].z);
-                h[3] = bf_hi(u[e].w); l[3] = bf_lo(u[e].w);
+                uint32_t h0, l0, h1, l1;
+                split2(u[e].x, u[e].y, h0, l0);
+                split2(u[e].z, u[e].w, h1, l1);
                 const int a = (e * PV + v) * 128 + unit + (cq & 1) * 8;
-                *reinterpret_cast<bf16x4*>(patch + a) = h;
-                *reinterpret_cast<bf16x4*>(patch + (a ^ 64)) = l;
+                *reinterpret_cast<uint2*>(patch + a) = make_uint2(h0, h1);
+                *reinterpret_cast<uint2*>(patch + (a ^ 64)) = make_uint2(l0, l1);
             }
         }
         __syncthreads();

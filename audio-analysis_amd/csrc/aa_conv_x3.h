@@ -78,6 +78,34 @@ constexpr int x3_waves_per_simd() {
     return w < 1 ? 1 : (w > 8 ? 8 : w);
 }
 
+// Two f32 values as packed bf16 hi and lo words (5 VALU ops)
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+    const f2 o = f2{x0, x1};
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(o, b2));
+    const f2 hf = f2{__uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(o - hf, b2));
+}
+
+// Two activations max(x, a x) (0 <= a <= 1) as packed bf16 hi and lo
+// words, in 8 VALU ops: one packed multiply, two raw maxes (no NaN
+// canonicalisation: the inputs are MFMA results), one packed conversion for
+// hi, its two halves back to f32 (shift / mask), one packed subtract, one
+// packed conversion for lo.
+__device__ __forceinline__ void leaky_split2(float x0, float x1, float a, uint32_t& hi, uint32_t& lo) {
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+    const f2 s = f2{x0, x1} * a;
+    float o0, o1;
+    asm("v_max_f32 %0, %1, %2" : "=v"(o0) : "v"(x0), "v"(s.x));
+    asm("v_max_f32 %0, %1, %2" : "=v"(o1) : "v"(x1), "v"(s.y));
+    const f2 o = f2{o0, o1};
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(o, b2));
+    const f2 hf = f2{__uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(o - hf, b2));
+}
+
 // byte offset of unit u of patch pixel (R, C)
 __device__ __forceinline__ int x3_addr(int R, int C, int u, int PW, int TW) {
     return (R * PW + C) * 128 + (((u + R * TW + C) & 7) << 4);
@@ -165,14 +193,11 @@ __device__ __forceinline__ void x3_store(const float* E, const float* __restrict
             if (ch0 < cout_store) {
                 char* o = reinterpret_cast<char*>(out) + ((size_t)n * Hout * Wout + (size_t)gh * Wout + gw) * cout_store * 4 +
                           (ch0 >> 5) * 128 + (ch0 & 31) * 2;
-                bf16x8 h, l;
+                uint32_t h[4], l[4];
 #pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    h[c] = bf_hi(v[c]);
-                    l[c] = bf_lo(v[c]);
-                }
-                *reinterpret_cast<bf16x8*>(o) = h;
-                *reinterpret_cast<bf16x8*>(o + 64) = l;
+                for (int c = 0; c < 4; ++c) split2(v[2 * c], v[2 * c + 1], h[c], l[c]);
+                *reinterpret_cast<uint4*>(o) = make_uint4(h[0], h[1], h[2], h[3]);
+                *reinterpret_cast<uint4*>(o + 64) = make_uint4(l[0], l[1], l[2], l[3]);
             }
         } else {
             float* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
@@ -524,16 +549,13 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                         const int R = pix[u] / PW, C = pix[u] - R * PW;
 #pragma unroll
                         for (int qq = 0; qq < 4; ++qq) {  // channels 8 qq + 4 kg + e: unit qq, byte 8 kg
-                            bf16x4 h, l;
+                            uint32_t hw[2], lw[2];
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) {
-                                const float o = fmaxf(d[u][4 * qq + e], d[u][4 * qq + e] * ae);
-                                h[e] = bf_hi(o);
-                                l[e] = bf_lo(o);
-                            }
+                            for (int e = 0; e < 4; e += 2)
+                                leaky_split2(d[u][4 * qq + e], d[u][4 * qq + e + 1], ae, hw[e >> 1], lw[e >> 1]);
                             const int a = x3_addr(R, C, qq, PW, TW) + kg * 8;
-                            *reinterpret_cast<bf16x4*>(patch + a) = h;
-                            *reinterpret_cast<bf16x4*>(patch + (a ^ 64)) = l;
+                            *reinterpret_cast<uint2*>(patch + a) = make_uint2(hw[0], hw[1]);
+                            *reinterpret_cast<uint2*>(patch + (a ^ 64)) = make_uint2(lw[0], lw[1]);
                         }
                     }
                 }
