@@ -306,6 +306,19 @@ def main_step(args, world, rank, dev):
                 "avg_ms": round(dom_live["avg_ms"], 4), "launches_timed": dom_live["count"],
                 "traffic_source": traffic_src,
                 "stages_ms": {c["name"]: round(c["avg_ms"], 4) for c in calib}}
+    # every stage against its own bound (the dominant one above): algorithmic
+    # flops or bytes of the calibration pass / its event-timed average
+    per = {}
+    for c in calib:
+        fe_stage = c["owner"] is fe
+        if fe_stage and c["name"].startswith("fe_stft"):
+            b, pk, a = "valu", VALU_F32_PEAK, c["flops"] / (c["avg_ms"] * 1e-3) / 1e12
+        elif fe_stage or c["flops"] == 0 or c["name"].startswith("head"):
+            b, pk, a = "hbm", HBM_PEAK_GBS, c["bytes"] / (c["avg_ms"] * 1e-3) / 1e9
+        else:
+            b, pk, a = "mfma", PEAK[args.precision], c["flops"] / (c["avg_ms"] * 1e-3) / 1e12
+        per[c["name"]] = {"bound": b, "achieved": round(a, 1), "frac": round(a / pk, 4)}
+    roofline["stages"] = per
     # whole step against the CNN's matrix roofline + the front end's VALU one
     step_flops = sum(c["flops"] for c in calib)
     roofline["step_tflops"] = round(step_flops / (elapsed / args.steps) / 1e12, 2)
