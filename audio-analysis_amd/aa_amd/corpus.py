@@ -61,17 +61,36 @@ def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world
     if examine_fn is None:
         from .analyse import examine as examine_fn
     import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from . import identify_tracks as it
+    mine = shard.shard(list(files), rank, world)
     local = {}
-    for i, f in shard.shard(list(files), rank, world):
-        # short tracks draw random window offsets from the global RandomState
-        # (src/identify_tracks.py:132, :167; the reference leaves it unseeded,
-        # one process per file): seeding it per file makes every file's result
-        # independent of which rank ran it and what ran before
-        np.random.seed(i)
-        t0 = time.time()
-        summary = examine_fn(str(f), bird_models, analyse_tracks=analyse_tracks)
-        summary["processing_time_seconds"] = round(time.time() - t0, 1)
-        local[i] = summary
+
+    def decode(f):
+        try:
+            return it.load_recording(str(f))
+        except Exception:  # left to examine(), which reports it the reference's way
+            return None
+
+    # the next file is read and decoded on a host thread while this one is
+    # classified (numpy releases the GIL in the bulk conversion)
+    with ThreadPoolExecutor(max_workers=1) as pool:
+        nxt = pool.submit(decode, mine[0][1]) if mine else None
+        for k, (i, f) in enumerate(mine):
+            pre = nxt.result()
+            nxt = pool.submit(decode, mine[k + 1][1]) if k + 1 < len(mine) else None
+            if pre is not None:
+                it._PREFETCHED[(str(f), 48000)] = pre
+            # short tracks draw random window offsets from the global RandomState
+            # (src/identify_tracks.py:132, :167; the reference leaves it unseeded,
+            # one process per file): seeding it per file makes every file's result
+            # independent of which rank ran it and what ran before
+            np.random.seed(i)
+            t0 = time.time()
+            summary = examine_fn(str(f), bird_models, analyse_tracks=analyse_tracks)
+            summary["processing_time_seconds"] = round(time.time() - t0, 1)
+            local[i] = summary
+            it._PREFETCHED.pop((str(f), 48000), None)
     return gather_documents(local, device=device)
 
 

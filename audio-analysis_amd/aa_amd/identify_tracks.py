@@ -211,8 +211,16 @@ def get_master_tag(track):
 # ---------------------------------------------------------------------------
 # decode (host) and the end-of-recording scan (GPU)
 # ---------------------------------------------------------------------------
+# decoded recordings handed over by a prefetching caller (aa_amd.corpus):
+# {(str(path), resample): (frames, sr)}, each entry consumed once
+_PREFETCHED = {}
+
+
 def load_recording(file, resample=48000):
     from .audio import decode
+    hit = _PREFETCHED.pop((str(file), resample), None)
+    if hit is not None:
+        return hit
     try:
         frames, sr = decode(file)
         if resample is not None and resample != sr:
