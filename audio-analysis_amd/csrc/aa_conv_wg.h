@@ -125,9 +125,11 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             l2[k] = *reinterpret_cast<const bf16x8*>(patch + (a ^ 64));
         };
         rd(0, 0);
+        if constexpr (AA_PIN_WG & 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             if (i + 1 < MF) rd(i + 1, (i + 1) & 1);
+            if constexpr (AA_PIN_WG & 2) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
                 acc[e][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.h[j], h2[i & 1], acc[e][i][j], 0, 0, 0);

@@ -38,6 +38,22 @@ namespace aa {
 
 constexpr int X3_CG = 32;  // channels per staged group
 
+// Scheduling pins for the kernels whose waves load their own B fragments
+// from global memory (conv_x3 with RING = false, conv_wg).  Bit 0: the next
+// step's fragment loads are issued before this step's MFMAs; bit 1: fragment
+// i+1's just-in-time A read before fragment i's MFMAs.  Without them the
+// scheduler sinks the prefetches down to their first use and the wave waits
+// out the L2 latency every step (s_waitcnt vmcnt(0) right after the issue,
+// tools/isa_stats.py).  In-pipeline A/B: fused first conv 153 -> 147 us,
+// Winograd 9x3 152 -> 138 us; the ring kernels (LDS-staged B, a barrier per
+// step) lose with either pin (3x3/64: 52 -> 58 / 71 us), so they stay unpinned.
+#ifndef AA_PIN_X3
+#define AA_PIN_X3 3
+#endif
+#ifndef AA_PIN_WG
+#define AA_PIN_WG 3
+#endif
+
 template <int KH, int KW, int TH, int TW, bool FUSED>
 __host__ __device__ constexpr size_t x3_patch_bytes() {
     size_t b = (size_t)(TH + KH - 1) * (TW + KW - 1) * 128;
@@ -370,6 +386,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         if (s + 1 < NSTEP) read_b(nxt, s + 1);
         if constexpr (!AJIT) {
             if (t + 1 < NTAP) read_a(nxt, t + 1);
+            if constexpr (!RING && (AA_PIN_X3 & 1)) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < MF; ++i)
 #pragma unroll
@@ -395,9 +412,11 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 }
             };
             rd(0, 0);
+            if constexpr (!RING && (AA_PIN_X3 & 1)) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < MF; ++i) {
                 if (i + 1 < MF) rd(i + 1, (i + 1) & 1);
+                if constexpr (!RING && (AA_PIN_X3 & 2)) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int j = 0; j < NF; ++j) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.bh[j], h2[i & 1], acc[i][j], 0, 0, 0);
