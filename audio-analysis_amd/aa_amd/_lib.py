@@ -76,6 +76,11 @@ class SnComponent(C.Structure):
                 ("area", C.c_int32), ("order", C.c_int32)]
 
 
+class FlacInfo(C.Structure):
+    _fields_ = [("sample_rate", C.c_int32), ("channels", C.c_int32), ("bits_per_sample", C.c_int32),
+                ("total_frames", C.c_int64)]
+
+
 _lib = None
 
 _SIGS = {
@@ -120,6 +125,8 @@ _SIGS = {
                             C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "aa_sn_components_from_mask": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t,
                                              C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    "aa_flac_info": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(FlacInfo)]),
+    "aa_flac_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
 }
 
 EXPORTED = tuple(_SIGS)

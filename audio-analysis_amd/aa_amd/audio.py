@@ -8,7 +8,11 @@ directly (PCM 8/16/24/32-bit and IEEE float32/64) and applies the same s16
 conversion ffmpeg's libswresample performs (no dither): u8 ``(x - 128) << 8``,
 s24/s32 ``>> 16`` of the 32-bit value (truncation), float ``clip(lrint(x *
 32768))`` -- so non-16-bit files give the reference's samples, not more
-precise ones.  Other containers need an external decoder and are rejected.
+precise ones.  FLAC streams are decoded natively (``aa_flac_decode`` in
+libaa.so, host code) and go through the same s16 conversion: ffmpeg's FLAC
+decoder left-justifies a b-bit sample into s16 (b <= 16) or s32, so the s16
+value is ``x << (16 - b)`` or ``x >> (b - 16)``.  Other containers (MP3, Ogg,
+AAC/M4A, Opus) need a codec this image does not have and are rejected.
 Resampling to 48 kHz (librosa soxr_hq in the reference) uses a polyphase FIR
 -- parity unpinned: soxr is not available.
 """
@@ -20,11 +24,51 @@ from math import gcd
 import numpy as np
 
 
+def _to_mono(q, channels):
+    """ffmpeg s16 integers -> librosa.util.buf_to_float, then the channel mean."""
+    x = q.astype(np.float32) / np.float32(32768.0)
+    if channels > 1:
+        x = x[: len(x) // channels * channels].reshape(-1, channels).mean(axis=1, dtype=np.float32)
+    return np.ascontiguousarray(x, dtype=np.float32)
+
+
+def _is_flac(data):
+    if data[:3] == b"ID3" and len(data) >= 10:  # ID3v2 tag in front of the stream
+        sz = (data[6] & 0x7F) << 21 | (data[7] & 0x7F) << 14 | (data[8] & 0x7F) << 7 | (data[9] & 0x7F)
+        off = 10 + sz + (10 if data[5] & 0x10 else 0)
+        return data[off:off + 4] == b"fLaC"
+    return data[:4] == b"fLaC"
+
+
+def decode_flac(data):
+    """FLAC bytes -> (ffmpeg-s16 integers as int32 [frames * channels], channels, sr)."""
+    import ctypes as C
+    from ._lib import FlacInfo, check, lib
+    buf = np.frombuffer(data, np.uint8)
+    info = FlacInfo()
+    check(lib().aa_flac_info(buf.ctypes.data, buf.size, C.byref(info)), "aa_flac_info")
+    n = C.c_int64()
+    if info.total_frames == 0:  # length not stated: count first
+        check(lib().aa_flac_decode(buf.ctypes.data, buf.size, None, 0, C.byref(n)), "aa_flac_decode")
+        cap = n.value
+    else:
+        cap = info.total_frames
+    out = np.empty(cap * info.channels, np.int32)
+    check(lib().aa_flac_decode(buf.ctypes.data, buf.size, out.ctypes.data, cap, C.byref(n)), "aa_flac_decode")
+    b = info.bits_per_sample
+    q = out[: n.value * info.channels]
+    q = q << (16 - b) if b <= 16 else q >> (b - 16)
+    return q, info.channels, info.sample_rate
+
+
 def decode(path):
     with open(path, "rb") as f:
         data = f.read()
+    if _is_flac(data):
+        q, channels, sr = decode_flac(data)
+        return _to_mono(q, channels), int(sr)
     if len(data) < 12 or data[:4] not in (b"RIFF", b"RF64") or data[8:12] != b"WAVE":
-        raise ValueError(f"{path}: not a RIFF/WAVE file")
+        raise ValueError(f"{path}: not a RIFF/WAVE or FLAC file")
     mv = memoryview(data)  # chunk bodies as views: no copy of the sample payload
     pos, fmt, payload = 12, None, None
     while pos + 8 <= len(data):
@@ -64,10 +108,7 @@ def decode(path):
         q = np.clip(np.rint(f.astype(np.float64) * 32768.0), -32768, 32767)
     else:
         raise ValueError(f"{path}: WAVE format tag {tag} unsupported")
-    x = q.astype(np.float32) / np.float32(32768.0)  # librosa.util.buf_to_float
-    if channels > 1:
-        x = x[: len(x) // channels * channels].reshape(-1, channels).mean(axis=1, dtype=np.float32)
-    return np.ascontiguousarray(x, dtype=np.float32), int(sr)
+    return _to_mono(q, channels), int(sr)
 
 
 def resample_poly(x, sr_in, sr_out):

@@ -21,6 +21,8 @@
  *   aa_track_mean  np.mean over models, windows     src/identify_tracks.py:547-551
  *   aa_span_nonzero  get_end                        src/identify_tracks.py:387-413
  *   aa_sn_*      signal_noise                       src/identify_tracks.py:650-706
+ *   aa_flac_*    load_recording's ffmpeg decode     src/identify_tracks.py:49-62
+ *                  (FLAC; host memory, no GPU)
  *
  * Return values: AA_OK (0) or an aa_status code; aa_last_error() gives a
  * thread-local message for the last failing call on this thread.
@@ -232,6 +234,26 @@ int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* workspace, 
 int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int64_t n_frames, void* workspace,
                                size_t workspace_bytes, aa_sn_component* out, int32_t max_out,
                                int32_t* n_out, void* stream);
+
+/* ---------------------------------------------------------------- FLAC decode */
+/* load_recording (src/identify_tracks.py:49-62) decodes through ffmpeg; these
+ * decode a FLAC stream (RFC 9639; an ID3v2 tag in front is skipped) held in
+ * HOST memory, on the calling thread.  Samples come out as the stream's own
+ * integers (bits_per_sample), interleaved; the caller applies ffmpeg's s16
+ * conversion.  Header CRC-8 and frame CRC-16 are verified (AA_ERR_INVALID on
+ * damage, with the byte offset in aa_last_error). */
+typedef struct aa_flac_stream_info {
+    int32_t sample_rate;
+    int32_t channels;        /* 1..8 */
+    int32_t bits_per_sample; /* 4..32 */
+    int64_t total_frames;    /* samples per channel; 0 = not stated */
+} aa_flac_stream_info;
+
+int aa_flac_info(const uint8_t* data, size_t len, aa_flac_stream_info* info);
+/* out: host int32 [cap_frames][channels], or NULL to count only;
+ * n_frames: frames (samples per channel) decoded.  AA_ERR_WORKSPACE when the
+ * stream holds more than cap_frames. */
+int aa_flac_decode(const uint8_t* data, size_t len, int32_t* out, int64_t cap_frames, int64_t* n_frames);
 
 #ifdef __cplusplus
 }

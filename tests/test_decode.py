@@ -67,7 +67,11 @@ def test_stereo_mean_of_s16(tmp_path):
 
 
 def test_rejects_non_wav(tmp_path):
-    p = tmp_path / "a.flac"
-    p.write_bytes(b"fLaC" + b"\0" * 64)
+    p = tmp_path / "a.ogg"
+    p.write_bytes(b"OggS" + b"\0" * 64)
     with pytest.raises(ValueError):
+        decode(p)
+    p = tmp_path / "a.flac"  # a FLAC marker with a broken metadata chain
+    p.write_bytes(b"fLaC" + b"\0" * 64)
+    with pytest.raises(RuntimeError):
         decode(p)
