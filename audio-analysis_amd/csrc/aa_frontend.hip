@@ -19,6 +19,7 @@
 #include "aa_common.h"
 #include "aa_wavefft.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -414,7 +415,8 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
 //   4. DFT-32 over m in registers -> E_h[k2']
 //   5. radix-2 across the lane pair (DPP quad_perm swap):
 //      Z[k1 + 32 k2'] = E0 + W64^k2' E1, Z[k1 + 32 (k2' + 32)] = E0 - W64^k2' E1
-//   6. real split X[k] = E + W4096^k O from Z[k], conj Z[2048 - k], with
+//   6. real split X[k] = E + W4096^k O from Z[k], conj Z[2048 - k] (both lanes
+//      of a pair, 16 bins each), with
 //      W4096^(k1 + 32 j) = W4096^k1 W128^j (one table entry per lane)
 //   7. |X|^power into the wave's LDS buffer (the periodic Hann was applied to
 //      the samples before step 1, by angle addition from two table values)
@@ -427,6 +429,9 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
 // frames: neighbouring frames overlap by 4096 - hop samples and one L2 then
 // serves the overlap.
 // ---------------------------------------------------------------------------
+// band slots of the wave-per-frame kernel's CSR image: whole rounds of 64 lanes
+__host__ __device__ constexpr int fe_mel_slots(int n_mels) { return (n_mels + 63) / 64 * 64; }
+
 #ifndef AA_FE_WPB
 #define AA_FE_WPB 8
 #endif
@@ -446,7 +451,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     char* cl = reinterpret_cast<char*>(lds);
     const int4* srows = reinterpret_cast<const int4*>(cl);  // CSR image (fe_cimg4096): rows | values
-    const float* svals = reinterpret_cast<const float*>(srows + n_mels);
+    const float* svals = reinterpret_cast<const float*>(srows + fe_mel_slots(n_mels));
     float2* wb = reinterpret_cast<float2*>(cl + cimg_bytes) + wave * kHalf;  // this wave's buffer
 
     for (int g = wave; g < cimg_bytes / 1024; g += kWpb)
@@ -504,10 +509,22 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
                 // backend must not fuse a pair into one 8-byte load, whose range
                 // check would not zero the two samples independently
                 const int offe = i0 - d.pad_left + l2;
-                int offo = offe + 1;
-                __asm__ volatile("" : "+v"(offo));
+                const int v0 = i0 - d.pad_left;  // the frame's first sample in the view
+                if (v0 >= 0 && v0 + 4096 <= d.n_valid) {
+                    // frame inside the view (wave-uniform): no sample is range
+                    // checked, so a lane's pair comes in one 8-byte load (32
+                    // fully used 512-B wave-instructions instead of 64 half-used)
 #pragma unroll
-                for (int r = 0; r < 32; ++r) y[r] = make_float2(load_view(rs, offe + 128 * r), load_view(rs, offo + 128 * r));
+                    for (int r = 0; r < 32; ++r) {
+                        const uint2 v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, (offe + 128 * r) * 4, 0, 0));
+                        y[r] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+                    }
+                } else {
+                    int offo = offe + 1;
+                    __asm__ volatile("" : "+v"(offo));
+#pragma unroll
+                    for (int r = 0; r < 32; ++r) y[r] = make_float2(load_view(rs, offe + 128 * r), load_view(rs, offo + 128 * r));
+                }
             }
             if (normalize && (i0 < 0 || i0 + 4096 > win_len)) {  // edge frame: + beta, centre padding 0
 #pragma unroll
@@ -620,31 +637,50 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
             for (int j = 0; j < 32; ++j) wb[k1 + 32 * j] = u[dperm(j)];  // Z[1024 + k1 + 32 j]
         }
         wave_sync();
-        // h = 0 lanes: X[k], k = k1 + 32 j < 1024 (bands above NC/2 take the
-        // generic kernel, see fe_fast4096), |X|^p straight into the band
-        // buffer, stored reversed from the top of the wave's buffer: bin k at
-        // float Pt[-k], Pt = float 2 kHalf - 1.  Step j writes bins
-        // [32 j, 32 j + 32), at or above float2 kHalf - 16 - 16 j, while later
-        // steps still read mirrors below float2 1024 - 32 j - 32: the two never
-        // meet, so the split needs no extra registers, no buffer and no guard.
+        // Both lanes of a pair split: lane h takes the bins k = k1 + 32 (16 h +
+        // i), i < 16 (all 1024 bins below NC/2 over the 64 lanes; bands above
+        // take the generic kernel, see fe_fast4096).  Z[k] is the h = 0 lane's
+        // u[dperm(16 h + i)] (the h = 1 lane swaps it over from its partner),
+        // its mirror Z[2048 - k] the h = 1 lanes' LDS copy.  |X|^p is stored
+        // reversed from the top of the wave's buffer (bin k at float Pt[-k],
+        // Pt = float 2 kHalf - 1), where it overlaps mirrors that later
+        // iterations still read, so the 16 values wait in registers until the
+        // loop is done.
         float* Pt = reinterpret_cast<float*>(wb) + (2 * kHalf - 1);
-        if (!h && !(DIAG & 8)) {
-            // Z[2048 - k] sits at wb[1024 - k1 - 32 j] = mb[32 (31 - j)]: one base
-            // register and non-negative immediate offsets (wb[1024], read for
+        if (!(DIAG & 8)) {
+            // mirror of bin k1 + 32 (16 h + i) at wb[1024 - k] = mb[32 (31 - i)]
+            // (one base register, non-negative immediates; wb[1024], read for
             // k = 0, is in the buffer and unused)
-            const float2* mb = wb + (32 - k1);
-            float* pk = Pt - k1 - 32 * 31;  // bin k1 + 32 j at pk[32 (31 - j)] = Pt[-k]
+            const float2* mb = wb + (32 - k1) - 512 * h;
+            float* pk = Pt - k1 - 512 * h - 32 * 15;  // bin k at pk[32 (15 - i)] = Pt[-k]
+            // W4096^k = W4096^k1 (W4096^512)^h W128^i, W4096^512 = (r, -r)
+            const float r2 = 0.70710678118654752440f;
+            const float2 wkh = h ? make_float2(r2 * (wk.x + wk.y), r2 * (wk.y - wk.x)) : wk;
+            float pw[16];
+            float2 zm[16];  // mirrors, read 8 ahead of their use
 #pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                const float2 a = u[dperm(j)];
-                const float2 zb = mb[32 * (31 - j)];
-                const float2 b = (j == 0 && k1 == 0) ? a : zb;  // Z[NC - k]; Z[0] for k = 0
+            for (int i = 0; i < 8; ++i) zm[i] = mb[32 * (31 - i)];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if (i % 8 == 0 && i + 8 < 16) {
+#pragma unroll
+                    for (int k = i + 8; k < i + 16; ++k) zm[k] = mb[32 * (31 - k)];
+                }
+                const float2 hiv = u[dperm(16 + i)];
+                const float2 oth = make_float2(swap_pair(hiv.x), swap_pair(hiv.y));
+                const float2 a = h ? oth : u[dperm(i)];
+                const float2 zb = zm[i];
+                const float2 b = (i == 0 && k1 == 0 && !h) ? a : zb;  // Z[NC - k]; Z[0] for k = 0
                 const float2 E = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
                 const float2 O = make_float2(0.5f * (a.y + b.y), -0.5f * (a.x - b.x));
-                float2 wj = cmul(wk, wconst128(j));  // W4096^k
+                float2 wj = cmul(wkh, wconst128(i));  // W4096^k
                 __asm__ volatile("" : "+v"(wj.x), "+v"(wj.y));  // formed here, not hoisted
                 const float2 X = cadd(E, cmul(wj, O));
-                if (!(DIAG & 16)) pk[32 * (31 - j)] = pow_mag<PM>(X.x, X.y, power);
+                pw[i] = pow_mag<PM>(X.x, X.y, power);
+            }
+            if (!(DIAG & 16)) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) pk[32 * (15 - i)] = pw[i];
             }
         }
         wave_sync();
@@ -653,11 +689,13 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
         // offsets 16-B aligned); the padding adds exact zeros
         float fmx = 0.f;
         float* orow = melF + (size_t)fi * n_mels;  // fi = w T + t
-        for (int m = lane; m < ((DIAG & 32) ? 0 : n_mels); m += 64) {
-            // row m covers bins [x, x + L): its values are stored reversed and
-            // front-padded to L4 = roundup(L, 4) (fe_cimg4096), so with P
-            // reversed the row is an ascending run pv[0 .. L4)
-            const int4 rw = srows[m];
+        const int nslot = fe_mel_slots(n_mels);
+        for (int si = lane; si < ((DIAG & 32) ? 0 : nslot); si += 64) {
+            // slot si holds band rw.w (-1: empty, length 0) covering bins
+            // [x, x + L): its values are stored reversed and front-padded to
+            // L4 = roundup(L, 4) (fe_cimg4096), so with P reversed the row is
+            // an ascending run pv[0 .. L4)
+            const int4 rw = srows[si];
             const float4* wv = reinterpret_cast<const float4*>(svals + rw.z);
             const float* pv = Pt - rw.x - (rw.y - 1);  // bins x + L4 - 1 down to x
             float s = 0.f;
@@ -669,7 +707,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
                 s = fmaf(a.w, pv[i + 3], s);
             }
             s *= apow;
-            if (!(DIAG & 64)) orow[m] = s;
+            if (!(DIAG & 64) && rw.w >= 0) orow[rw.w] = s;
             fmx = fmaxf(fmx, s);
         }
         fmx = wave_max(fmx);
@@ -935,13 +973,28 @@ extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** 
         // CSR image of the wave-per-frame kernel, byte-identical to its LDS
         // region: rows (first bin, padded length, value offset) | values, each
         // row zero-padded to whole float4s (value offsets 16-B aligned)
-        std::vector<int4> prow(rows.size());
+        // Rows sit in fe_mel_slots() slots, slot i served by lane i % 64 (the
+        // .w field names the band): the longest row first goes to the
+        // least-loaded lane with a free slot, so the lanes' loop trip counts
+        // stay close (round-robin rows gave lane 31 the 3 widest-spaced rows:
+        // 52 bins against a mean of 32).  Empty slots have length 0.
+        const int nslot = fe_mel_slots(cfg->n_mels);
+        std::vector<int4> prow(nslot, make_int4(0, 0, 0, -1));
         std::vector<float> pval;
-        // (the kernel keeps the band power reversed: values are stored last
-        // bin first, zero-padded at the front, so a row reads one ascending run)
-        for (size_t m = 0; m < rows.size(); ++m) {
+        std::vector<int> order(rows.size());
+        for (size_t m = 0; m < rows.size(); ++m) order[m] = (int)m;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return rows[a].y > rows[b].y; });
+        std::vector<int> load(64, 0), used(64, 0);
+        for (int m : order) {
+            int best = -1;
+            for (int l = 0; l < 64; ++l)
+                if (used[l] < nslot / 64 && (best < 0 || load[l] < load[best])) best = l;
             const int len = (rows[m].y + 3) & ~3, pad = len - rows[m].y;
-            prow[m] = make_int4(rows[m].x, len, (int)pval.size(), 0);
+            // (the kernel keeps the band power reversed: values are stored last
+            // bin first, zero-padded at the front, so a row reads one ascending run)
+            prow[best + 64 * used[best]] = make_int4(rows[m].x, len, (int)pval.size(), m);
+            load[best] += len;
+            ++used[best];
             for (int i = 0; i < len; ++i) pval.push_back(i < pad ? 0.f : vals[rows[m].z + rows[m].y - 1 - (i - pad)]);
         }
         const size_t raw = sizeof(int4) * prow.size() + sizeof(float) * pval.size();

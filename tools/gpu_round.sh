@@ -22,7 +22,7 @@ for P in $PRECS; do
   cp gpurun_out/kernel_stats_$P.txt profiles/$R/bench_kernel_stats_$P.txt
   cp gpurun_out/stats_$P/*kernel_stats.csv profiles/$R/bench_kernel_stats_$P.csv 2>/dev/null || cp gpurun_out/stats_$P/*/*kernel_stats.csv profiles/$R/bench_kernel_stats_$P.csv
 done
-timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 || { cat gpurun_out/bench.log; exit 6; }
+timeout -k 10 400 python bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err || { cat gpurun_out/bench.err; exit 6; }
 cp gpurun_out/bench.log profiles/$R/bench.json
 cat gpurun_out/kernel_stats_bf16x3.txt
 tail -1 gpurun_out/bench.log
