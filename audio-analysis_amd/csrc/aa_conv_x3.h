@@ -537,11 +537,15 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             __syncthreads();
             constexpr int NPX = PH * PW;
             constexpr int NGRP = (NPX + 31) / 32;
-            for (int g0 = wave0; g0 < ((DIAG & 64) ? 0 : NGRP); g0 += 8) {
-                bf16x8 xh[2], xl[2];
-                int pix[2];
+            // NU groups of 32 pixels per wave and pass (groups g0 + 4 u): all
+            // of them in one pass when that takes at most 3 (12x21 tiles: 322
+            // patch pixels, 11 groups), else passes of 2
+            constexpr int NU = (NGRP + 3) / 4 <= 3 ? (NGRP + 3) / 4 : 2;
+            for (int g0 = wave0; g0 < ((DIAG & 64) ? 0 : NGRP); g0 += 4 * NU) {
+                bf16x8 xh[NU], xl[NU];
+                int pix[NU];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
+                for (int u = 0; u < NU; ++u) {
                     pix[u] = min((g0 + 4 * u) * 32 + l32, NPX - 1);
                     const int r = pix[u] / PW, c = pix[u] - r * PW;
                     const float* xp = X + r * XW + c;
@@ -555,15 +559,15 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                         xl[u][j] = bf_lo(xv[j]);
                     }
                 }
-                f32x16 d[2];
+                f32x16 d[NU];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xh[u], cb, 0, 0, 0);
+                for (int u = 0; u < NU; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xh[u], cb, 0, 0, 0);
 #pragma unroll
-                for (int u = 0; u < 2; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xl[u], d[u], 0, 0, 0);
+                for (int u = 0; u < NU; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xl[u], d[u], 0, 0, 0);
 #pragma unroll
-                for (int u = 0; u < 2; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wal, xh[u], d[u], 0, 0, 0);
+                for (int u = 0; u < NU; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wal, xh[u], d[u], 0, 0, 0);
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
+                for (int u = 0; u < NU; ++u) {
                     if ((g0 + 4 * u) * 32 + l32 < NPX) {
                         const int R = pix[u] / PW, C = pix[u] - R * PW;
 #pragma unroll
