@@ -47,6 +47,11 @@ constexpr int X3_CG = 32;  // channels per staged group
 // tools/isa_stats.py).  In-pipeline A/B: fused first conv 153 -> 147 us,
 // Winograd 9x3 152 -> 138 us; the ring kernels (LDS-staged B, a barrier per
 // step) lose with either pin (3x3/64: 52 -> 58 / 71 us), so they stay unpinned.
+// fused first layer: the log-mel patch split into bf16 hi / lo once per
+// element at staging instead of once per tap read (A/B switch)
+#ifndef AA_X3_XSPLIT
+#define AA_X3_XSPLIT 1
+#endif
 #ifndef AA_PIN_X3
 #define AA_PIN_X3 3
 #endif
@@ -499,7 +504,10 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             // v_mfma_f32_32x32x16_bf16 (weights hi/lo x log-mel hi/lo, the 9 taps
             // in k, the bias as C), activation, hi/lo into the swizzled patch
             constexpr int XW = PW + 2, XN = (PH + 2) * XW;
+            // X: the log-mel patch split once per element, bf16 hi in the low and
+            // bf16 lo in the high half of a dword (AA_X3_XSPLIT), else f32
             float* X = reinterpret_cast<float*>(smem + (size_t)PH * PW * 128);
+            uint32_t* Xs = reinterpret_cast<uint32_t*>(X);
             // buffer loads: the window's base in an SGPR offset, the element in the lane's offset
             const __amdgpu_buffer_rsrc_t lrs = x3_wrsrc(in);
             const int esz = fc.lm_f16 ? 2 : 4;
@@ -517,7 +525,16 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int idx = i0 + u * NTHR + threadIdx.x;
-                    if (idx < XN) X[idx] = fc.has_mag ? powf(v[u], fc.mag_exp) : v[u];
+                    if (idx < XN) {
+                        const float x = fc.has_mag ? powf(v[u], fc.mag_exp) : v[u];
+                        if constexpr (AA_X3_XSPLIT) {
+                            uint32_t h, l;
+                            split2(x, x, h, l);  // (both halves the same value)
+                            Xs[idx] = (h & 0xffffu) | (l << 16);
+                        } else {
+                            X[idx] = x;
+                        }
+                    }
                 }
             }
             const int l32 = lane & 31, kg = lane >> 5;
@@ -548,15 +565,36 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 for (int u = 0; u < NU; ++u) {
                     pix[u] = min((g0 + 4 * u) * 32 + l32, NPX - 1);
                     const int r = pix[u] / PW, c = pix[u] - r * PW;
-                    const float* xp = X + r * XW + c;
-                    float xv[8];
-                    xv[0] = xp[off0];
+                    if constexpr (AA_X3_XSPLIT) {
+                        // taps 2k, 2k+1 of the pre-split patch -> one dword of
+                        // the hi fragment (low halves) and one of the lo (high halves)
+                        const uint32_t* xp = Xs + r * XW + c;
+                        uint32_t xv[8];
+                        xv[0] = xp[off0];
 #pragma unroll
-                    for (int j = 1; j < 8; ++j) xv[j] = xp[(j / 3) * XW + j % 3];
+                        for (int j = 1; j < 8; ++j) xv[j] = xp[(j / 3) * XW + j % 3];
+                        uint4 hh, ll;
+                        hh.x = __builtin_amdgcn_perm(xv[1], xv[0], 0x05040100u);
+                        hh.y = __builtin_amdgcn_perm(xv[3], xv[2], 0x05040100u);
+                        hh.z = __builtin_amdgcn_perm(xv[5], xv[4], 0x05040100u);
+                        hh.w = __builtin_amdgcn_perm(xv[7], xv[6], 0x05040100u);
+                        ll.x = __builtin_amdgcn_perm(xv[1], xv[0], 0x07060302u);
+                        ll.y = __builtin_amdgcn_perm(xv[3], xv[2], 0x07060302u);
+                        ll.z = __builtin_amdgcn_perm(xv[5], xv[4], 0x07060302u);
+                        ll.w = __builtin_amdgcn_perm(xv[7], xv[6], 0x07060302u);
+                        xh[u] = __builtin_bit_cast(bf16x8, hh);
+                        xl[u] = __builtin_bit_cast(bf16x8, ll);
+                    } else {
+                        const float* xp = X + r * XW + c;
+                        float xv[8];
+                        xv[0] = xp[off0];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        xh[u][j] = bf_hi(xv[j]);
-                        xl[u][j] = bf_lo(xv[j]);
+                        for (int j = 1; j < 8; ++j) xv[j] = xp[(j / 3) * XW + j % 3];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            xh[u][j] = bf_hi(xv[j]);
+                            xl[u][j] = bf_lo(xv[j]);
+                        }
                     }
                 }
                 f32x16 d[NU];
