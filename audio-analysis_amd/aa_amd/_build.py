@@ -17,7 +17,11 @@ ARCH = os.environ.get("AA_OFFLOAD_ARCH", "gfx950")
 # per-source flags: the FFT front end is written in scalar f32; SLP packing it
 # into v_pk_* ops needs paired SGPR constants and register shuffles that push
 # the wave-per-frame kernel past its 128-VGPR budget (spills)
-EXTRA_FLAGS = {"aa_frontend.hip": ["-fno-slp-vectorize"], "aa_signal.hip": ["-fno-slp-vectorize"]}
+# the CNN kernels keep MFMA accumulators in VGPRs: no AGPR copies
+# (v_accvgpr_read) between the fused first layer's MFMAs and its activation
+# split (in-pipeline A/B: step +0.5 %)
+EXTRA_FLAGS = {"aa_frontend.hip": ["-fno-slp-vectorize"], "aa_signal.hip": ["-fno-slp-vectorize"],
+               "aa_cnn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def hipcc() -> str:

@@ -27,6 +27,7 @@ def build(name, table, wg="-"):
     cmd = [cc, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={_build.ARCH}", f"-I{_build.INCLUDE}",
            *([f"-DAA_X3_ALT(X)={table}"] if table != "-" else []),
            *([f"-DAA_WG_ALT(X)={wg}"] if wg != "-" else []),
+           *_build.EXTRA_FLAGS.get("aa_cnn.hip", []),
            *os.environ.get("AB_DEFS", "").split(), "-c", str(_build.CSRC / "aa_cnn.hip"), "-o", str(obj)]
     subprocess.run(cmd, check=True)
     objs = [_build.PKG.parent / "build" / (s.rsplit(".", 1)[0] + ".o") for s in _build.SOURCES
