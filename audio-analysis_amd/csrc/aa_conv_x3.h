@@ -512,28 +512,31 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             const __amdgpu_buffer_rsrc_t lrs = x3_wrsrc(in);
             const int esz = fc.lm_f16 ? 2 : 4;
             const int lbase = __builtin_amdgcn_readfirstlane(n * fc.H0 * fc.W0 * esz);
-            for (int i0 = 0; i0 < ((DIAG & 512) ? 0 : XN); i0 += 4 * NTHR) {
-                float v[4];
+            // XU elements per thread and pass (XN = 400 for 12x21 tiles: one
+            // pass of 2 over 256 threads), split in pairs
+            constexpr int XU = (XN + NTHR - 1) / NTHR <= 2 ? 2 : 4;
+            for (int i0 = 0; i0 < ((DIAG & 512) ? 0 : XN); i0 += XU * NTHR) {
+                float v[XU];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < XU; ++u) {
                     const int idx = min(i0 + u * NTHR + (int)threadIdx.x, XN - 1);
                     const int r = idx / XW, c = idx - r * XW;
                     const int e = min(oh0 + r, fc.H0 - 1) * fc.W0 + min(ow0 + c, fc.W0 - 1);
                     v[u] = fc.lm_f16 ? (float)__builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(lrs, e * 2, lbase, 0))
                                      : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lrs, e * 4, lbase, 0));
+                    if (fc.has_mag) v[u] = powf(v[u], fc.mag_exp);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int idx = i0 + u * NTHR + threadIdx.x;
-                    if (idx < XN) {
-                        const float x = fc.has_mag ? powf(v[u], fc.mag_exp) : v[u];
-                        if constexpr (AA_X3_XSPLIT) {
-                            uint32_t h, l;
-                            split2(x, x, h, l);  // (both halves the same value)
-                            Xs[idx] = (h & 0xffffu) | (l << 16);
-                        } else {
-                            X[idx] = x;
-                        }
+                for (int u = 0; u < XU; u += 2) {
+                    const int idx = i0 + u * NTHR + threadIdx.x, idx2 = idx + NTHR;
+                    if constexpr (AA_X3_XSPLIT) {
+                        uint32_t h, l;
+                        split2(v[u], v[u + 1], h, l);
+                        if (idx < XN) Xs[idx] = __builtin_amdgcn_perm(l, h, 0x05040100u);     // hi | lo << 16
+                        if (idx2 < XN) Xs[idx2] = __builtin_amdgcn_perm(l, h, 0x07060302u);
+                    } else {
+                        if (idx < XN) X[idx] = v[u];
+                        if (idx2 < XN) X[idx2] = v[u + 1];
                     }
                 }
             }
