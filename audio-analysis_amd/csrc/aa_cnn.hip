@@ -1192,7 +1192,7 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
 #define AA_X3_CFGS(X)                                 \
     X(3, 3, 32, 3, 4, 1, 4, 2, 12, 21, 0, 1, 0)       \
     X(3, 3, 32, 1, 4, 2, 3, 2, 10, 18, 1, 0, 4)       \
-    X(3, 3, 64, 1, 2, 2, 3, 2, 12, 8, 1, 1, 4)        \
+    X(3, 3, 64, 1, 2, 2, 3, 2, 12, 8, 1, 1, 0)        \
     X(9, 3, 64, 3, 2, 2, 4, 2, 21, 6, 0, 1, 4)        \
     X(1, 3, 128, 1, 2, 2, 3, 2, 7, 12, 1, 1, 4)
 #endif
