@@ -1194,7 +1194,7 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     X(3, 3, 32, 1, 4, 2, 3, 2, 10, 18, 1, 0, 4)       \
     X(3, 3, 64, 1, 2, 2, 3, 2, 12, 8, 1, 1, 0)        \
     X(9, 3, 64, 3, 2, 2, 4, 2, 21, 6, 0, 1, 4)        \
-    X(1, 3, 128, 1, 2, 2, 3, 2, 7, 12, 1, 1, 4)
+    X(1, 3, 128, 1, 2, 2, 3, 2, 7, 12, 1, 1, 0)
 #endif
 
 // conv_wg (split-bf16, Winograd F(2,3) along W) instantiations: (kh, C_in,
