@@ -38,6 +38,17 @@ namespace aa {
 
 constexpr int X3_CG = 32;  // channels per staged group
 
+// Build switches kept for in-pipeline A/B runs (tools/ab_build.py AB_DEFS):
+// AA_X3_XSPLIT: the fused first layer's log-mel patch split into bf16 hi / lo
+// once per element as it is staged, instead of once per tap read;
+// AA_X3_REMAP: XCD-aware block order (x3_block) for conv_x3 as for conv_wg.
+#ifndef AA_X3_XSPLIT
+#define AA_X3_XSPLIT 1
+#endif
+#ifndef AA_X3_REMAP
+#define AA_X3_REMAP 1
+#endif
+
 // Scheduling pins for the kernels whose waves load their own B fragments
 // from global memory (conv_x3 with RING = false, conv_wg).  Bit 0: the next
 // step's fragment loads are issued before this step's MFMAs; bit 1: fragment
@@ -47,11 +58,6 @@ constexpr int X3_CG = 32;  // channels per staged group
 // tools/isa_stats.py).  In-pipeline A/B: fused first conv 153 -> 147 us,
 // Winograd 9x3 152 -> 138 us; the ring kernels (LDS-staged B, a barrier per
 // step) lose with either pin (3x3/64: 52 -> 58 / 71 us), so they stay unpinned.
-// fused first layer: the log-mel patch split into bf16 hi / lo once per
-// element at staging instead of once per tap read (A/B switch)
-#ifndef AA_X3_XSPLIT
-#define AA_X3_XSPLIT 1
-#endif
 #ifndef AA_PIN_X3
 #define AA_PIN_X3 3
 #endif
@@ -138,9 +144,10 @@ __device__ __forceinline__ int x3_addr(int R, int C, int u, int PW, int TW) {
 // channel block) with the channel block fastest: the blocks that stage the
 // same input patch (all channel blocks of a tile) and its neighbours (the
 // next tiles, which share the halo) meet in the same L2.  In-pipeline A/B:
-// the Winograd 9x3 kernel (two channel blocks per tile) gains a little, the
-// conv_x3 kernels lose a little (-0.8 % on the step when all remap), so only
-// conv_wg remaps.
+// the Winograd 9x3 kernel (two channel blocks per tile) gains a little; the
+// conv_x3 kernels lost 0.8 % of the step with it at first and gained 0.3 %
+// (3 of 3 rounds) after the later occupancy and first-layer changes, so they
+// remap too (AA_X3_REMAP).
 struct BlockPos {
     int tile, cb, n;
 };
@@ -269,7 +276,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     char* patch = smem;
     char* Bs = smem + x3_patch_bytes<KH, KW, TH, TW, FUSED>();
 
-    const BlockPos bp = x3_block<false>();
+    const BlockPos bp = x3_block<AA_X3_REMAP != 0>();
     const int n = bp.n, cb = bp.cb;
     const int th = bp.tile / tiles_w, tw = bp.tile - (bp.tile / tiles_w) * tiles_w;
     const int oh0 = th * TH, ow0 = tw * TW;
