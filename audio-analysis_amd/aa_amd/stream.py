@@ -15,6 +15,8 @@ classifying it on its own.
 """
 from __future__ import annotations
 
+import os
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 from typing import Iterable, List, Sequence
 
@@ -61,6 +63,10 @@ class StreamRunner:
         self.compute_stream = torch.cuda.Stream(device=self.device)
         self.slots = [self._slot() for _ in range(2)]
         self._next = 0
+        # host staging copies, one recording per thread (numpy copies run
+        # without the GIL): a batch is ~90 MB of PCM, which one core copies
+        # more slowly than the GPU classifies it
+        self._pool = ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1))
 
     def _slot(self):
         dev, W, M = self.device, self.max_windows, len(self.models)
@@ -116,9 +122,10 @@ class StreamRunner:
         rows, begins, counts, owners = [], [], [], []
         off = 0
         h_pcm = slot["h_pcm"].numpy()
+        copies = []
         for rec, views in batch:
             n = len(rec.pcm)
-            h_pcm[off:off + n] = rec.pcm
+            copies.append(self._pool.submit(np.copyto, h_pcm[off:off + n], rec.pcm))
             for ti, tv in enumerate(views):
                 if not tv:
                     continue
@@ -127,6 +134,8 @@ class StreamRunner:
                 owners.append((rec.key, ti))
                 rows.extend(pack_windows(tv, n, offset=off))
             off += n
+        for c in copies:
+            c.result()
         nw, nt = len(rows), len(owners)
         if nw:
             slot["h_win"].numpy()[:nw] = np.asarray(rows, dtype=np.int64)
