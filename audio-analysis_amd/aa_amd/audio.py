@@ -48,7 +48,10 @@ def decode_flac(data):
     info = FlacInfo()
     check(lib().aa_flac_info(buf.ctypes.data, buf.size, C.byref(info)), "aa_flac_info")
     n = C.c_int64()
-    if info.total_frames == 0:  # length not stated: count first
+    # length not stated, or a header claiming more samples than any plausible
+    # compression of this file holds (a bogus STREAMINFO must not size a huge
+    # allocation): count the decodable frames first
+    if info.total_frames == 0 or info.total_frames * info.channels > 64 * len(data) + (1 << 24):
         check(lib().aa_flac_decode(buf.ctypes.data, buf.size, None, 0, C.byref(n)), "aa_flac_decode")
         cap = n.value
     else:
@@ -104,8 +107,14 @@ def decode(path):
         else:
             raise ValueError(f"{path}: {bits}-bit PCM unsupported")
     elif tag == 3:  # IEEE float -> av_clip_int16(lrint(x * 32768))
+        if bits not in (32, 64):
+            raise ValueError(f"{path}: {bits}-bit IEEE float unsupported")
         f = np.frombuffer(payload[:len(payload) // (bits // 8) * (bits // 8)], "<f4" if bits == 32 else "<f8")
-        q = np.clip(np.rint(f.astype(np.float64) * 32768.0), -32768, 32767)
+        with np.errstate(invalid="ignore"):
+            q = np.clip(np.rint(f.astype(np.float64) * 32768.0), -32768, 32767)
+        # a NaN converts to the integer indefinite (INT_MIN) and clips to -32768,
+        # as libswresample's packed float -> s16 conversion does
+        q = np.where(np.isnan(q), -32768.0, q)
     else:
         raise ValueError(f"{path}: WAVE format tag {tag} unsupported")
     return _to_mono(q, channels), int(sr)

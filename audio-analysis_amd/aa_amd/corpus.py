@@ -87,11 +87,26 @@ def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world
             # independent of which rank ran it and what ran before
             np.random.seed(i)
             t0 = time.time()
-            summary = examine_fn(str(f), bird_models, analyse_tracks=analyse_tracks)
-            summary["processing_time_seconds"] = round(time.time() - t0, 1)
+            try:
+                summary = examine_fn(str(f), bird_models, analyse_tracks=analyse_tracks)
+                summary["processing_time_seconds"] = round(time.time() - t0, 1)
+            except Exception as e:
+                # the reference's per-file process logs and exits 1 without a
+                # sidecar (src/analyse.py:482-487); here the failure stays with
+                # its file and the collective below still runs on every rank
+                logging.error("Terminated with error", exc_info=True)
+                summary = {FAILED: f"{type(e).__name__}: {e}"}
+            finally:
+                it._PREFETCHED.pop((str(f), 48000), None)
             local[i] = summary
-            it._PREFETCHED.pop((str(f), 48000), None)
     return gather_documents(local, device=device)
+
+
+FAILED = "__failed__"  # marks a file whose examine() raised: no sidecar is written for it
+
+
+def failed(result) -> bool:
+    return FAILED in result
 
 
 def write_results(files, results, to_stdout=False):
@@ -99,11 +114,14 @@ def write_results(files, results, to_stdout=False):
     merged into an existing sidecar (src/analyse.py:454-468) -- or, with -o,
     one JSON list of {"file", "analysis_result"} on stdout."""
     if to_stdout:
-        print(json.dumps([{"file": str(files[i]), "analysis_result": r} for i, r in results.items()],
-                         sort_keys=True, indent=4))
+        print(json.dumps([{"file": str(files[i]), "analysis_result": r} for i, r in results.items()
+                          if not failed(r)], sort_keys=True, indent=4))
         return
     from .analyse import write_metadata
     for i, r in results.items():
+        if failed(r):
+            logging.error("%s: not analysed (%s)", files[i], r[FAILED])
+            continue
         write_metadata(files[i], r)
 
 

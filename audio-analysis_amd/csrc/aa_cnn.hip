@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void conv_small(const float* __restrict__ in, 
             if (has_mag) v = powf(v, mag_exp);
             x[i * KW + j] = v;
         }
-    TO* o = out + (size_t)(n * Hc * Wc + p) * COUT;
+    TO* o = out + ((size_t)n * Hc * Wc + p) * COUT;
 #pragma unroll
     for (int c0 = 0; c0 < COUT; c0 += 8) {
         float r[8];
@@ -1246,9 +1246,10 @@ template <int KH, int KW, int CIN, int WM, int WN, int MF, int NF, int POOL, int
 static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream_t st, const Stage* first) {
     auto k = conv_x3<KH, KW, CIN, WM, WN, MF, NF, POOL, TH, TW, FUSED, 0, RING, AJIT, OCC, IN_SPLIT, OUT_SPLIT>;
     constexpr int BN = WN * NF * 16;
-    // buffer-resource addressing (32-bit byte offsets) of activations and weights
-    AA_CHECK((double)n * s.Hin * s.Win * s.cin * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
-             "conv %s: batch %d too large for one launch", s.name.c_str(), n);
+    // buffer-resource addressing: the resources are based at the window
+    // (64-bit), offsets inside one window are 32-bit
+    AA_CHECK((double)s.Hin * s.Win * s.cin * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
+             "conv %s: one window's activations exceed 2 GiB", s.name.c_str());
     const size_t lds = x3_lds_bytes<KH, KW, CIN, BN, TH, TW, FUSED, RING>();
     FirstConv fc{};
     if (FUSED) {
@@ -1276,8 +1277,8 @@ template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int
 static int launch_wg(const Stage& s, const void* in, void* out, int n, hipStream_t st) {
     auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IN_SPLIT, OUT_SPLIT>;
     constexpr int BN = WN * NF * 16;
-    AA_CHECK((double)n * s.Hin * s.Win * s.cin * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
-             "conv %s: batch %d too large for one launch", s.name.c_str(), n);
+    AA_CHECK((double)s.Hin * s.Win * s.cin * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
+             "conv %s: one window's activations exceed 2 GiB", s.name.c_str());
     const size_t lds = wg_lds_bytes<KH, BN, TH, TW>();
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
     static size_t attr = 0;
@@ -1865,6 +1866,21 @@ extern "C" int aa_model_forward(void* model, const void* x, int32_t n, float* lo
     char* buf[2] = {static_cast<char*>(workspace),
                     static_cast<char*>(workspace) + align_up(m->act_elems[0] * es * n, 256)};
     hipStream_t st = static_cast<hipStream_t>(stream);
+    // launch grids carry the window index in blockIdx.z (at most 65,535):
+    // larger batches run as consecutive chunks through the same workspace
+    constexpr int32_t CHUNK = 32768;
+    if (n > CHUNK) {
+        const size_t in_bytes = (size_t)m->in_h * m->in_w * m->in_c *
+                                (m->st.size() >= 2 && m->st[1].lm_f16 ? 2 : 4);
+        for (int32_t c0 = 0; c0 < n; c0 += CHUNK) {
+            const int32_t nc = std::min(CHUNK, n - c0);
+            const int rc = aa_model_forward(model, static_cast<const char*>(x) + (size_t)c0 * in_bytes, nc,
+                                            logits + (size_t)c0 * m->L, probs ? probs + (size_t)c0 * m->L : nullptr,
+                                            workspace, workspace_bytes, stream);
+            if (rc != AA_OK) return rc;
+        }
+        return AA_OK;
+    }
     const void* in = x;
     for (size_t k = 0; k < m->st.size(); ++k) {
         Stage& s = m->st[k];

@@ -140,9 +140,10 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     };
 
     // one input value quad (4 channels of group g) of pixel (gh, gw), in f32
-    // (buffer loads: the window's base in an SGPR offset, the pixel in the lane's 32-bit offset)
-    const __amdgpu_buffer_rsrc_t ars = x3_wrsrc(in);
-    const int wbase = __builtin_amdgcn_readfirstlane(n * Hin * Win * CIN * 4);
+    // (buffer loads: the resource based at the window (64-bit), the pixel in the
+    // lane's 32-bit offset -- any batch size, one window < 2 GiB)
+    const __amdgpu_buffer_rsrc_t ars = x3_wrsrc(reinterpret_cast<const char*>(in) + (size_t)n * Hin * Win * CIN * 4);
+    constexpr int wbase = 0;
     auto load4 = [&](int gh, int gw, int g, int cq) -> float4 {
         const int pix = gh * Win + gw;
         if constexpr (IN_SPLIT) {

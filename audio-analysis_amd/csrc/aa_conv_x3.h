@@ -450,10 +450,12 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             // (slot - R*TW - C) & 7 of pixel (R, C).  Out-of-image pixels read a
             // clamped (finite) pixel: they only feed discarded outputs.
             constexpr int UNITS = PH * PW * 8;
-            // buffer loads: the window's and group's base in the SGPR offset,
-            // the pixel / unit in the lane's VGPR offset
-            const __amdgpu_buffer_rsrc_t ars = x3_wrsrc(in);
-            const int abase_s = __builtin_amdgcn_readfirstlane(n * Hin * Win * CIN * 4 + g * 128);
+            // buffer loads: the resource based at the window (64-bit, so any
+            // batch size), the group's base in the SGPR offset, the pixel /
+            // unit in the lane's VGPR offset
+            const __amdgpu_buffer_rsrc_t ars =
+                x3_wrsrc(reinterpret_cast<const char*>(in) + (size_t)n * Hin * Win * CIN * 4);
+            const int abase_s = g * 128;
             for (int i0 = wave0 * 64; i0 < UNITS; i0 += NW * 64) {
                 const int idx = i0 + lane;
                 if (idx < UNITS) {
@@ -515,10 +517,12 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             // bf16 lo in the high half of a dword (AA_X3_XSPLIT), else f32
             float* X = reinterpret_cast<float*>(smem + (size_t)PH * PW * 128);
             uint32_t* Xs = reinterpret_cast<uint32_t*>(X);
-            // buffer loads: the window's base in an SGPR offset, the element in the lane's offset
-            const __amdgpu_buffer_rsrc_t lrs = x3_wrsrc(in);
+            // buffer loads: the resource based at the window (64-bit, so any
+            // batch size), the element in the lane's offset
             const int esz = fc.lm_f16 ? 2 : 4;
-            const int lbase = __builtin_amdgcn_readfirstlane(n * fc.H0 * fc.W0 * esz);
+            const __amdgpu_buffer_rsrc_t lrs =
+                x3_wrsrc(reinterpret_cast<const char*>(in) + (size_t)n * fc.H0 * fc.W0 * esz);
+            constexpr int lbase = 0;
             // XU elements per thread and pass (XN = 400 for 12x21 tiles: one
             // pass of 2 over 256 threads), split in pairs
             constexpr int XU = (XN + NTHR - 1) / NTHR <= 2 ? 2 : 4;

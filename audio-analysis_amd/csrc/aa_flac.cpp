@@ -204,12 +204,16 @@ int read_subframe(BitReader& br, int block, int bps, int64_t* s) {
         for (int i = 0; i < order; ++i) s[i] = br.get_signed(bps);
         int rc = read_residual(br, block, order, s);
         if (rc) return rc;
+        // predictions in wrapping uint64 arithmetic: a conforming stream never
+        // overflows (identical results), a crafted one cannot reach undefined
+        // behaviour
+        uint64_t* u = reinterpret_cast<uint64_t*>(s);
         switch (order) {
             case 0: break;
-            case 1: for (int i = 1; i < block; ++i) s[i] += s[i - 1]; break;
-            case 2: for (int i = 2; i < block; ++i) s[i] += 2 * s[i - 1] - s[i - 2]; break;
-            case 3: for (int i = 3; i < block; ++i) s[i] += 3 * s[i - 1] - 3 * s[i - 2] + s[i - 3]; break;
-            default: for (int i = 4; i < block; ++i) s[i] += 4 * s[i - 1] - 6 * s[i - 2] + 4 * s[i - 3] - s[i - 4];
+            case 1: for (int i = 1; i < block; ++i) u[i] += u[i - 1]; break;
+            case 2: for (int i = 2; i < block; ++i) u[i] += 2 * u[i - 1] - u[i - 2]; break;
+            case 3: for (int i = 3; i < block; ++i) u[i] += 3 * u[i - 1] - 3 * u[i - 2] + u[i - 3]; break;
+            default: for (int i = 4; i < block; ++i) u[i] += 4 * u[i - 1] - 6 * u[i - 2] + 4 * u[i - 3] - u[i - 4];
         }
     } else if (type >= 32) {  // LPC, order 1-32
         const int order = type - 31;
@@ -223,10 +227,10 @@ int read_subframe(BitReader& br, int block, int bps, int64_t* s) {
         for (int j = 0; j < order; ++j) c[j] = br.get_signed(prec);
         int rc = read_residual(br, block, order, s);
         if (rc) return rc;
-        for (int i = order; i < block; ++i) {
-            int64_t acc = 0;
-            for (int j = 0; j < order; ++j) acc += c[j] * s[i - 1 - j];
-            s[i] += acc >> shift;
+        for (int i = order; i < block; ++i) {  // wrapping, as above
+            uint64_t acc = 0;
+            for (int j = 0; j < order; ++j) acc += (uint64_t)c[j] * (uint64_t)s[i - 1 - j];
+            s[i] = (int64_t)((uint64_t)s[i] + (uint64_t)((int64_t)acc >> shift));
         }
     } else {
         AA_CHECK(false, AA_ERR_INVALID, "FLAC: reserved subframe type %d", type);
@@ -286,15 +290,16 @@ int decode_frame(const uint8_t* d, size_t len, size_t& pos, const StreamInfo& si
     AA_CHECK(crc16(d + pos, body_end - pos) == want, AA_ERR_INVALID, "FLAC: frame CRC mismatch at byte %zu", pos);
     int64_t* a = ch[0].data();
     int64_t* b = nch > 1 ? ch[1].data() : nullptr;
+    // stereo decorrelation, wrapping like the predictions
     if (ch_code == 8) {         // left, side: right = left - side
-        for (int i = 0; i < block; ++i) b[i] = a[i] - b[i];
+        for (int i = 0; i < block; ++i) b[i] = (int64_t)((uint64_t)a[i] - (uint64_t)b[i]);
     } else if (ch_code == 9) {  // side, right: left = side + right
-        for (int i = 0; i < block; ++i) a[i] += b[i];
+        for (int i = 0; i < block; ++i) a[i] = (int64_t)((uint64_t)a[i] + (uint64_t)b[i]);
     } else if (ch_code == 10) { // mid, side
         for (int i = 0; i < block; ++i) {
             const int64_t side = b[i], mid = (int64_t)((uint64_t)a[i] << 1) | (side & 1);
-            a[i] = (mid + side) >> 1;
-            b[i] = (mid - side) >> 1;
+            a[i] = (int64_t)((uint64_t)mid + (uint64_t)side) >> 1;
+            b[i] = (int64_t)((uint64_t)mid - (uint64_t)side) >> 1;
         }
     }
     pos = body_end + 2;

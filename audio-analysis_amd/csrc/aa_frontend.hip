@@ -1046,6 +1046,19 @@ extern "C" int aa_fe_run(void* plan, const float* pcm, int64_t pcm_len, const aa
     AA_CHECK(n_win >= 0, AA_ERR_INVALID, "aa_fe_run: n_win < 0");
     (void)pcm_len;  // window views are validated by the host against pcm_len
     if (n_win == 0) return AA_OK;
+    // the per-window grids carry the window in blockIdx.y (at most 65,535):
+    // larger batches run as consecutive chunks through the same workspace
+    constexpr int32_t CHUNK = 32768;
+    if (n_win > CHUNK) {
+        const size_t ob = (size_t)p->cfg.n_mels * p->T * p->cfg.channels * (p->cfg.out_f16 ? 2 : 4);
+        for (int32_t c0 = 0; c0 < n_win; c0 += CHUNK) {
+            const int32_t nc = std::min(CHUNK, n_win - c0);
+            const int rc = aa_fe_run(plan, pcm, pcm_len, windows + c0, nc, static_cast<char*>(out) + c0 * ob,
+                                     win_status ? win_status + c0 : nullptr, workspace, workspace_bytes, stream);
+            if (rc != AA_OK) return rc;
+        }
+        return AA_OK;
+    }
     FeWs ws = fe_ws_layout(*p, n_win, static_cast<char*>(workspace));
     AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE,
              "aa_fe_run: workspace %zu < %zu bytes", workspace_bytes, ws.bytes);

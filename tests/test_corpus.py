@@ -33,16 +33,22 @@ def fake_examine(path, models, analyse_tracks=False):
         "non_bird_tags": ["noise"], "models": list(models), "tracks": analyse_tracks}
 
 
+def bad_examine(path, models, analyse_tracks=False):
+    if path.endswith("rec03.wav"):
+        raise ValueError("Could not load rec03.wav")  # e.g. an unsupported codec
+    return fake_examine(path, models, analyse_tracks)
+
+
 def _strip(res):
     return json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "processing_time_seconds"}
                        for k, v in res.items()}, sort_keys=True)
 
 
-def _cpu_worker(rank, world, port, q):
+def _cpu_worker(rank, world, port, q, examine=fake_examine):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, _strip(corpus.run(FILES, ["m1", "m2"], True, examine_fn=fake_examine, rank=rank,
+        q.put((rank, _strip(corpus.run(FILES, ["m1", "m2"], True, examine_fn=examine, rank=rank,
                                        world=world))))
     finally:
         dist.destroy_process_group()
@@ -73,6 +79,22 @@ def test_corpus_gloo_matches_single_process(world):
     outs = _spawn(_cpu_worker, world)
     for r in range(world):
         assert outs[r] == single  # every rank holds every file's document, byte for byte
+
+
+def test_corpus_failed_file_does_not_stall_the_gather(tmp_path):
+    """A file whose examine() raises (the reference's process would log and
+    exit 1 for that file alone) is marked failed; the all-gather still
+    completes on every rank, the other files keep their results, and no
+    sidecar is written for the failed one."""
+    single = json.loads(_strip(corpus.run(FILES, ["m1", "m2"], True, examine_fn=bad_examine)))
+    assert corpus.FAILED in single["3"] and len(single) == len(FILES)
+    outs = _spawn(_cpu_worker, 2, bad_examine)
+    assert outs[0] == outs[1] == json.dumps(single, sort_keys=True)
+    files = [str(tmp_path / f) for f in FILES]
+    res = corpus.run(files, ["m1"], True, examine_fn=bad_examine)
+    corpus.write_results(files, res)
+    written = sorted(p.name for p in tmp_path.glob("*.txt"))
+    assert written == [f"rec{i:02d}.txt" for i in range(7) if i != 3]
 
 
 def _gpu_worker(rank, world, port, q, files, models):

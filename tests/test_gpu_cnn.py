@@ -63,6 +63,29 @@ def test_cnn_bf16x3_parity(gpu, model_root, name, T):
     assert np.abs(pr - rpr).max() <= LOGIT_TOL
 
 
+@pytest.mark.parametrize("T,n", [(226, 600), (513, 300)])
+def test_cnn_bf16x3_large_batch(gpu, model_root, T, n):
+    """Batches above the old 2^31-byte launch limit (~473 windows at T = 226,
+    ~207 at T = 513): the split-bf16 kernels address each window through a
+    buffer resource based at that window, so one forward over n windows gives
+    the same logits bit for bit as the same windows in batches of 50, and the
+    oracle's on a sample of them."""
+    from aa_amd.model import Model
+    path = model_root / "model1" / "audioModel.safetensors"
+    rng = np.random.default_rng(T)
+    base = calibration_input(10, 160, T, True, rng)
+    x = np.concatenate([base[rng.permutation(10)] + rng.normal(0, 0.5, (10, 160, T, 1)).astype(np.float32)
+                        for _ in range(n // 10)])
+    m = Model(path, x.shape[1:], precision="bf16x3")
+    xt = torch.from_numpy(x).cuda()
+    lg_all = m.forward(xt)[0].cpu().numpy()
+    lg_parts = np.concatenate([m.forward(xt[i:i + 50])[0].cpu().numpy() for i in range(0, n, 50)])
+    assert np.array_equal(lg_all, lg_parts)
+    pick = np.r_[0:3, n - 3:n]
+    rlg, _ = cnn_oracle.forward(path, x[pick])
+    assert np.abs(lg_all[pick] - rlg).max() <= LOGIT_TOL
+
+
 def test_cnn_bf16x3_magtransform(gpu, tmp_path):
     path = make_model(tmp_path / "mag3", name="magmodel", seed=11, mag=2)
     x = calibration_input(3, 160, 226, False, np.random.default_rng(5))
