@@ -12,7 +12,8 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG.parent / "csrc"
 INCLUDE = PKG.parent.parent / "include"
 LIB = PKG / "libaa.so"
-SOURCES = ["aa_api.cpp", "aa_frontend.hip", "aa_cnn.hip", "aa_scan.hip", "aa_signal.hip", "aa_flac.cpp"]
+SOURCES = ["aa_api.cpp", "aa_frontend.hip", "aa_cnn.hip", "aa_scan.hip", "aa_signal.hip", "aa_flac.cpp",
+           "aa_resample.hip"]
 ARCH = os.environ.get("AA_OFFLOAD_ARCH", "gfx950")
 # per-source flags: the FFT front end is written in scalar f32; SLP packing it
 # into v_pk_* ops needs paired SGPR constants and register shuffles that push

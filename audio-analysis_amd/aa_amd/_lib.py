@@ -116,6 +116,9 @@ _SIGS = {
                                 C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "aa_span_nonzero": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p,
                                   C.c_void_p]),
+    "aa_pcm_s16_to_f32": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p]),
+    "aa_resample_poly": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                   C.c_int32, C.c_void_p, C.c_int64, C.c_void_p]),
     "aa_sn_create": (C.c_int, [C.POINTER(SnConfig), C.POINTER(C.c_void_p)]),
     "aa_sn_destroy": (C.c_int, [C.c_void_p]),
     "aa_sn_geometry": (C.c_int, [C.POINTER(SnConfig), C.POINTER(C.c_int32)]),

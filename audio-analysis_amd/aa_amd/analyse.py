@@ -220,17 +220,29 @@ def filter_by_location(meta_data, tracks):
                 mr.add_prediction("bird", conf, None, thr, normalize_confidence=False)
 
 
-def species_identify(file_name, bird_models, analyse_tracks):
-    labels = []
-    result = {}
+def read_sidecar(file_name):
+    """The recording's FILE.txt metadata (tracks, location), or None (:132-137)."""
     meta_file = Path(file_name).with_suffix(".txt")
-    meta_data = None
-    region_code = None
     if meta_file.exists():
         with meta_file.open("r") as f:
-            meta_data = json.load(f)
-    if bird_models is not None:
-        res = classify(file_name, bird_models, analyse_tracks, meta_data)
+            return json.load(f)
+    return None
+
+
+def species_identify(file_name, bird_models, analyse_tracks):
+    meta_data = read_sidecar(file_name)
+    res = classify(file_name, bird_models, analyse_tracks, meta_data) if bird_models is not None else None
+    return species_result(res, meta_data, analyse_tracks, bird_models is not None)
+
+
+def species_result(res, meta_data, analyse_tracks, have_models=True):
+    """species_identify's result document from classify()'s return value
+    (src/analyse.py:129-175); shared by the per-file path and the batched
+    corpus runner (aa_amd.batch), so both write the same JSON."""
+    labels = []
+    result = {}
+    region_code = None
+    if have_models:
         if res is not None:
             tracks, length, signals, raw_length, bird_labels = res
             if meta_data is not None:

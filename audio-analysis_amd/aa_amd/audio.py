@@ -13,14 +13,13 @@ libaa.so, host code) and go through the same s16 conversion: ffmpeg's FLAC
 decoder left-justifies a b-bit sample into s16 (b <= 16) or s32, so the s16
 value is ``x << (16 - b)`` or ``x >> (b - 16)``.  Other containers (MP3, Ogg,
 AAC/M4A, Opus) need a codec this image does not have and are rejected.
-Resampling to 48 kHz (librosa soxr_hq in the reference) uses a polyphase FIR
--- parity unpinned: soxr is not available.
+Resampling to 48 kHz (librosa soxr_hq in the reference) runs on the GPU with
+a filter designed to libsoxr's HQ specification (aa_amd.resample) -- parity
+with libsoxr's samples unpinned: libsoxr is not available.
 """
 from __future__ import annotations
 
 import struct
-from math import gcd
-
 import numpy as np
 
 
@@ -120,7 +119,7 @@ def decode(path):
     return _to_mono(q, channels), int(sr)
 
 
-def resample_poly(x, sr_in, sr_out):
-    from scipy.signal import resample_poly as rp
-    g = gcd(int(sr_in), int(sr_out))
-    return rp(x, sr_out // g, sr_in // g).astype(np.float32)
+def resample(x, sr_in, sr_out):
+    """librosa.resample(res_type="soxr_hq") to sr_out, on the GPU (aa_amd.resample)."""
+    from .resample import resample as gpu_resample
+    return gpu_resample(x, sr_in, sr_out)

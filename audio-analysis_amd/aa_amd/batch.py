@@ -1,0 +1,445 @@
+"""Batched corpus analysis: K recordings per GPU pass (BASELINE configs[3]).
+
+The reference analyses one recording per process (``analyse.py FILE``,
+src/analyse.py:434-470 -> classify(), src/identify_tracks.py:416-573).  Per
+file that is decode, get_end, signal_noise, the track builder, the front end
+and the models over the tracks' windows, and the post-processing to JSON.
+On the GPU every one of those device steps is small for a single 60 s file
+(tens of microseconds), so running them file by file leaves the device idle
+behind launch latencies and blocking readbacks.  Here a rank takes its files
+K at a time:
+
+  * decode: worker threads read each PCM16 48 kHz WAV straight into a pinned
+    host slot (other formats and rates go through ``load_recording``); the
+    batch crosses PCIe as int16 and ``aa_pcm_s16_to_f32`` widens it on the
+    device exactly as the host decode would;
+  * get_end: one ``aa_span_nonzero`` launch over every file's chunk spans,
+    one readback;
+  * signal_noise: one ``aa_sn_run`` per file back to back into per-file
+    result slots, one readback of the counts and component rows;
+  * tracks: host, per file (as the reference);
+  * classify: ``Classifier.classify_batch`` -- one front-end launch set over
+    every file's windows, one forward per model, one track mean, one copy;
+  * post-processing (``analyse.species_result``) on a host thread while the
+    next batch runs on the device.
+
+Each file's result is the document ``analyse.examine`` writes for it alone,
+byte for byte (tests/test_gpu_batch.py): numpy's global RandomState is
+reseeded per file right before its window schedule, exactly as the per-file
+corpus path seeds it before ``examine``.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import struct
+import time
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+
+SR = 48000
+
+
+@dataclass
+class Decoded:
+    """A decoded recording: ``s16`` (interleaved int16 samples as a view of a
+    pinned slot, ``channels`` of them per frame) or ``f32`` (mono samples at
+    ``sr_in``, resampled to 48 kHz on the device as they are uploaded)."""
+    n: int                   # frames at 48 kHz
+    sr: int                  # 48000
+    s16: object = None       # numpy int16 [n * channels] (view into a pinned slot)
+    s16_t: object = None     # the same bytes as a pinned torch int16 tensor
+    channels: int = 1
+    f32: object = None       # numpy float32 [n_in] at sr_in
+    sr_in: int = SR
+    slot: int = -1
+    dev: object = None       # the recording's samples in the batch's device PCM
+
+    def frames(self):
+        """Host float32 samples at 48 kHz (only band-pass filtered tracks need them)."""
+        if self.f32 is None:
+            from .audio import _to_mono
+            self.f32 = _to_mono(np.asarray(self.s16), self.channels)
+        if self.sr_in != SR:
+            return self.dev.cpu().numpy()
+        return self.f32
+
+
+def _wav_pcm16(buf: np.ndarray, size: int):
+    """(data offset, data bytes, channels, sr) if buf[:size] is a PCM16 RIFF/WAVE
+    file, else None (decode() handles everything else)."""
+    b = buf[:min(size, 1 << 16)].tobytes()
+    if len(b) < 12 or b[:4] != b"RIFF" or b[8:12] != b"WAVE":
+        return None
+    pos, fmt = 12, None
+    while pos + 8 <= size:
+        if pos + 8 > len(b):
+            b = buf[:min(size, pos + (1 << 16))].tobytes()
+        cid, csz = b[pos:pos + 4], struct.unpack("<I", b[pos + 4:pos + 8])[0]
+        if cid == b"fmt ":
+            if pos + 8 + 16 > len(b):
+                return None
+            fmt = struct.unpack("<HHIIHH", b[pos + 8:pos + 24])
+            if fmt[0] == 0xFFFE and csz >= 26 and pos + 34 <= len(b):
+                fmt = (struct.unpack("<H", b[pos + 32:pos + 34])[0],) + fmt[1:]
+        elif cid == b"data":
+            if fmt is None:
+                return None
+            tag, ch, sr, _, _, bits = fmt
+            if tag != 1 or bits != 16 or not 1 <= ch <= 8 or (pos + 8) % 2:
+                return None
+            n = min(csz, size - pos - 8)
+            return pos + 8, n // (2 * ch) * 2 * ch, ch, sr
+        pos += 8 + csz + (csz & 1)
+    return None
+
+
+class SlotPool:
+    """Pinned host slots, each holding one file's bytes (one per recording in
+    flight: the prefetch depth plus the batch on the device)."""
+
+    def __init__(self, n_slots: int, slot_bytes: int):
+        self.bytes = int(slot_bytes)
+        self.t = [torch.empty(self.bytes, dtype=torch.uint8, pin_memory=True) for _ in range(n_slots)]
+        self.np = [t.numpy() for t in self.t]
+        self.free = list(range(n_slots))
+        import threading
+        self._cv = threading.Condition()
+
+    def get(self) -> int:
+        with self._cv:
+            while not self.free:
+                self._cv.wait()
+            return self.free.pop()
+
+    def put(self, i: int):
+        with self._cv:
+            self.free.append(i)
+            self._cv.notify()
+
+
+def decode_into(path, pool: SlotPool):
+    """Decode one file; PCM16 48 kHz WAV lands in a pinned slot untouched."""
+    from . import identify_tracks as it
+    size = os.path.getsize(path)
+    if size <= pool.bytes:
+        i = pool.get()
+        try:
+            buf = pool.np[i]
+            with open(path, "rb", buffering=0) as f:
+                got = f.readinto(memoryview(buf)[:size])
+            w = _wav_pcm16(buf, got)
+            if w is not None and w[3] == SR:
+                off, nb, ch, sr = w
+                t = pool.t[i][off:off + nb].view(torch.int16)
+                return Decoded(n=nb // (2 * ch), sr=sr, s16=buf[off:off + nb].view(np.int16), s16_t=t,
+                               channels=ch, slot=i)
+        except Exception:
+            pool.put(i)
+            raise
+        pool.put(i)
+    # FLAC, other WAV encodings; other rates are resampled on the device at upload
+    frames, sr = it.load_recording(str(path), resample=None)
+    from .resample import out_length
+    return Decoded(n=out_length(len(frames), sr, SR), sr=SR, f32=np.ascontiguousarray(frames, dtype=np.float32),
+                   sr_in=sr)
+
+
+class _Laps:
+    """Wall time per host phase of the batch loop (AA_BATCH_PROFILE=1 prints it)."""
+
+    def __init__(self):
+        self.t = {}
+
+    def lap(self, name, t0):
+        t1 = time.perf_counter()
+        self.t[name] = self.t.get(name, 0.0) + (t1 - t0)
+        return t1
+
+    def report(self):
+        return " ".join(f"{k}={1e3 * v:.1f}ms" for k, v in self.t.items())
+
+
+@dataclass
+class _Rec:
+    idx: int
+    path: str
+    dec: Decoded
+    meta: object
+    off: int = 0
+    length: float = 0.0
+    signals: list = field(default_factory=list)
+    tracks: list = field(default_factory=list)
+    res: object = None
+    err: object = None
+
+
+class BatchAnalyser:
+    """examine() for many files of one rank, K per device pass."""
+
+    def __init__(self, bird_models, analyse_tracks=False, device=None, precision=None, batch=16, workers=8):
+        from .identify_tracks import _group_models
+        from .pipeline import Classifier
+        self.bird_models = bird_models
+        self.analyse_tracks = bool(analyse_tracks)
+        self.dev = torch.device(device or "cuda")
+        self.K = int(batch)
+        self.workers = int(workers)
+        self.groups = _group_models(bird_models) if bird_models is not None else None
+        self.clf = Classifier.shared(precision=precision, device=self.dev)
+        self._pcm = torch.empty(0, dtype=torch.float32, device=self.dev)
+        self._s16 = torch.empty(0, dtype=torch.int16, device=self.dev)
+        self._copy = torch.cuda.Stream(device=self.dev)
+        self._sn_out = None
+        self.timing = _Laps()
+
+    # ---- device buffers -------------------------------------------------
+    def _buffers(self, n_f32, n_s16):
+        if self._pcm.numel() < n_f32:
+            self._pcm = torch.empty(int(n_f32 * 1.25) + 1, dtype=torch.float32, device=self.dev)
+        if self._s16.numel() < n_s16:
+            self._s16 = torch.empty(int(n_s16 * 1.25) + 1, dtype=torch.int16, device=self.dev)
+        return self._pcm, self._s16
+
+    # ---- one batch --------------------------------------------------------
+    def _upload(self, recs):
+        """PCM of the batch into one device f32 buffer (recording r at r.off)."""
+        total = sum(r.dec.n for r in recs)
+        n16 = sum(r.dec.n * r.dec.channels for r in recs if r.dec.s16 is not None)
+        pcm, s16 = self._buffers(total, n16)
+        cur = torch.cuda.current_stream(self.dev)
+        self._copy.wait_stream(cur)  # the previous batch is done with both buffers
+        off = o16 = 0
+        with torch.cuda.stream(self._copy):
+            for r in recs:
+                r.off = off
+                d = r.dec
+                if d.s16 is not None:
+                    s16[o16:o16 + d.s16_t.numel()].copy_(d.s16_t, non_blocking=True)
+                    d.o16 = o16
+                    o16 += d.s16_t.numel()
+                elif d.sr_in == SR:
+                    pcm[off:off + d.n].copy_(torch.from_numpy(d.f32), non_blocking=False)
+                off += d.n
+        cur.wait_stream(self._copy)
+        done = torch.cuda.Event()
+        done.record(self._copy)
+        L = _lib.lib()
+        from .resample import resample_device
+        for r in recs:
+            d = r.dec
+            d.dev = pcm[r.off:r.off + d.n]
+            if d.s16 is not None and d.n:
+                _lib.check(L.aa_pcm_s16_to_f32(_lib.dptr(s16) + 2 * d.o16, d.n, d.channels,
+                                               _lib.dptr(pcm) + 4 * r.off, _lib.stream_ptr(cur)),
+                           "aa_pcm_s16_to_f32")
+            elif d.s16 is None and d.sr_in != SR:  # librosa.resample to 48 kHz (aa_amd.resample)
+                resample_device(torch.from_numpy(d.f32).to(self.dev), d.sr_in, SR, out=d.dev)
+        return pcm[:total], done
+
+    def _get_end(self, pcm, recs):
+        """get_end (src/identify_tracks.py:387-413) of every recording, one launch."""
+        from .gpu_ops import get_end_spans
+        spans, owner, starts = [], [], []
+        for k, r in enumerate(recs):
+            sp, st, hop = get_end_spans(r.dec.n, r.dec.sr)
+            r.length = r.dec.n / r.dec.sr
+            if len(st):
+                spans.append(sp + r.off)
+                owner += [k] * len(st)
+                starts += st
+        if not spans:
+            return
+        sp = torch.from_numpy(np.concatenate(spans)).to(self.dev)
+        flags = torch.empty(len(owner), dtype=torch.int32, device=self.dev)
+        _lib.check(_lib.lib().aa_span_nonzero(_lib.dptr(pcm), int(pcm.numel()), _lib.dptr(sp), len(owner),
+                                              _lib.dptr(flags), _lib.stream_ptr()), "aa_span_nonzero")
+        f = flags.cpu().numpy()
+        seen = set()
+        for j in np.flatnonzero(f == 0):
+            k = owner[j]
+            if k not in seen:  # the first constant chunk of recording k
+                seen.add(k)
+                recs[k].length = starts[j] * 281 // recs[k].dec.sr
+
+    def _signal_noise(self, pcm, recs):
+        """signal_noise (src/identify_tracks.py:650-706) of every recording:
+        back-to-back aa_sn_run launches into per-recording result slots, one
+        readback."""
+        from .identify_tracks import Signal
+        from .signals import detector
+        by_sr = {}
+        for k, r in enumerate(recs):
+            by_sr.setdefault(r.dec.sr, []).append(k)
+        cap = 4096
+        for sr, ks in by_sr.items():
+            det = detector(sr, 281, self.dev)
+            nsig = [int(sr * recs[k].length) for k in ks]
+            ws = det._workspace(max(nsig))
+            if self._sn_out is None or self._sn_out.shape[0] < len(ks):
+                self._sn_out = torch.empty((len(ks), cap, 6), dtype=torch.int32, device=self.dev)
+                self._sn_n = torch.zeros((len(ks), 2), dtype=torch.int32, device=self.dev)
+            out, cnt = self._sn_out, self._sn_n
+            L = _lib.lib()
+            for j, k in enumerate(ks):
+                r = recs[k]
+                _lib.check(L.aa_sn_run(det._h, _lib.dptr(pcm) + 4 * r.off if nsig[j] else 0, nsig[j], _lib.dptr(ws),
+                                       ws.numel(), _lib.dptr(out[j]), cap, _lib.dptr(cnt[j]), 0, _lib.stream_ptr()),
+                           "aa_sn_run")
+            n = cnt[:len(ks)].cpu().numpy()
+            top = int(min(cap, n[:, 0].max())) if len(ks) else 0
+            rows_all = out[:len(ks), :max(top, 1)].cpu().numpy()
+            for j, k in enumerate(ks):
+                c, status = int(n[j, 0]), int(n[j, 1])
+                if status & _lib.AA_SN_NONFINITE:
+                    recs[k].err = ValueError("Audio buffer is not finite everywhere")  # librosa valid_audio
+                    continue
+                if status & _lib.AA_SN_RUN_OVERFLOW or c > cap:
+                    # more components than the batch slots hold: this recording alone
+                    try:
+                        stats = det.components(pcm[recs[k].off:recs[k].off + nsig[j]])
+                    except Exception as e:
+                        recs[k].err = e
+                        continue
+                else:
+                    rows = rows_all[j, :c].astype(np.int64)
+                    stats = rows[np.lexsort((rows[:, 5], rows[:, 0]))][:, :5]
+                recs[k].signals = [Signal(*t) for t in det.to_tuples(stats)]
+
+    def _classify(self, pcm, recs):
+        from .identify_tracks import MAX_FRQUENCY, Signal, get_tracks_from_signals
+        from .pipeline import BatchRec
+        todo = []
+        for r in recs:
+            if r.err is not None:
+                continue
+            raw_length = r.dec.n / r.dec.sr
+            if self.analyse_tracks:
+                if r.meta is None:
+                    r.res = None
+                    continue
+                tracks = []
+                for t in r.meta["Tracks"]:
+                    s = Signal(t["start"], t["end"], t.get("minFreq", 0), t.get("maxFreq", MAX_FRQUENCY))
+                    s.track_id = t["id"]
+                    tracks.append(s)
+            else:
+                tracks = get_tracks_from_signals([s.copy() for s in r.signals], r.length)
+            if len(tracks) == 0:
+                r.res = ([], r.length, [], raw_length, [])
+                continue
+            r.tracks = tracks
+            todo.append(r)
+        if not todo:
+            return
+        sr = todo[0].dec.sr
+        if any(r.dec.sr != sr for r in todo):  # (load_recording resamples everything to 48 kHz)
+            for r in todo:
+                self._classify(pcm, [r])
+            return
+        brs = [BatchRec(n=r.dec.n, off=r.off, tracks=r.tracks, frames=r.dec.frames, seed=r.idx) for r in todo]
+        out = self.clf.classify_batch(pcm, sr, brs, self.groups)
+        for r, o in zip(todo, out):
+            if isinstance(o, BaseException):
+                r.err = o
+            else:
+                r.res = (r.tracks, r.length, r.signals, r.dec.n / r.dec.sr, list(o))
+
+    def _finish(self, recs, t0):
+        from .analyse import species_result
+        from .corpus import FAILED
+        out = {}
+        dt = round((time.time() - t0) / max(len(recs), 1), 1)
+        for r in recs:
+            if r.err is not None:
+                logging.error("%s: %s", r.path, r.err)
+                out[r.idx] = {FAILED: f"{type(r.err).__name__}: {r.err}"}
+                continue
+            doc = species_result(r.res, r.meta, self.analyse_tracks, self.bird_models is not None)
+            doc["processing_time_seconds"] = dt
+            out[r.idx] = doc
+        return out
+
+    def process(self, items, pool=None):
+        """items: [(file_idx, path, Decoded | Exception, sidecar meta)] -> {file_idx: document}."""
+        t0 = time.time()
+        recs, failed = [], []
+        for idx, path, dec, meta in items:
+            if isinstance(dec, BaseException):
+                failed.append(_Rec(idx, str(path), None, meta, err=dec))
+            else:
+                recs.append(_Rec(idx, str(path), dec, meta))
+        if recs and self.bird_models is not None:
+            try:
+                tm = self.timing
+                t = time.perf_counter()
+                pcm, _ = self._upload(recs)
+                t = tm.lap("upload", t)
+                self._get_end(pcm, recs)
+                t = tm.lap("get_end", t)
+                self._signal_noise(pcm, recs)
+                t = tm.lap("signal_noise", t)
+                self._classify(pcm, recs)
+                tm.lap("classify", t)
+            finally:
+                # (the slots stay held until here: band-pass filtered tracks
+                # read a recording's host samples during classify)
+                if pool is not None:
+                    for r in recs:
+                        if r.dec.slot >= 0:
+                            pool.put(r.dec.slot)
+                            r.dec.slot = -1
+        return recs + failed, t0
+
+    def run(self, jobs):
+        """jobs: [(file_idx, path)] -> {file_idx: document} (the files of this rank)."""
+        from .analyse import read_sidecar
+        if not jobs:
+            return {}
+        if self.bird_models is None:  # examine() without models reads no audio
+            from .analyse import species_result
+            return {i: dict(species_result(None, read_sidecar(p), self.analyse_tracks, False),
+                            processing_time_seconds=0.0) for i, p in sorted(jobs)}
+        K = self.K
+        slot_bytes = max(os.path.getsize(p) for _, p in jobs) + 4096
+        pool = SlotPool(min(len(jobs), 3 * K), slot_bytes)
+
+        def load(job):
+            idx, path = job
+            meta = None
+            try:
+                meta = read_sidecar(path)
+                return idx, path, decode_into(path, pool), meta
+            except Exception as e:
+                logging.error("Could not load %s", path, exc_info=True)
+                return idx, path, Exception(f"Could not load {path}") if not isinstance(e, ValueError) else e, meta
+
+        results = {}
+        with ThreadPoolExecutor(max_workers=self.workers) as io, ThreadPoolExecutor(max_workers=1) as post:
+            futs = [io.submit(load, j) for j in jobs[:2 * K]]
+            nxt = 2 * K
+            pending = None
+            for b0 in range(0, len(jobs), K):
+                t = time.perf_counter()
+                items = [f.result() for f in futs[:K]]
+                self.timing.lap("wait_decode", t)
+                futs = futs[K:]
+                while len(futs) < 2 * K and nxt < len(jobs):
+                    futs.append(io.submit(load, jobs[nxt]))
+                    nxt += 1
+                recs, t0 = self.process(items, pool)
+                t = time.perf_counter()
+                if pending is not None:
+                    results.update(pending.result())
+                self.timing.lap("wait_post", t)
+                pending = post.submit(self._finish, recs, t0)
+            if pending is not None:
+                results.update(pending.result())
+        if os.environ.get("AA_BATCH_PROFILE"):
+            logging.warning("batch phases over %d files: %s", len(jobs), self.timing.report())
+        return dict(sorted(results.items()))

@@ -54,16 +54,24 @@ def gather_documents(local: dict, device=None, group=None) -> dict:
     return dict(sorted(out.items()))
 
 
-def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world=1, device=None):
+def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world=1, device=None, batch=16):
     """Classify this rank's share of ``files``; returns {file_idx: summary}
     of ALL files on every rank (after the gather).  ``summary`` is what
-    analyse.examine returns plus ``processing_time_seconds`` (src/analyse.py:451-453)."""
+    analyse.examine returns plus ``processing_time_seconds`` (src/analyse.py:451-453).
+    With a GPU and the real examine, files go ``batch`` at a time through
+    aa_amd.batch (the same documents, byte for byte); ``batch=0`` or a
+    custom ``examine_fn`` runs them one by one."""
+    mine = shard.shard(list(files), rank, world)
+    if examine_fn is None and batch and torch.cuda.is_available():
+        from .batch import BatchAnalyser
+        ba = BatchAnalyser(bird_models, analyse_tracks, device=torch.device("cuda", torch.cuda.current_device()),
+                           batch=batch)
+        return gather_documents(ba.run([(i, str(f)) for i, f in mine]), device=device)
     if examine_fn is None:
         from .analyse import examine as examine_fn
     import numpy as np
     from concurrent.futures import ThreadPoolExecutor
     from . import identify_tracks as it
-    mine = shard.shard(list(files), rank, world)
     local = {}
 
     def decode(f):

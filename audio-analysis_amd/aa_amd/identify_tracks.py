@@ -224,8 +224,8 @@ def load_recording(file, resample=48000):
     try:
         frames, sr = decode(file)
         if resample is not None and resample != sr:
-            from .audio import resample_poly
-            frames = resample_poly(frames, sr, resample)
+            from .audio import resample as resample_to
+            frames = resample_to(frames, sr, resample)  # librosa.resample (soxr_hq), on the GPU
             sr = resample
         return frames, sr
     except Exception:

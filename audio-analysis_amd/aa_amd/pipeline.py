@@ -80,12 +80,35 @@ class Classifier:
         return self._models[key]
 
     def classify_tracks(self, frames, sr, tracks, groups, pcm=None):
-        from .identify_tracks import DEFAULT_BIRDS
+        """One recording (classify()): the batch core below with one entry,
+        the caller's RandomState as it is."""
         dev = self.device
         if pcm is None:
             pcm = torch.from_numpy(np.ascontiguousarray(frames, dtype=np.float32)).to(dev)
-        views = None
-        logmel = None
+        rec = BatchRec(n=len(frames), off=0, tracks=tracks, frames=lambda: frames, seed=None)
+        res = self.classify_batch(pcm, sr, [rec], groups, raise_errors=True)[0]
+        if isinstance(res, BaseException):
+            raise res
+        return res
+
+    def classify_batch(self, pcm, sr, recs, groups, raise_errors=False):
+        """The model-group loop of classify() (src/identify_tracks.py:444-571)
+        for several recordings at once: every recording's windows in one
+        front-end launch set, one forward per model, one track mean, one
+        device->host copy.  ``pcm``: device f32 holding recording r at
+        ``recs[r].off``.  A recording with ``seed`` set reseeds numpy's global
+        RandomState right before its window schedule (what aa_amd.corpus does
+        per file), so its windows do not depend on its batch neighbours.
+        Returns per recording the bird labels (a set), or the exception the
+        single-recording path would have raised for it (non-finite audio);
+        the results land on each recording's tracks.  ``raise_errors``: raise
+        a recording's exception instead (the single-recording path)."""
+        from .identify_tracks import DEFAULT_BIRDS
+        dev = self.device
+        R = len(recs)
+        errs = [None] * R
+        views = None  # per recording: per track window views (global sample offsets)
+        logmel = rows = fe = None
         bird_labels = set()
         for group in groups:
             if len(group) > 1:
@@ -96,35 +119,55 @@ class Classifier:
                 # get_spect's MFCC branch (:269-280): librosa.feature.mfcc + tf.image.resize_with_pad
                 raise NotImplementedError("MFCC features (use_mfcc)")
             labels = meta.get("labels")
-            ebird_ids = meta.get("ebird_ids")
             model_name = meta.get("name", False)
-            pre_model = meta.get("pre_model", False)
-            prob_thresh = meta.get("threshold", 0.7)
             bird_labels.update(meta.get("bird_labels", DEFAULT_BIRDS))
             if model_name == "embeddings":
                 raise NotImplementedError("tensorflow_hub embedding models need a network fetch")
             if views is None:
-                views, spans = schedule(len(frames), sr, tracks, s.segment_length, meta.get("segment_stride", 1.5),
-                                        s.fmin, s.fmax, meta.get("pad_short_tracks", False), return_spans=True)
-                # band-pass filtered tracks (:152-162): their windows read a
-                # filtered copy appended after the recording's samples
-                extra, views = filtered_sources(frames, sr, tracks, views, spans, meta.get("filter_freq", False),
-                                                meta.get("filter_below", None), len(frames))
-                if len(extra):
-                    pcm = torch.cat([pcm, torch.from_numpy(extra).to(dev)])
-                flat = [v for tv in views for v in tv]
+                views, extras = [], []
+                extra_at = int(pcm.numel())
+                for i, r in enumerate(recs):
+                    if r.seed is not None:
+                        np.random.seed(r.seed)
+                    try:
+                        v, spans = schedule(r.n, sr, r.tracks, s.segment_length, meta.get("segment_stride", 1.5),
+                                            s.fmin, s.fmax, meta.get("pad_short_tracks", False), return_spans=True)
+                        # band-pass filtered tracks (:152-162): their windows read a
+                        # filtered copy appended after the batch's samples
+                        ff, fb = meta.get("filter_freq", False), meta.get("filter_below", None)
+                        if ff or fb:
+                            extra, v = filtered_sources(r.frames(), sr, r.tracks, v, spans, ff, fb, extra_at - r.off)
+                            if len(extra):
+                                extras.append(extra)
+                                extra_at += len(extra)
+                    except Exception as e:
+                        if raise_errors:
+                            raise
+                        errs[i] = e  # (e.g. :146's assertion on a recording shorter than a window)
+                        v = [[] for _ in r.tracks]
+                    views.append([[(src + r.off, n, p) for (src, n, p) in tv] for tv in v])
+                if extras:
+                    pcm = torch.cat([pcm, torch.from_numpy(np.concatenate(extras)).to(dev)])
+                flat = [w for rv in views for tv in rv for w in tv]
                 fe = self.frontend(s)
                 if flat:
                     rows = torch.from_numpy(pack_windows(flat, int(pcm.numel()), win_len=s.win_len)).to(dev)
                     status = torch.empty(len(flat), dtype=torch.int32, device=dev)
                     logmel = fe.run(pcm, rows, status=status)
-                    if int(status.max().item()) != 0:
-                        raise ValueError("Audio buffer is not finite everywhere")  # librosa valid_audio
+                    st = status.cpu().numpy()
+                    if st.any():  # librosa valid_audio, per recording
+                        k = 0
+                        for i, rv in enumerate(views):
+                            nw = sum(len(tv) for tv in rv)
+                            if st[k:k + nw].any():
+                                errs[i] = ValueError("Audio buffer is not finite everywhere")
+                            k += nw
             else:
                 logging.info("Re using track data this will cuase problems if the STFT settings are "
                              "not the same for multiple models")
-            counts = [len(tv) for tv in views]
-            if sum(counts) == 0:
+            counts = [[len(tv) for tv in rv] for rv in views]
+            total = sum(sum(c) for c in counts)
+            if total == 0:
                 continue
             group_mel = logmel
             if "efficientnet" in model_name.lower():
@@ -133,19 +176,38 @@ class Classifier:
                 # front end with three times the channels
                 fe3 = self.frontend(dataclasses.replace(fe.s, channels=fe.s.channels * 3))
                 group_mel = fe3.run(pcm, rows)
-            begin = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32)
-            probs = torch.empty((len(group), sum(counts), len(labels)), dtype=torch.float32, device=dev)
+            probs = torch.empty((len(group), total, len(labels)), dtype=torch.float32, device=dev)
             for k, (path, m_meta) in enumerate(group):
                 m = self.model(path, m_meta, group_mel.shape[1:])
                 if m.n_labels != len(labels):
                     raise ValueError(f"{path}: {m.n_labels} outputs for {len(labels)} labels")
                 m.forward(group_mel, probs=probs[k])
-            sel = [i for i, c in enumerate(counts) if c > 0]
+            # one track mean over every recording's tracks that have windows
+            flat_counts = np.asarray([c for rc in counts for c in rc], np.int64)
+            begin = np.concatenate([[0], np.cumsum(flat_counts)[:-1]]).astype(np.int32)
+            sel = np.flatnonzero(flat_counts > 0)
             wb = torch.from_numpy(begin[sel]).to(dev)
-            wc = torch.from_numpy(np.asarray(counts, np.int32)[sel]).to(dev)
+            wc = torch.from_numpy(flat_counts[sel].astype(np.int32)).to(dev)
             means = track_mean(probs, wb, wc).cpu().numpy()
-            apply_group_scores(tracks, sel, means, meta)
-        return bird_labels
+            row, t0 = 0, 0
+            for i, (r, rc) in enumerate(zip(recs, counts)):
+                nt = len(rc)
+                mine = [t for t in range(nt) if rc[t] > 0]
+                if mine and errs[i] is None:  # (a recording with no windows skips the group, :530-531)
+                    apply_group_scores(r.tracks, mine, means[row:row + len(mine)], meta)
+                row += len(mine)
+                t0 += nt
+        return [e if e is not None else set(bird_labels) for e in errs]
+
+
+@dataclasses.dataclass
+class BatchRec:
+    """One recording of a classify_batch call."""
+    n: int                 # samples
+    off: int               # first sample in the batch's device PCM
+    tracks: list           # Signal objects; results are appended to them
+    frames: object         # callable -> host float32 samples (band-pass filtering only)
+    seed: object = None    # np.random.seed before this recording's window schedule
 
 
 def apply_group_scores(tracks, track_idx, means, meta):

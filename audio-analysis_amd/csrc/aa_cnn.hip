@@ -1377,7 +1377,7 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
             constexpr int TH_ = TH, TW_ = TW, OCC_ = OCC;                                                  \
             constexpr bool RING_ = RING, AJIT_ = AJIT;                                                     \
             if (s.fused_first) {                                                                           \
-                if constexpr (CIN == 32 && KH == 3 && KW == 3 && WM * WN == 4)                             \
+                if constexpr (CIN == 32 && KH == 3 && KW == 3)                                             \
                     return s.out_split ? AA_X3L(true, false, true) : AA_X3L(true, false, false);          \
             } else if (s.in_split) {                                                                       \
                 return s.out_split ? AA_X3L(false, true, true) : AA_X3L(false, true, false);              \

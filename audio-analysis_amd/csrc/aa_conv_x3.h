@@ -260,7 +260,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     static_assert(TH * TW <= WM * MF * 16, "tile covered by the waves' fragments");
     static_assert(CIN % X3_CG == 0, "C_in multiple of 32");
     static_assert((KW - 1) % 2 == 0, "odd kernel width (the swizzle needs even row jumps)");
-    static_assert(!FUSED || (CIN == 32 && WM * WN == 4), "fused first layer: 32 channels, 4 waves");
+    static_assert(!FUSED || CIN == 32, "fused first layer: 32 channels");
     static_assert(!(FUSED && IN_SPLIT), "the fused first layer reads the f32 log-mel");
     constexpr int NTHR = WM * WN * 64;
     constexpr int BN = WN * NF * 16;
@@ -552,32 +552,39 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 }
             }
             const int l32 = lane & 31, kg = lane >> 5;
+            // MFMA row m (A operand lane m) computes first-layer channel
+            // 16 ((m >> 2) & 1) + 4 (m >> 3) + (m & 3), so that the D register r
+            // of a k-group kg lane (row 8 (r / 4) + 4 kg + r % 4) holds channel
+            // 16 kg + r: each lane owns two whole 8-channel units of its pixel
+            // and writes them as ds_write_b128 (eight consecutive pixels per
+            // lane group: conflict-free), not as eight half units
+            const int ch1 = 16 * ((l32 >> 2) & 1) + 4 * (l32 >> 3) + (l32 & 3);
             bf16x8 wa, wal;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int tap = 8 * kg + j;
-                const float wv = tap < 9 ? fc.w[l32 * 9 + tap] : 0.f;
+                const float wv = tap < 9 ? fc.w[ch1 * 9 + tap] : 0.f;
                 wa[j] = bf_hi(wv);
                 wal[j] = bf_lo(wv);
             }
-            f32x16 cb;  // D row (channel) of register r: 8 (r / 4) + 4 kg + r % 4
+            f32x16 cb;  // D register r: channel 16 kg + r
 #pragma unroll
-            for (int r = 0; r < 16; ++r) cb[r] = fc.b[8 * (r >> 2) + 4 * kg + (r & 3)];
+            for (int r = 0; r < 16; ++r) cb[r] = fc.b[16 * kg + r];
             const float ae = fc.alpha;  // host: act folded to a slope in [0, 1]
             const int off0 = kg ? 2 * XW + 2 : 0;  // k-group 1 only needs tap 8 (j = 0)
             __syncthreads();
             constexpr int NPX = PH * PW;
             constexpr int NGRP = (NPX + 31) / 32;
-            // NU groups of 32 pixels per wave and pass (groups g0 + 4 u): all
-            // of them in one pass when that takes at most 3 (12x21 tiles: 322
-            // patch pixels, 11 groups), else passes of 2
-            constexpr int NU = (NGRP + 3) / 4 <= 3 ? (NGRP + 3) / 4 : 2;
-            for (int g0 = wave0; g0 < ((DIAG & 64) ? 0 : NGRP); g0 += 4 * NU) {
+            // NU groups of 32 pixels per wave and pass (groups g0 + NW u): all
+            // of them in one pass when that takes at most 3 (12x21 tiles on 4
+            // waves: 322 patch pixels, 11 groups), else passes of 2
+            constexpr int NU = (NGRP + NW - 1) / NW <= 3 ? (NGRP + NW - 1) / NW : 2;
+            for (int g0 = wave0; g0 < ((DIAG & 64) ? 0 : NGRP); g0 += NW * NU) {
                 bf16x8 xh[NU], xl[NU];
                 int pix[NU];
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
-                    pix[u] = min((g0 + 4 * u) * 32 + l32, NPX - 1);
+                    pix[u] = min((g0 + NW * u) * 32 + l32, NPX - 1);
                     const int r = pix[u] / PW, c = pix[u] - r * PW;
                     if constexpr (AA_X3_XSPLIT) {
                         // taps 2k, 2k+1 of the pre-split patch -> one dword of
@@ -620,17 +627,17 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 for (int u = 0; u < NU; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wal, xh[u], d[u], 0, 0, 0);
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
-                    if ((g0 + 4 * u) * 32 + l32 < NPX) {
+                    if ((g0 + NW * u) * 32 + l32 < NPX) {
                         const int R = pix[u] / PW, C = pix[u] - R * PW;
 #pragma unroll
-                        for (int qq = 0; qq < 4; ++qq) {  // channels 8 qq + 4 kg + e: unit qq, byte 8 kg
-                            uint32_t hw[2], lw[2];
+                        for (int h = 0; h < 2; ++h) {  // channels 16 kg + 8 h + e: unit 2 kg + h
+                            uint32_t hw[4], lw[4];
 #pragma unroll
-                            for (int e = 0; e < 4; e += 2)
-                                leaky_split2(d[u][4 * qq + e], d[u][4 * qq + e + 1], ae, hw[e >> 1], lw[e >> 1]);
-                            const int a = x3_addr(R, C, qq, PW, TW) + kg * 8;
-                            *reinterpret_cast<uint2*>(patch + a) = make_uint2(hw[0], hw[1]);
-                            *reinterpret_cast<uint2*>(patch + (a ^ 64)) = make_uint2(lw[0], lw[1]);
+                            for (int e = 0; e < 8; e += 2)
+                                leaky_split2(d[u][8 * h + e], d[u][8 * h + e + 1], ae, hw[e >> 1], lw[e >> 1]);
+                            const int a = x3_addr(R, C, 2 * kg + h, PW, TW);
+                            *reinterpret_cast<uint4*>(patch + a) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+                            *reinterpret_cast<uint4*>(patch + (a ^ 64)) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
                         }
                     }
                 }
@@ -660,8 +667,12 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             }
         }
         if (!(DIAG & 2) && !AJIT) read_a(F0, 0);
+        // a wave whose fragments all lie in tile rows past the conv output
+        // (the bottom tile row of a tall tile) skips its MFMAs: those outputs
+        // are discarded by the epilogue
+        const bool wave_idle = oh0 + (wm * MF * 16) / TW >= Hout * POOL;
 #pragma unroll
-        for (int t = 0; t < ((DIAG & 2) ? 0 : NTAP); t += 2) {
+        for (int t = 0; t < ((DIAG & 2) || wave_idle ? 0 : NTAP); t += 2) {
             step(F0, F1, g, t);
             if (t + 1 < NTAP) step(F1, F0, g, t + 1);
         }

@@ -1,0 +1,241 @@
+// Runtime-shaped layers: the kernels behind any conv / pool / elementwise
+// shape the tuned tables of aa_cnn.hip do not cover, and behind the graph
+// (DAG) models of aa_graph.hip.  Included by both.
+//
+// gconv_x3: split-bf16 implicit GEMM on v_mfma_f32_16x16x32_bf16 for any
+// kernel size, stride and padding (explicit top/left; the output size sets
+// the bottom/right), C_in padded to 32 with zero weights, any C_out.  A
+// 256-thread block computes 64 output pixels x 64 output channels: per
+// K step (tap, 32 input channels) it gathers the 64 pixels' 32 channels
+// (zero outside the image), splits them into bf16 hi / lo in LDS next to the
+// step's pre-split weight slice, and each wave (2 x 2 over the tile) runs
+// 2 x 2 fragments x 3 MFMAs (hi*hi + lo*hi + hi*lo, f32 accumulation, as
+// conv_x3).  LDS rows are 96 B (32 bf16 + 16 B), which makes the 16-lane
+// ds_read_b128 fragment reads conflict-free.  Fused epilogue: bias,
+// activation, NHWC f32 store (4 channels per lane).
+//
+// gconv_f32: the same geometry in exact f32 FMA chains (VALU), for C_in < 16
+// and the f32 parity mode.
+#pragma once
+
+#include "aa_common.h"
+
+namespace aa {
+
+enum GAct { GACT_NONE = 0, GACT_RELU = 1, GACT_LEAKY = 2, GACT_SIGMOID = 3, GACT_SWISH = 4 };
+
+__device__ __forceinline__ float gact(float v, int act, float alpha) {
+    switch (act) {
+        case GACT_RELU: return fmaxf(v, 0.f);
+        case GACT_LEAKY: return v >= 0.f ? v : v * alpha;
+        case GACT_SIGMOID: return 1.f / (1.f + expf(-v));
+        case GACT_SWISH: return v * (1.f / (1.f + expf(-v)));
+        default: return v;
+    }
+}
+
+struct ConvGeom {
+    int Hin, Win, Cin;   // input (NHWC)
+    int Hout, Wout, Cout;
+    int kh, kw, sh, sw;  // kernel, strides
+    int pt, pl;          // top / left zero padding
+    int cin_pad;         // Cin rounded up to 32 (gconv_x3 weight packing)
+};
+
+typedef __attribute__((ext_vector_type(8))) __bf16 gbf16x8;
+typedef __attribute__((ext_vector_type(4))) float gf32x4;
+
+constexpr int GX_ROW = 48;  // bf16 per LDS row: 32 + 16 B of padding (96 B)
+
+// weights: [tap][cin_pad / 32][cout_pad][64] bf16, per row 32 hi then 32 lo
+__global__ __launch_bounds__(256) void gconv_x3(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
+                                                const float* __restrict__ bias, float* __restrict__ out,
+                                                ConvGeom g, int cout_pad, int act, float alpha) {
+    __shared__ __attribute__((aligned(16))) uint16_t Ah[64 * GX_ROW], Al[64 * GX_ROW];
+    __shared__ __attribute__((aligned(16))) uint16_t Bh[64 * GX_ROW], Bl[64 * GX_ROW];
+    const int n = blockIdx.z;
+    const int pix0 = blockIdx.x * 64, ch0 = blockIdx.y * 64;
+    const int HWo = g.Hout * g.Wout;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    // staging role: row r (pixel / channel of the tile), 8-element quad q
+    const int r = t >> 2, q = t & 3;
+    const int P = pix0 + r;
+    const bool pv = P < HWo;
+    const int oy = pv ? P / g.Wout : 0, ox = pv ? P - (P / g.Wout) * g.Wout : 0;
+    const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
+    const int ncc = g.cin_pad / 32;
+    gf32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
+    const bool vec = (g.Cin & 7) == 0;
+    for (int tap = 0; tap < g.kh * g.kw; ++tap) {
+        const int ky = tap / g.kw, kx = tap - (tap / g.kw) * g.kw;
+        const int iy = oy * g.sh - g.pt + ky, ix = ox * g.sw - g.pl + kx;
+        const bool inside = pv && iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
+        const float* px = img + ((size_t)(inside ? iy : 0) * g.Win + (inside ? ix : 0)) * g.Cin;
+        for (int cc = 0; cc < ncc; ++cc) {
+            const int c0 = cc * 32 + 8 * q;
+            float v[8];
+            if (inside && vec && c0 + 8 <= g.Cin) {
+                const float4 a = *reinterpret_cast<const float4*>(px + c0);
+                const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
+                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+                v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = (inside && c0 + e < g.Cin) ? px[c0 + e] : 0.f;
+            }
+            gbf16x8 h, l;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                h[e] = (__bf16)v[e];
+                l[e] = (__bf16)(v[e] - (float)h[e]);
+            }
+            const uint16_t* wrow = wpk + (((size_t)(tap * ncc + cc) * cout_pad) + ch0 + r) * 64;
+            const uint4 wh = *reinterpret_cast<const uint4*>(wrow + 8 * q);
+            const uint4 wl = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
+            __syncthreads();  // the previous step's fragments are read
+            *reinterpret_cast<gbf16x8*>(Ah + r * GX_ROW + 8 * q) = h;
+            *reinterpret_cast<gbf16x8*>(Al + r * GX_ROW + 8 * q) = l;
+            *reinterpret_cast<uint4*>(Bh + r * GX_ROW + 8 * q) = wh;
+            *reinterpret_cast<uint4*>(Bl + r * GX_ROW + 8 * q) = wl;
+            __syncthreads();
+            const int ko = 8 * (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int wr = (wn * 32 + i * 16 + (lane & 15)) * GX_ROW + ko;
+                const gbf16x8 w_h = *reinterpret_cast<const gbf16x8*>(Bh + wr);
+                const gbf16x8 w_l = *reinterpret_cast<const gbf16x8*>(Bl + wr);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int xr = (wm * 32 + j * 16 + (lane & 15)) * GX_ROW + ko;
+                    const gbf16x8 x_h = *reinterpret_cast<const gbf16x8*>(Ah + xr);
+                    const gbf16x8 x_l = *reinterpret_cast<const gbf16x8*>(Al + xr);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_h, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_l, x_h, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_l, acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+    // D[channel][pixel]: lane holds channels 4 (lane >> 4) .. + 3 of pixel lane & 15
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int Pj = pix0 + wm * 32 + j * 16 + (lane & 15);
+        if (Pj >= HWo) continue;
+        float* o = out + ((size_t)n * HWo + Pj) * g.Cout;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = ch0 + wn * 32 + i * 16 + 4 * (lane >> 4);
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gact(acc[i][j][e] + (c + e < g.Cout ? bias[c + e] : 0.f), act, alpha);
+            if (c + 4 <= g.Cout && (g.Cout & 3) == 0) {
+                *reinterpret_cast<float4*>(o + c) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+                for (int e = 0; e < 4 && c + e < g.Cout; ++e) o[c + e] = v[e];
+            }
+        }
+    }
+}
+
+// exact f32: one thread per (output pixel, 8 output channels); weights [Cout][kh][kw][Cin]
+__global__ __launch_bounds__(256) void gconv_f32(const float* __restrict__ in, const float* __restrict__ w,
+                                                 const float* __restrict__ bias, float* __restrict__ out, ConvGeom g,
+                                                 int act, float alpha) {
+    const int n = blockIdx.z;
+    const int P = blockIdx.x * 256 + threadIdx.x;
+    const int c0 = blockIdx.y * 8;
+    if (P >= g.Hout * g.Wout) return;
+    const int oy = P / g.Wout, ox = P - (P / g.Wout) * g.Wout;
+    const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = c0 + c < g.Cout ? bias[c0 + c] : 0.f;
+    for (int ky = 0; ky < g.kh; ++ky) {
+        const int iy = oy * g.sh - g.pt + ky;
+        if (iy < 0 || iy >= g.Hin) continue;
+        for (int kx = 0; kx < g.kw; ++kx) {
+            const int ix = ox * g.sw - g.pl + kx;
+            if (ix < 0 || ix >= g.Win) continue;
+            const float* px = img + ((size_t)iy * g.Win + ix) * g.Cin;
+            const size_t wt = (size_t)(ky * g.kw + kx) * g.Cin;
+            for (int ci = 0; ci < g.Cin; ++ci) {
+                const float x = px[ci];
+#pragma unroll
+                for (int c = 0; c < 8; ++c)
+                    if (c0 + c < g.Cout) acc[c] = fmaf(w[(size_t)(c0 + c) * g.kh * g.kw * g.Cin + wt + ci], x, acc[c]);
+            }
+        }
+    }
+    float* o = out + ((size_t)n * g.Hout * g.Wout + P) * g.Cout;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], act, alpha);
+}
+
+// max / average pooling with explicit padding (average over the taps inside
+// the image: TF's "same"-padded AvgPool excludes the padding); one thread per
+// (output pixel, channel)
+__global__ __launch_bounds__(256) void gpool2d(const float* __restrict__ in, float* __restrict__ out, int Hin, int Win,
+                                               int C, int Hout, int Wout, int kh, int kw, int sh, int sw, int pt,
+                                               int pl, int avg, int act, float alpha) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const int n = blockIdx.y;
+    if (i >= (size_t)Hout * Wout * C) return;
+    const int c = (int)(i % C);
+    const int P = (int)(i / C);
+    const int oy = P / Wout, ox = P - (P / Wout) * Wout;
+    const float* img = in + (size_t)n * Hin * Win * C;
+    float m = avg ? 0.f : -INFINITY;
+    int cnt = 0;
+    for (int ky = 0; ky < kh; ++ky) {
+        const int iy = oy * sh - pt + ky;
+        if (iy < 0 || iy >= Hin) continue;
+        for (int kx = 0; kx < kw; ++kx) {
+            const int ix = ox * sw - pl + kx;
+            if (ix < 0 || ix >= Win) continue;
+            const float v = img[((size_t)iy * Win + ix) * C + c];
+            m = avg ? m + v : fmaxf(m, v);
+            ++cnt;
+        }
+    }
+    if (avg) m = cnt ? m / (float)cnt : 0.f;
+    out[(size_t)n * Hout * Wout * C + i] = gact(m, act, alpha);
+}
+
+// host: split-bf16 weight packing for gconv_x3 from a compact f32 [tap][Cout][Cin]
+// image (BN already folded): [tap][cin_pad/32][cout_pad][32 hi | 32 lo]
+static inline uint16_t g_f2bf(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
+    u += 0x7fff + ((u >> 16) & 1);
+    return (uint16_t)(u >> 16);
+}
+static inline float g_bf2f(uint16_t b) {
+    const uint32_t u = (uint32_t)b << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+static inline std::vector<uint16_t> gconv_pack_x3(const std::vector<float>& w_tco, int ntap, int cout, int cin,
+                                                  int cout_pad, int cin_pad) {
+    const int ncc = cin_pad / 32;
+    std::vector<uint16_t> h((size_t)ntap * ncc * cout_pad * 64, 0);
+    for (int t = 0; t < ntap; ++t)
+        for (int o = 0; o < cout; ++o)
+            for (int c = 0; c < cin; ++c) {
+                const float w = w_tco[((size_t)t * cout + o) * cin + c];
+                const uint16_t hi = g_f2bf(w);
+                const size_t row = ((size_t)(t * ncc + c / 32) * cout_pad + o) * 64;
+                h[row + c % 32] = hi;
+                h[row + 32 + c % 32] = g_f2bf(w - g_bf2f(hi));
+            }
+    return h;
+}
+
+}  // namespace aa

@@ -82,6 +82,8 @@ def parse(argv=None):
                          "4: a corpus of 60 s WAV files through the whole analyse path (configs[3])")
     ap.add_argument("--clips", type=int, default=1000, help="--config 3: clips per rank")
     ap.add_argument("--files", type=int, default=32, help="--config 4: files per rank")
+    ap.add_argument("--batch", type=int, default=16,
+                    help="--config 4: recordings per device pass (aa_amd.batch); 0 = one file at a time")
     return ap.parse_args(argv)
 
 
@@ -445,6 +447,11 @@ def main_stream(args, world, rank, dev):
         print(json.dumps(out), flush=True)
 
 
+def _write_clip(path, seed):
+    from tools import synth
+    synth.write_wav(path, synth.clip(seed))
+
+
 def main_corpus(args, world, rank, dev):
     """configs[3]: a corpus of 60 s WAV files through the whole analyse path
     (aa_amd.corpus: decode, signal_noise, tracks, classify() with model1,
@@ -458,19 +465,21 @@ def main_corpus(args, world, rank, dev):
     root = Path(tempfile.mkdtemp(prefix="aa_bench4_"))
     model = make_model(root / "model1", "model1", seed=1)
     n = args.files
-    files = []
-    for i in range(n * world):  # every rank writes the whole (small) corpus into its own temp dir
-        p = root / f"clip{i:05d}.wav"
-        if i % world == rank or i == 0:
-            synth.write_wav(p, synth.clip(5000 + i))
-        files.append(p)
+    files = [root / f"clip{i:05d}.wav" for i in range(n * world)]
+    # every rank writes its own share (plus file 0 for the warm-up) into its own
+    # temp dir, on a pool of host processes
+    mine = [i for i in range(n * world) if i % world == rank or i == 0]
+    from concurrent.futures import ProcessPoolExecutor
+    import multiprocessing as mpc
+    with ProcessPoolExecutor(max_workers=min(16, len(mine)), mp_context=mpc.get_context("spawn")) as ex:
+        list(ex.map(_write_clip, [str(files[i]) for i in mine], [5000 + i for i in mine]))
     models = [str(model)]
-    corpus.run([files[0]], models, rank=0, world=1)  # warm-up: plans, kernels, model upload (untimed)
+    corpus.run([files[0]], models, rank=0, world=1, batch=args.batch)  # warm-up: plans, kernels, model upload
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    res = corpus.run(files, models, rank=rank, world=world, device=dev if world > 1 else None)
+    res = corpus.run(files, models, rank=rank, world=world, device=dev if world > 1 else None, batch=args.batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -486,8 +495,9 @@ def main_corpus(args, world, rank, dev):
            "scaling": "weak", "vs_baseline": None, "dtype": "bf16x3",
            "data": "synthetic 60 s 48 kHz int16 WAV files (noise+chirps, seeded), seeded random-init model1",
            "config": {"workload": "config4: corpus of 60 s WAV files through analyse.examine (decode, "
-                                  "signal_noise, tracks, classify, species JSON), one file per stream, "
-                                  "JSON all-gathered", "model": "model1", "global_batch": world,
+                                  "signal_noise, tracks, classify, species JSON), files sharded over ranks, K per device pass, "
+                                  "JSON all-gathered", "model": "model1", "global_batch": world * max(args.batch, 1),
+                      "files_per_device_pass": max(args.batch, 1),
                       "seq_len": 48000 * 60, "parallelism": f"dp{world}", "files_per_rank": n,
                       "documents_gathered": len(res), "tracks_classified": n_pred}}
     if rank == 0:

@@ -20,6 +20,8 @@
  *                MagTransform.call                  src/magtransformv2.py:19-21
  *   aa_track_mean  np.mean over models, windows     src/identify_tracks.py:547-551
  *   aa_span_nonzero  get_end                        src/identify_tracks.py:387-413
+ *   aa_pcm_s16_to_f32  load_recording's s16 -> f32  src/identify_tracks.py:49-62
+ *   aa_resample_poly   load_recording's resample     src/identify_tracks.py:49-62
  *   aa_sn_*      signal_noise                       src/identify_tracks.py:650-706
  *   aa_flac_*    load_recording's ffmpeg decode     src/identify_tracks.py:49-62
  *                  (FLAC; host memory, no GPU)
@@ -192,6 +194,21 @@ int aa_track_mean(const float* probs, int32_t n_models, int64_t model_stride, in
  * a constant mel block exactly when every sample its frames cover is zero. */
 int aa_span_nonzero(const float* pcm, int64_t n, const int64_t* spans, int32_t n_spans,
                     int32_t* flags, void* stream);
+
+/* Device PCM16 (interleaved, `channels` <= 8) -> mono f32, as load_recording
+ * delivers it (src/identify_tracks.py:49-62: ffmpeg s16, librosa buf_to_float
+ * x / 32768, channel mean): bit-identical to the host decode.  Lets a batch of
+ * recordings cross PCIe as int16. */
+int aa_pcm_s16_to_f32(const int16_t* in, int64_t n_frames, int32_t channels, float* out, void* stream);
+
+/* Rational polyphase resampling by L / M (load_recording's librosa.resample
+ * to 48 kHz, src/identify_tracks.py:49-62; libsoxr's HQ recipe restated, see
+ * aa_amd/resample.py): y[m] = sum_t bank[r][t] x[k0 - t] with q = m M + half,
+ * k0 = q / L, r = q % L; x is zero outside [0, n_in).  bank: device f32
+ * [L][taps] (bank[r][t] = h[r + t L] of the filter on the L-times upsampled
+ * grid, centre tap `half`). */
+int aa_resample_poly(const float* x, int64_t n_in, const float* bank, int32_t L, int32_t M, int32_t taps,
+                     int32_t half, float* y, int64_t n_out, void* stream);
 
 /* ---------------------------------------------------------------- signal detector */
 /* signal_noise (src/identify_tracks.py:650-706): |STFT| (n_fft 4096) of the
