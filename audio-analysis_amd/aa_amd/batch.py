@@ -101,15 +101,22 @@ def _wav_pcm16(buf: np.ndarray, size: int):
 
 class SlotPool:
     """Pinned host slots, each holding one file's bytes (one per recording in
-    flight: the prefetch depth plus the batch on the device)."""
+    flight: the prefetch depth plus the batches on the device)."""
 
     def __init__(self, n_slots: int, slot_bytes: int):
-        self.bytes = int(slot_bytes)
-        self.t = [torch.empty(self.bytes, dtype=torch.uint8, pin_memory=True) for _ in range(n_slots)]
-        self.np = [t.numpy() for t in self.t]
-        self.free = list(range(n_slots))
         import threading
+        self.bytes = int(slot_bytes)
+        self.t, self.np, self.free = [], [], []
         self._cv = threading.Condition()
+        self.grow(n_slots)
+
+    def grow(self, n_slots: int):
+        with self._cv:
+            while len(self.t) < n_slots:
+                self.t.append(torch.empty(self.bytes, dtype=torch.uint8, pin_memory=True))
+                self.np.append(self.t[-1].numpy())
+                self.free.append(len(self.t) - 1)
+                self._cv.notify()
 
     def get(self) -> int:
         with self._cv:
@@ -162,7 +169,7 @@ class _Laps:
         return t1
 
     def report(self):
-        return " ".join(f"{k}={1e3 * v:.1f}ms" for k, v in self.t.items())
+        return " ".join(f"{k}={1e3 * v:.1f}ms" if isinstance(v, float) else f"{k}={v}" for k, v in self.t.items())
 
 
 @dataclass
@@ -179,10 +186,55 @@ class _Rec:
     err: object = None
 
 
-class BatchAnalyser:
-    """examine() for many files of one rank, K per device pass."""
+class _Lane:
+    """One batch in flight: its own HIP stream and every device buffer a batch
+    touches (PCM, int16 staging, signal_noise workspace and result slots, the
+    front-end / model workspaces), so two host threads can each drive a batch:
+    while one waits on its readbacks the other runs its host steps, and the
+    device overlaps the two batches' kernels."""
 
-    def __init__(self, bird_models, analyse_tracks=False, device=None, precision=None, batch=16, workers=8):
+    def __init__(self, dev):
+        self.dev = dev
+        self.stream = torch.cuda.Stream(device=dev)
+        self.copy = torch.cuda.Stream(device=dev)
+        self.pcm = torch.empty(0, dtype=torch.float32, device=dev)
+        self.s16 = torch.empty(0, dtype=torch.int16, device=dev)
+        self.sn_ws = None
+        self.sn_buf = None
+        self.ws = {}  # classify_batch workspaces
+
+    def buffers(self, n_f32, n_s16):
+        if self.pcm.numel() < n_f32:
+            self.pcm = torch.empty(int(n_f32 * 1.25) + 1, dtype=torch.float32, device=self.dev)
+        if self.s16.numel() < n_s16:
+            self.s16 = torch.empty(int(n_s16 * 1.25) + 1, dtype=torch.int16, device=self.dev)
+        return self.pcm, self.s16
+
+
+SN_CAP = 4096   # components per recording kept in the batch slots
+_SN_LOCK = __import__("threading").Lock()
+SN_HEAD = 64    # component rows read back with the counts (more: a second copy)
+
+_POOLS = {}
+
+
+def slot_pool(n_slots, slot_bytes):
+    """Pinned slots persist across runs (allocating pinned memory is slow):
+    one grow-only pool per slot size class."""
+    size = -(-int(slot_bytes) // (1 << 20)) << 20
+    pool = _POOLS.get(size)
+    if pool is None:
+        pool = _POOLS[size] = SlotPool(0, size)
+    pool.grow(n_slots)
+    return pool
+
+
+class BatchAnalyser:
+    """examine() for many files of one rank, K per device pass, ``lanes``
+    batches in flight."""
+
+    def __init__(self, bird_models, analyse_tracks=False, device=None, precision=None, batch=16, workers=8,
+                 lanes=2):
         from .identify_tracks import _group_models
         from .pipeline import Classifier
         self.bird_models = bird_models
@@ -190,32 +242,21 @@ class BatchAnalyser:
         self.dev = torch.device(device or "cuda")
         self.K = int(batch)
         self.workers = int(workers)
+        self.n_lanes = max(1, int(lanes))
         self.groups = _group_models(bird_models) if bird_models is not None else None
         self.clf = Classifier.shared(precision=precision, device=self.dev)
-        self._pcm = torch.empty(0, dtype=torch.float32, device=self.dev)
-        self._s16 = torch.empty(0, dtype=torch.int16, device=self.dev)
-        self._copy = torch.cuda.Stream(device=self.dev)
-        self._sn_out = None
         self.timing = _Laps()
 
-    # ---- device buffers -------------------------------------------------
-    def _buffers(self, n_f32, n_s16):
-        if self._pcm.numel() < n_f32:
-            self._pcm = torch.empty(int(n_f32 * 1.25) + 1, dtype=torch.float32, device=self.dev)
-        if self._s16.numel() < n_s16:
-            self._s16 = torch.empty(int(n_s16 * 1.25) + 1, dtype=torch.int16, device=self.dev)
-        return self._pcm, self._s16
-
     # ---- one batch --------------------------------------------------------
-    def _upload(self, recs):
+    def _upload(self, lane, recs):
         """PCM of the batch into one device f32 buffer (recording r at r.off)."""
         total = sum(r.dec.n for r in recs)
         n16 = sum(r.dec.n * r.dec.channels for r in recs if r.dec.s16 is not None)
-        pcm, s16 = self._buffers(total, n16)
+        pcm, s16 = lane.buffers(total, n16)
         cur = torch.cuda.current_stream(self.dev)
-        self._copy.wait_stream(cur)  # the previous batch is done with both buffers
+        lane.copy.wait_stream(cur)  # the lane's previous batch is done with both buffers
         off = o16 = 0
-        with torch.cuda.stream(self._copy):
+        with torch.cuda.stream(lane.copy):
             for r in recs:
                 r.off = off
                 d = r.dec
@@ -226,9 +267,7 @@ class BatchAnalyser:
                 elif d.sr_in == SR:
                     pcm[off:off + d.n].copy_(torch.from_numpy(d.f32), non_blocking=False)
                 off += d.n
-        cur.wait_stream(self._copy)
-        done = torch.cuda.Event()
-        done.record(self._copy)
+        cur.wait_stream(lane.copy)
         L = _lib.lib()
         from .resample import resample_device
         for r in recs:
@@ -240,7 +279,7 @@ class BatchAnalyser:
                            "aa_pcm_s16_to_f32")
             elif d.s16 is None and d.sr_in != SR:  # librosa.resample to 48 kHz (aa_amd.resample)
                 resample_device(torch.from_numpy(d.f32).to(self.dev), d.sr_in, SR, out=d.dev)
-        return pcm[:total], done
+        return pcm[:total]
 
     def _get_end(self, pcm, recs):
         """get_end (src/identify_tracks.py:387-413) of every recording, one launch."""
@@ -267,51 +306,53 @@ class BatchAnalyser:
                 seen.add(k)
                 recs[k].length = starts[j] * 281 // recs[k].dec.sr
 
-    def _signal_noise(self, pcm, recs):
+    def _signal_noise(self, lane, pcm, recs):
         """signal_noise (src/identify_tracks.py:650-706) of every recording:
-        back-to-back aa_sn_run launches into per-recording result slots, one
-        readback."""
+        back-to-back aa_sn_run launches into per-recording slots
+        [1 + SN_CAP][6] int32 (row 0: count, status), one readback of every
+        slot's head."""
         from .identify_tracks import Signal
         from .signals import detector
         by_sr = {}
         for k, r in enumerate(recs):
             by_sr.setdefault(r.dec.sr, []).append(k)
-        cap = 4096
+        L = _lib.lib()
         for sr, ks in by_sr.items():
             det = detector(sr, 281, self.dev)
             nsig = [int(sr * recs[k].length) for k in ks]
-            ws = det._workspace(max(nsig))
-            if self._sn_out is None or self._sn_out.shape[0] < len(ks):
-                self._sn_out = torch.empty((len(ks), cap, 6), dtype=torch.int32, device=self.dev)
-                self._sn_n = torch.zeros((len(ks), 2), dtype=torch.int32, device=self.dev)
-            out, cnt = self._sn_out, self._sn_n
-            L = _lib.lib()
+            need = L.aa_sn_workspace_bytes(det._h, max(nsig))
+            if lane.sn_ws is None or lane.sn_ws.numel() < need:
+                lane.sn_ws = torch.empty(need, dtype=torch.uint8, device=self.dev)
+            if lane.sn_buf is None or lane.sn_buf.shape[0] < len(ks):
+                lane.sn_buf = torch.empty((len(ks), 1 + SN_CAP, 6), dtype=torch.int32, device=self.dev)
+            buf, ws = lane.sn_buf, lane.sn_ws
             for j, k in enumerate(ks):
                 r = recs[k]
                 _lib.check(L.aa_sn_run(det._h, _lib.dptr(pcm) + 4 * r.off if nsig[j] else 0, nsig[j], _lib.dptr(ws),
-                                       ws.numel(), _lib.dptr(out[j]), cap, _lib.dptr(cnt[j]), 0, _lib.stream_ptr()),
-                           "aa_sn_run")
-            n = cnt[:len(ks)].cpu().numpy()
-            top = int(min(cap, n[:, 0].max())) if len(ks) else 0
-            rows_all = out[:len(ks), :max(top, 1)].cpu().numpy()
+                                       ws.numel(), _lib.dptr(buf[j, 1:]), SN_CAP, _lib.dptr(buf[j, 0]), 0,
+                                       _lib.stream_ptr()), "aa_sn_run")
+            head = buf[:len(ks), :1 + SN_HEAD].cpu().numpy()
             for j, k in enumerate(ks):
-                c, status = int(n[j, 0]), int(n[j, 1])
+                c, status = int(head[j, 0, 0]), int(head[j, 0, 1])
                 if status & _lib.AA_SN_NONFINITE:
                     recs[k].err = ValueError("Audio buffer is not finite everywhere")  # librosa valid_audio
                     continue
-                if status & _lib.AA_SN_RUN_OVERFLOW or c > cap:
-                    # more components than the batch slots hold: this recording alone
+                if status & _lib.AA_SN_RUN_OVERFLOW or c > SN_CAP:
+                    # more components than a slot holds: this recording alone,
+                    # through the detector's own (shared) buffers
                     try:
-                        stats = det.components(pcm[recs[k].off:recs[k].off + nsig[j]])
+                        with _SN_LOCK:
+                            stats = det.components(pcm[recs[k].off:recs[k].off + nsig[j]])
                     except Exception as e:
                         recs[k].err = e
                         continue
                 else:
-                    rows = rows_all[j, :c].astype(np.int64)
+                    rows = head[j, 1:1 + c] if c <= SN_HEAD else buf[j, 1:1 + c].cpu().numpy()
+                    rows = rows.astype(np.int64)
                     stats = rows[np.lexsort((rows[:, 5], rows[:, 0]))][:, :5]
-                recs[k].signals = [Signal(*t) for t in det.to_tuples(stats)]
+                recs[k].signals = [Signal(*tu) for tu in det.to_tuples(stats)]
 
-    def _classify(self, pcm, recs):
+    def _classify(self, lane, pcm, recs):
         from .identify_tracks import MAX_FRQUENCY, Signal, get_tracks_from_signals
         from .pipeline import BatchRec
         todo = []
@@ -337,13 +378,8 @@ class BatchAnalyser:
             todo.append(r)
         if not todo:
             return
-        sr = todo[0].dec.sr
-        if any(r.dec.sr != sr for r in todo):  # (load_recording resamples everything to 48 kHz)
-            for r in todo:
-                self._classify(pcm, [r])
-            return
         brs = [BatchRec(n=r.dec.n, off=r.off, tracks=r.tracks, frames=r.dec.frames, seed=r.idx) for r in todo]
-        out = self.clf.classify_batch(pcm, sr, brs, self.groups)
+        out = self.clf.classify_batch(pcm, SR, brs, self.groups, ws=lane.ws)
         for r, o in zip(todo, out):
             if isinstance(o, BaseException):
                 r.err = o
@@ -365,7 +401,7 @@ class BatchAnalyser:
             out[r.idx] = doc
         return out
 
-    def process(self, items, pool=None):
+    def process(self, items, lane, pool=None):
         """items: [(file_idx, path, Decoded | Exception, sidecar meta)] -> {file_idx: document}."""
         t0 = time.time()
         recs, failed = [], []
@@ -374,18 +410,19 @@ class BatchAnalyser:
                 failed.append(_Rec(idx, str(path), None, meta, err=dec))
             else:
                 recs.append(_Rec(idx, str(path), dec, meta))
-        if recs and self.bird_models is not None:
+        if recs:
             try:
-                tm = self.timing
-                t = time.perf_counter()
-                pcm, _ = self._upload(recs)
-                t = tm.lap("upload", t)
-                self._get_end(pcm, recs)
-                t = tm.lap("get_end", t)
-                self._signal_noise(pcm, recs)
-                t = tm.lap("signal_noise", t)
-                self._classify(pcm, recs)
-                tm.lap("classify", t)
+                with torch.cuda.stream(lane.stream):
+                    tm = self.timing
+                    t = time.perf_counter()
+                    pcm = self._upload(lane, recs)
+                    t = tm.lap("upload", t)
+                    self._get_end(pcm, recs)
+                    t = tm.lap("get_end", t)
+                    self._signal_noise(lane, pcm, recs)
+                    t = tm.lap("signal_noise", t)
+                    self._classify(lane, pcm, recs)
+                    tm.lap("classify", t)
             finally:
                 # (the slots stay held until here: band-pass filtered tracks
                 # read a recording's host samples during classify)
@@ -394,10 +431,14 @@ class BatchAnalyser:
                         if r.dec.slot >= 0:
                             pool.put(r.dec.slot)
                             r.dec.slot = -1
-        return recs + failed, t0
+        t = time.perf_counter()
+        docs = self._finish(recs + failed, t0)
+        self.timing.lap("post", t)
+        return docs
 
     def run(self, jobs):
         """jobs: [(file_idx, path)] -> {file_idx: document} (the files of this rank)."""
+        import threading
         from .analyse import read_sidecar
         if not jobs:
             return {}
@@ -406,8 +447,10 @@ class BatchAnalyser:
             return {i: dict(species_result(None, read_sidecar(p), self.analyse_tracks, False),
                             processing_time_seconds=0.0) for i, p in sorted(jobs)}
         K = self.K
+        lanes = [_Lane(self.dev) for _ in range(min(self.n_lanes, -(-len(jobs) // K)))]
         slot_bytes = max(os.path.getsize(p) for _, p in jobs) + 4096
-        pool = SlotPool(min(len(jobs), 3 * K), slot_bytes)
+        # slots: every lane's batch plus two batches of prefetch
+        pool = slot_pool(min(len(jobs), (len(lanes) + 2) * K), slot_bytes)
 
         def load(job):
             idx, path = job
@@ -419,27 +462,49 @@ class BatchAnalyser:
                 logging.error("Could not load %s", path, exc_info=True)
                 return idx, path, Exception(f"Could not load {path}") if not isinstance(e, ValueError) else e, meta
 
-        results = {}
-        with ThreadPoolExecutor(max_workers=self.workers) as io, ThreadPoolExecutor(max_workers=1) as post:
-            futs = [io.submit(load, j) for j in jobs[:2 * K]]
-            nxt = 2 * K
-            pending = None
-            for b0 in range(0, len(jobs), K):
-                t = time.perf_counter()
-                items = [f.result() for f in futs[:K]]
-                self.timing.lap("wait_decode", t)
-                futs = futs[K:]
-                while len(futs) < 2 * K and nxt < len(jobs):
-                    futs.append(io.submit(load, jobs[nxt]))
-                    nxt += 1
-                recs, t0 = self.process(items, pool)
-                t = time.perf_counter()
-                if pending is not None:
-                    results.update(pending.result())
-                self.timing.lap("wait_post", t)
-                pending = post.submit(self._finish, recs, t0)
-            if pending is not None:
-                results.update(pending.result())
+        results, errors = {}, []
+        lock = threading.Lock()
+        batches = [jobs[b:b + K] for b in range(0, len(jobs), K)]
+        with ThreadPoolExecutor(max_workers=self.workers) as io:
+            futs = {}  # batch index -> its decode futures, submitted two batches ahead
+            state = {"next": 0, "submitted": 0}
+
+            def submit_upto(b):
+                while state["submitted"] < min(b, len(batches)):
+                    futs[state["submitted"]] = [io.submit(load, j) for j in batches[state["submitted"]]]
+                    state["submitted"] += 1
+
+            def worker(lane):
+                torch.cuda.set_device(self.dev)
+                try:
+                    while True:
+                        with lock:
+                            b = state["next"]
+                            if b >= len(batches):
+                                return
+                            state["next"] += 1
+                            submit_upto(b + 1 + len(lanes))
+                            fb = futs.pop(b)
+                        t = time.perf_counter()
+                        items = [f.result() for f in fb]
+                        self.timing.lap("wait_decode", t)
+                        docs = self.process(items, lane, pool)
+                        with lock:
+                            results.update(docs)
+                except BaseException as e:  # surfaces in the caller
+                    errors.append(e)
+
+            with lock:
+                submit_upto(len(lanes) + 1)
+            threads = [threading.Thread(target=worker, args=(ln,), daemon=True) for ln in lanes]
+            for th in threads:
+                th.start()
+            for th in threads:
+                th.join()
+        for ln in lanes:
+            ln.stream.synchronize()
+        if errors:
+            raise errors[0]
         if os.environ.get("AA_BATCH_PROFILE"):
-            logging.warning("batch phases over %d files: %s", len(jobs), self.timing.report())
+            logging.warning("batch phases over %d files (%d lanes): %s", len(jobs), len(lanes), self.timing.report())
         return dict(sorted(results.items()))

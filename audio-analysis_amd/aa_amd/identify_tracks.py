@@ -41,8 +41,19 @@ def segment_overlap(first, second):
         max(first[1], second[1]) - min(first[0], second[0]))
 
 
+_MEL = {}
+
+
 def mel_freq(f):
-    return 2595.0 * np.log10(1.0 + f / 700.0)
+    """2595 log10(1 + f / 700) (:712-713), memoised per frequency: the
+    detector's signals take their frequencies from the 2049 STFT bins, and
+    numpy's scalar arithmetic costs ~8 us a call -- the same value each time."""
+    m = _MEL.get(f)
+    if m is None:
+        m = 2595.0 * np.log10(1.0 + f / 700.0)
+        if len(_MEL) < (1 << 16):
+            _MEL[f] = m
+    return m
 
 
 # ---------------------------------------------------------------------------

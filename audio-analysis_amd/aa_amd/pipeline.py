@@ -18,6 +18,7 @@ from __future__ import annotations
 import dataclasses
 import logging
 import os
+import threading
 from pathlib import Path
 
 import numpy as np
@@ -65,19 +66,22 @@ class Classifier:
         self.device = torch.device(device or "cuda")
         self._models = {}
         self._fes = {}
+        self._lock = threading.RLock()
 
     def frontend(self, s: FeSettings) -> FrontEnd:
-        if s not in self._fes:
-            self._fes[s] = FrontEnd(s, self.device)
-        return self._fes[s]
+        with self._lock:
+            if s not in self._fes:
+                self._fes[s] = FrontEnd(s, self.device)
+            return self._fes[s]
 
     def model(self, path, meta, in_shape) -> Model:
         key = (str(Path(path).resolve()), tuple(in_shape))
-        if key not in self._models:
-            logging.info("Loading %s", str(path))
-            self._models[key] = Model(path, in_shape, precision=self.precision, device=self.device,
-                                      meta=meta)
-        return self._models[key]
+        with self._lock:
+            if key not in self._models:
+                logging.info("Loading %s", str(path))
+                self._models[key] = Model(path, in_shape, precision=self.precision, device=self.device,
+                                          meta=meta)
+            return self._models[key]
 
     def classify_tracks(self, frames, sr, tracks, groups, pcm=None):
         """One recording (classify()): the batch core below with one entry,
@@ -91,7 +95,7 @@ class Classifier:
             raise res
         return res
 
-    def classify_batch(self, pcm, sr, recs, groups, raise_errors=False):
+    def classify_batch(self, pcm, sr, recs, groups, raise_errors=False, ws=None):
         """The model-group loop of classify() (src/identify_tracks.py:444-571)
         for several recordings at once: every recording's windows in one
         front-end launch set, one forward per model, one track mean, one
@@ -102,7 +106,9 @@ class Classifier:
         Returns per recording the bird labels (a set), or the exception the
         single-recording path would have raised for it (non-finite audio);
         the results land on each recording's tracks.  ``raise_errors``: raise
-        a recording's exception instead (the single-recording path)."""
+        a recording's exception instead (the single-recording path).  ``ws``:
+        a dict of this caller's device workspaces (grown here), for callers
+        that run several batches concurrently on their own streams."""
         from .identify_tracks import DEFAULT_BIRDS
         dev = self.device
         R = len(recs)
@@ -127,11 +133,16 @@ class Classifier:
                 views, extras = [], []
                 extra_at = int(pcm.numel())
                 for i, r in enumerate(recs):
-                    if r.seed is not None:
-                        np.random.seed(r.seed)
                     try:
-                        v, spans = schedule(r.n, sr, r.tracks, s.segment_length, meta.get("segment_stride", 1.5),
-                                            s.fmin, s.fmax, meta.get("pad_short_tracks", False), return_spans=True)
+                        if r.seed is not None:
+                            with _RNG_LOCK:  # numpy's global RandomState: seed and draws together
+                                np.random.seed(r.seed)
+                                v, spans = schedule(r.n, sr, r.tracks, s.segment_length,
+                                                    meta.get("segment_stride", 1.5), s.fmin, s.fmax,
+                                                    meta.get("pad_short_tracks", False), return_spans=True)
+                        else:
+                            v, spans = schedule(r.n, sr, r.tracks, s.segment_length, meta.get("segment_stride", 1.5),
+                                                s.fmin, s.fmax, meta.get("pad_short_tracks", False), return_spans=True)
                         # band-pass filtered tracks (:152-162): their windows read a
                         # filtered copy appended after the batch's samples
                         ff, fb = meta.get("filter_freq", False), meta.get("filter_below", None)
@@ -153,7 +164,7 @@ class Classifier:
                 if flat:
                     rows = torch.from_numpy(pack_windows(flat, int(pcm.numel()), win_len=s.win_len)).to(dev)
                     status = torch.empty(len(flat), dtype=torch.int32, device=dev)
-                    logmel = fe.run(pcm, rows, status=status)
+                    logmel = fe.run(pcm, rows, status=status, workspace=_grow(ws, "fe", fe.workspace_bytes(len(flat)), dev))
                     st = status.cpu().numpy()
                     if st.any():  # librosa valid_audio, per recording
                         k = 0
@@ -175,13 +186,13 @@ class Classifier:
                 # channel is the same log-mel, so this is the first group's
                 # front end with three times the channels
                 fe3 = self.frontend(dataclasses.replace(fe.s, channels=fe.s.channels * 3))
-                group_mel = fe3.run(pcm, rows)
+                group_mel = fe3.run(pcm, rows, workspace=_grow(ws, "fe", fe3.workspace_bytes(int(rows.shape[0])), dev))
             probs = torch.empty((len(group), total, len(labels)), dtype=torch.float32, device=dev)
             for k, (path, m_meta) in enumerate(group):
                 m = self.model(path, m_meta, group_mel.shape[1:])
                 if m.n_labels != len(labels):
                     raise ValueError(f"{path}: {m.n_labels} outputs for {len(labels)} labels")
-                m.forward(group_mel, probs=probs[k])
+                m.forward(group_mel, probs=probs[k], workspace=_grow(ws, "model", m.workspace_bytes(total), dev))
             # one track mean over every recording's tracks that have windows
             flat_counts = np.asarray([c for rc in counts for c in rc], np.int64)
             begin = np.concatenate([[0], np.cumsum(flat_counts)[:-1]]).astype(np.int32)
@@ -198,6 +209,19 @@ class Classifier:
                 row += len(mine)
                 t0 += nt
         return [e if e is not None else set(bird_labels) for e in errs]
+
+
+_RNG_LOCK = threading.Lock()
+
+
+def _grow(ws, key, need, dev):
+    """A caller-owned workspace (None: the plan's own)."""
+    if ws is None:
+        return None
+    t = ws.get(key)
+    if t is None or t.numel() < need:
+        t = ws[key] = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
+    return t
 
 
 @dataclasses.dataclass
