@@ -66,6 +66,20 @@ class Layer(C.Structure):
     ]
 
 
+class Node(C.Structure):
+    _fields_ = [
+        ("op", C.c_int32), ("in0", C.c_int32), ("in1", C.c_int32), ("kh", C.c_int32), ("kw", C.c_int32),
+        ("sh", C.c_int32), ("sw", C.c_int32), ("pt", C.c_int32), ("pb", C.c_int32), ("pl", C.c_int32),
+        ("pr", C.c_int32), ("filters", C.c_int32), ("act", C.c_int32), ("alpha", C.c_float),
+        ("off", C.c_int64 * 2),
+    ]
+
+
+AA_G = {"conv": 1, "dwconv": 2, "maxpool": 3, "avgpool": 4, "gmaxpool": 5, "gavgpool": 6, "add": 7, "mul": 8,
+        "affine": 9, "dense": 10, "pow": 11}
+AA_GACT = {None: 0, "linear": 0, "relu": 1, "leaky": 2, "sigmoid": 3, "swish": 4}
+
+
 class SnConfig(C.Structure):
     _fields_ = [("sr", C.c_int32), ("n_fft", C.c_int32), ("hop_length", C.c_int32),
                 ("signal_width", C.c_double), ("freq_range", C.c_double)]
@@ -112,6 +126,16 @@ _SIGS = {
     "aa_model_set_input_f16": (C.c_int, [C.c_void_p, C.c_int32]),
     "aa_model_stage_time": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double),
                                       C.POINTER(C.c_int64)]),
+    "aa_graph_create": (C.c_int, [C.POINTER(Node), C.c_int32, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
+                                  C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "aa_graph_destroy": (C.c_int, [C.c_void_p]),
+    "aa_graph_n_outputs": (C.c_int, [C.c_void_p]),
+    "aa_graph_workspace_bytes": (C.c_size_t, [C.c_void_p, C.c_int32]),
+    "aa_graph_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_size_t, C.c_void_p]),
+    "aa_graph_n_stages": (C.c_int, [C.c_void_p]),
+    "aa_graph_stage_info": (C.c_int, [C.c_void_p, C.c_int32, C.c_char_p, C.c_int32, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_double)]),
     "aa_track_mean": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_void_p,
                                 C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "aa_span_nonzero": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p,

@@ -146,26 +146,42 @@ class Model(_lib.StageTiming):
         except Exception:
             logging.info("Could not load model", exc_info=True)  # :324-326
             raise
-        layers, blob = layer_table(arch, tensors)
         self.in_shape = tuple(int(v) for v in in_shape)  # (H, W, C)
         prec = {"f32": _lib.AA_PREC_F32, "bf16": _lib.AA_PREC_BF16, "fp8": _lib.AA_PREC_FP8,
                 "bf16x3": _lib.AA_PREC_BF16X3}[precision]
         h = C.c_void_p()
+        from .graph import graph_table, is_graph
+        self.graph = is_graph(arch)
         with torch.cuda.device(self.device):
-            _lib.check(_lib.lib().aa_model_create(layers, len(layers), blob.ctypes.data, blob.size,
-                                                  *self.in_shape, prec, C.byref(h)), "aa_model_create")
+            if self.graph:
+                # a Keras graph (residual / squeeze-excite / depthwise / strided
+                # "same" convs): the node executor (aa_graph_*), split-bf16 or f32
+                if prec not in (_lib.AA_PREC_BF16X3, _lib.AA_PREC_F32):
+                    logging.info("%s: graph models run in split-bf16 (precision %s not served)", model_path,
+                                 precision)
+                    prec = _lib.AA_PREC_BF16X3
+                nodes, blob, _ = graph_table(arch, tensors, self.in_shape)
+                _lib.check(_lib.lib().aa_graph_create(nodes, len(nodes), blob.ctypes.data, blob.size,
+                                                      *self.in_shape, prec, C.byref(h)), "aa_graph_create")
+                self._timing_prefix = "aa_graph"
+            else:
+                layers, blob = layer_table(arch, tensors)
+                _lib.check(_lib.lib().aa_model_create(layers, len(layers), blob.ctypes.data, blob.size,
+                                                      *self.in_shape, prec, C.byref(h)), "aa_model_create")
         self._h = h
-        self.n_labels = _lib.lib().aa_model_n_outputs(h)
+        self.n_labels = (_lib.lib().aa_graph_n_outputs if self.graph else _lib.lib().aa_model_n_outputs)(h)
         self._ws = None
         self._in_f16 = False
 
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and _lib._lib is not None:
-            _lib.lib().aa_model_destroy(h)
+            (_lib.lib().aa_graph_destroy if getattr(self, "graph", False) else _lib.lib().aa_model_destroy)(h)
             self._h = None
 
     def workspace_bytes(self, n: int) -> int:
+        if self.graph:
+            return int(_lib.lib().aa_graph_workspace_bytes(self._h, int(n)))
         return int(_lib.lib().aa_model_workspace_bytes(self._h, int(n)))
 
     def _workspace(self, n: int) -> torch.Tensor:
@@ -184,6 +200,9 @@ class Model(_lib.StageTiming):
         if x.dtype not in (torch.float32, torch.float16):
             raise ValueError(f"input dtype {x.dtype}: float32 or float16")
         f16 = x.dtype == torch.float16
+        if f16 and self.graph:
+            x = x.float()  # (graphs read f32)
+            f16 = False
         if f16 != self._in_f16:
             _lib.check(_lib.lib().aa_model_set_input_f16(self._h, int(f16)), "aa_model_set_input_f16")
             self._in_f16 = f16
@@ -194,9 +213,10 @@ class Model(_lib.StageTiming):
         if n == 0:
             return logits, probs
         ws = workspace if workspace is not None else self._workspace(n)
-        _lib.check(_lib.lib().aa_model_forward(
-            self._h, _lib.dptr(x), n, _lib.dptr(logits), _lib.dptr(probs), _lib.dptr(ws),
-            int(ws.numel()), _lib.stream_ptr(stream)), "aa_model_forward")
+        fwd = _lib.lib().aa_graph_forward if self.graph else _lib.lib().aa_model_forward
+        _lib.check(fwd(self._h, _lib.dptr(x), n, _lib.dptr(logits), _lib.dptr(probs), _lib.dptr(ws),
+                       int(ws.numel()), _lib.stream_ptr(stream)),
+                   "aa_graph_forward" if self.graph else "aa_model_forward")
         return logits, probs
 
     def predict(self, x: torch.Tensor) -> torch.Tensor:

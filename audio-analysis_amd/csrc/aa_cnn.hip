@@ -1083,6 +1083,7 @@ __global__ void track_mean(const float* __restrict__ probs, int n_models, long l
 
 #include "aa_conv_x3.h"
 #include "aa_conv_wg.h"
+#include "aa_gconv.h"
 
 namespace aa {
 
@@ -1092,8 +1093,10 @@ namespace aa {
 // ST_SMALL: C_in = 1 3x3 -> 32 first conv (VALU, fusable into the next
 // stage); ST_MFMA: tuned matrix-core conv; ST_HEAD: 1x1 conv + global max;
 // ST_GENERIC: any other conv shape / pool window (f32 VALU fallback);
-// ST_POOLDENSE: GlobalMaxPool2D [+ Dense] [+ sigmoid] after a conv stage
-enum StageKind { ST_SMALL = 0, ST_MFMA = 1, ST_HEAD = 2, ST_GENERIC = 3, ST_POOLDENSE = 4 };
+// ST_POOLDENSE: GlobalMaxPool2D [+ Dense] [+ sigmoid] after a conv stage;
+// ST_GCONV: split-bf16 mode, a conv with C_in >= 16 and no tuned tile: the
+// runtime-shaped MFMA kernel gconv_x3 (aa_gconv.h) [+ gpool2d for the max pool]
+enum StageKind { ST_SMALL = 0, ST_MFMA = 1, ST_HEAD = 2, ST_GENERIC = 3, ST_POOLDENSE = 4, ST_GCONV = 5 };
 
 struct Stage {
     int kind = ST_MFMA;
@@ -1117,6 +1120,7 @@ struct Stage {
     int in_split = 0;     // split-bf16: input / output in the grouped-split layout (aa_conv_x3.h)
     int out_split = 0;
     int wg = 0;           // split-bf16 Winograd F(2,3)-along-W kernel (aa_conv_wg.h) and its weight packing
+    int cin_pad = 0;      // ST_GCONV: C_in rounded up to 32
 };
 
 struct Model {
@@ -1125,6 +1129,7 @@ struct Model {
     int L = 0;
     std::vector<Stage> st;
     size_t act_elems[2] = {0, 0};  // per-window elements of the ping-pong buffers
+    size_t tmp_elems = 0;          // per-window f32 elements of an ST_GCONV stage's unpooled output
     StageTimer timer;  // HIP events around the stages in timer.mask
 };
 
@@ -1297,7 +1302,7 @@ static int launch_wg(const Stage& s, const void* in, void* out, int n, hipStream
 
 template <typename T>
 static int launch_stage(const Model& m, const Stage& s, const void* in, void* out, float* logits,
-                        float* probs, int n, hipStream_t st, const Stage* first) {
+                        float* probs, int n, hipStream_t st, const Stage* first, float* tmp) {
     using GT = typename Prec<T>::G;
     if (s.kind == ST_SMALL) {
         dim3 grid((s.Hc * s.Wc + 255) / 256, n);
@@ -1306,6 +1311,29 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
                            s.act, s.alpha);
         AA_LAUNCH_CHECK();
         return AA_OK;
+    }
+    if (s.kind == ST_GCONV) {
+        if constexpr (!is_split<T>()) {
+            set_error("%s: the runtime-shaped MFMA conv is split-bf16 only", s.name.c_str());
+            return AA_ERR_UNSUPPORTED;
+        } else {
+            const ConvGeom g{s.Hin, s.Win, s.cin, s.Hc, s.Wc, s.cout, s.kh, s.kw, 1, 1, 0, 0, s.cin_pad};
+            const bool pooled = s.ph > 1 || s.pw > 1;
+            float* conv_out = pooled ? tmp : static_cast<float*>(out);
+            const int gact_ = s.act == ACT_LEAKY ? GACT_LEAKY : s.act == ACT_RELU ? GACT_RELU : GACT_NONE;
+            hipLaunchKernelGGL(gconv_x3, dim3((s.Hc * s.Wc + 63) / 64, s.cout_pad / 64, n), dim3(256), 0, st,
+                               (const float*)in, (const uint16_t*)s.d_w, s.d_b, conv_out, g, s.cout_pad, gact_,
+                               s.alpha);
+            AA_LAUNCH_CHECK();
+            if (pooled) {  // max pool after the (monotonic) activation: the pool of the activated values
+                const size_t items = (size_t)s.Hout * s.Wout * s.cout;
+                hipLaunchKernelGGL(gpool2d, dim3((unsigned)((items + 255) / 256), n), dim3(256), 0, st, tmp,
+                                   (float*)out, s.Hc, s.Wc, s.cout, s.Hout, s.Wout, s.ph, s.pw, s.ph, s.pw, 0, 0, 0,
+                                   GACT_NONE, 0.f);
+                AA_LAUNCH_CHECK();
+            }
+            return AA_OK;
+        }
     }
     if (s.kind == ST_GENERIC) {
         if constexpr (is_fp8<T>()) {
@@ -1619,6 +1647,8 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             s.kind = ST_SMALL;
         } else if (!s.is_first && s.pool && mfma_bn(precision, s.kh, s.kw, s.cin, s.pool)) {
             s.kind = ST_MFMA;
+        } else if (precision == AA_PREC_BF16X3 && !s.is_first && s.cin >= 16) {
+            s.kind = ST_GCONV;  // any other shape with a real contraction: the runtime-shaped MFMA kernel
         } else {
             s.kind = ST_GENERIC;
             if (precision == AA_PREC_FP8) {
@@ -1636,6 +1666,34 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         }
         int bn_tile = 32;
         if (s.kind == ST_MFMA) bn_tile = mfma_bn(precision, s.kh, s.kw, s.cin, s.pool);
+        if (s.kind == ST_GCONV) {
+            // [tap][cin_pad / 32][cout_pad][32 hi | 32 lo], BN folded (aa_gconv.h)
+            s.cout_pad = (s.cout + 63) / 64 * 64;
+            s.cin_pad = (s.cin + 31) / 32 * 32;
+            const int ntap = s.kh * s.kw;
+            std::vector<float> w_tco((size_t)ntap * s.cout * s.cin);
+            for (int t = 0; t < ntap; ++t)
+                for (int o = 0; o < s.cout; ++o)
+                    for (int c = 0; c < s.cin; ++c)
+                        w_tco[((size_t)t * s.cout + o) * s.cin + c] =
+                            (float)(kern[((size_t)t * s.cin + c) * s.cout + o] * scale[o]);
+            const std::vector<uint16_t> h = gconv_pack_x3(w_tco, ntap, s.cout, s.cin, s.cout_pad, s.cin_pad);
+            std::vector<float> bias(s.cout_pad, 0.f);
+            for (int o = 0; o < s.cout; ++o) bias[o] = (float)shift[o];
+            if (!upload(s, h.data(), h.size() * 2, bias)) break;
+            s.flops = 2.0 * s.Hc * s.Wc * K * s.cout;
+            s.bytes = 4.0 * s.Hin * s.Win * s.cin + 4.0 * s.Hout * s.Wout * s.cout;
+            char nm[96], pl[24] = "";
+            if (s.ph > 1 || s.pw > 1) snprintf(pl, sizeof pl, s.ph == s.pw ? "_pool%d" : "_pool%dx%d", s.ph, s.pw);
+            snprintf(nm, sizeof nm, "conv_gx3_%dx%d_%d_%d%s", s.kh, s.kw, s.cin, s.cout, pl);
+            s.name = nm;
+            if (s.ph > 1 || s.pw > 1) m->tmp_elems = std::max(m->tmp_elems, (size_t)s.Hc * s.Wc * s.cout);
+            m->st.push_back(s);
+            H = s.Hout;
+            W = s.Wout;
+            C = s.cout;
+            continue;
+        }
         s.wg = precision == AA_PREC_BF16X3 && s.kind == ST_MFMA && wg_bn(s.kh, s.kw, s.cin, s.pool) > 0;
         const bool rowmajor = s.kind == ST_SMALL || s.kind == ST_GENERIC;  // f32 [cout][K]
         s.cout_pad = rowmajor ? s.cout : (s.cout + bn_tile - 1) / bn_tile * bn_tile;
@@ -1841,7 +1899,8 @@ extern "C" size_t aa_model_workspace_bytes(const void* model, int32_t max_batch)
     if (!model || max_batch < 0) return 0;
     const Model* m = static_cast<const Model*>(model);
     const size_t es = prec_bytes(m->prec);
-    return align_up(m->act_elems[0] * es * max_batch, 256) + align_up(m->act_elems[1] * es * max_batch, 256);
+    return align_up(m->act_elems[0] * es * max_batch, 256) + align_up(m->act_elems[1] * es * max_batch, 256) +
+           align_up(m->tmp_elems * 4 * max_batch, 256);
 }
 
 extern "C" int aa_model_set_input_f16(void* model, int32_t f16) {
@@ -1865,6 +1924,7 @@ extern "C" int aa_model_forward(void* model, const void* x, int32_t n, float* lo
     const size_t es = prec_bytes(m->prec);
     char* buf[2] = {static_cast<char*>(workspace),
                     static_cast<char*>(workspace) + align_up(m->act_elems[0] * es * n, 256)};
+    float* tmp = reinterpret_cast<float*>(buf[1] + align_up(m->act_elems[1] * es * n, 256));
     hipStream_t st = static_cast<hipStream_t>(stream);
     // launch grids carry the window index in blockIdx.z (at most 65,535):
     // larger batches run as consecutive chunks through the same workspace
@@ -1890,10 +1950,10 @@ extern "C" int aa_model_forward(void* model, const void* x, int32_t n, float* lo
         hipEvent_t e0;
         int rc = m->timer.begin((int)k, st, &e0);
         if (rc != AA_OK) return rc;
-        rc = m->prec == AA_PREC_BF16     ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st, first)
-             : m->prec == AA_PREC_FP8    ? launch_stage<fp8>(*m, s, in, out, logits, probs, n, st, first)
-             : m->prec == AA_PREC_BF16X3 ? launch_stage<bf16x3>(*m, s, in, out, logits, probs, n, st, first)
-                                         : launch_stage<float>(*m, s, in, out, logits, probs, n, st, first);
+        rc = m->prec == AA_PREC_BF16     ? launch_stage<bf16>(*m, s, in, out, logits, probs, n, st, first, tmp)
+             : m->prec == AA_PREC_FP8    ? launch_stage<fp8>(*m, s, in, out, logits, probs, n, st, first, tmp)
+             : m->prec == AA_PREC_BF16X3 ? launch_stage<bf16x3>(*m, s, in, out, logits, probs, n, st, first, tmp)
+                                         : launch_stage<float>(*m, s, in, out, logits, probs, n, st, first, tmp);
         if (rc != AA_OK) return rc;
         rc = m->timer.end((int)k, st, e0);
         if (rc != AA_OK) return rc;

@@ -48,7 +48,7 @@ typedef __attribute__((ext_vector_type(4))) float gf32x4;
 constexpr int GX_ROW = 48;  // bf16 per LDS row: 32 + 16 B of padding (96 B)
 
 // weights: [tap][cin_pad / 32][cout_pad][64] bf16, per row 32 hi then 32 lo
-__global__ __launch_bounds__(256) void gconv_x3(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
+static __global__ __launch_bounds__(256) void gconv_x3(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
                                                 const float* __restrict__ bias, float* __restrict__ out,
                                                 ConvGeom g, int cout_pad, int act, float alpha) {
     __shared__ __attribute__((aligned(16))) uint16_t Ah[64 * GX_ROW], Al[64 * GX_ROW];
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void gconv_x3(const float* __restrict__ in, co
 }
 
 // exact f32: one thread per (output pixel, 8 output channels); weights [Cout][kh][kw][Cin]
-__global__ __launch_bounds__(256) void gconv_f32(const float* __restrict__ in, const float* __restrict__ w,
+static __global__ __launch_bounds__(256) void gconv_f32(const float* __restrict__ in, const float* __restrict__ w,
                                                  const float* __restrict__ bias, float* __restrict__ out, ConvGeom g,
                                                  int act, float alpha) {
     const int n = blockIdx.z;
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void gconv_f32(const float* __restrict__ in, c
 // max / average pooling with explicit padding (average over the taps inside
 // the image: TF's "same"-padded AvgPool excludes the padding); one thread per
 // (output pixel, channel)
-__global__ __launch_bounds__(256) void gpool2d(const float* __restrict__ in, float* __restrict__ out, int Hin, int Win,
+static __global__ __launch_bounds__(256) void gpool2d(const float* __restrict__ in, float* __restrict__ out, int Hin, int Win,
                                                int C, int Hout, int Wout, int kh, int kw, int sh, int sw, int pt,
                                                int pl, int avg, int act, float alpha) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;

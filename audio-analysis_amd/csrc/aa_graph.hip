@@ -1,0 +1,517 @@
+// CNN graphs: Keras Functional models that are not one conv chain --
+// residual Add, squeeze-and-excite Multiply, DepthwiseConv2D, strided and
+// "same"-padded convs, global average pooling -- i.e. the layer set of the
+// EfficientNet route of classify() (reference src/identify_tracks.py:539-540;
+// the CLI's default models /models/*/audioModel.keras, src/analyse.py:414-418,
+// are whatever Keras graph the AI-Model release holds).
+//
+// Execution: the node list (include/aa.h aa_node, topological order) runs
+// node by node over a batch of windows, each node's output an NHWC f32
+// tensor in a workspace region reused once its last consumer has run
+// (first-fit over the freed intervals).  Kernels:
+//   conv (C_in >= 16, split-bf16)  gconv_x3 (aa_gconv.h, MFMA)
+//   conv (C_in < 16, or f32 mode)  gconv_f32 (exact f32 FMA chains)
+//   depthwise conv                 gdwconv (one lane per output element)
+//   max / avg pool, global pools   gpool2d / ggpool
+//   add, broadcast multiply        gbinary
+//   affine / activation / pow      gaffine / gpow
+//   dense                          gdense
+// every one with its activation fused.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "aa_common.h"
+#include "aa_gconv.h"
+
+namespace aa {
+
+__global__ __launch_bounds__(256) void gdwconv(const float* __restrict__ in, const float* __restrict__ w,
+                                               const float* __restrict__ bias, float* __restrict__ out, int Hin,
+                                               int Win, int C, int Hout, int Wout, int kh, int kw, int sh, int sw,
+                                               int pt, int pl, int act, float alpha) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const int n = blockIdx.y;
+    if (i >= (size_t)Hout * Wout * C) return;
+    const int c = (int)(i % C);
+    const int P = (int)(i / C);
+    const int oy = P / Wout, ox = P - (P / Wout) * Wout;
+    const float* img = in + (size_t)n * Hin * Win * C;
+    float acc = bias ? bias[c] : 0.f;
+    for (int ky = 0; ky < kh; ++ky) {
+        const int iy = oy * sh - pt + ky;
+        if (iy < 0 || iy >= Hin) continue;
+        for (int kx = 0; kx < kw; ++kx) {
+            const int ix = ox * sw - pl + kx;
+            if (ix < 0 || ix >= Win) continue;
+            acc = fmaf(w[(ky * kw + kx) * C + c], img[((size_t)iy * Win + ix) * C + c], acc);
+        }
+    }
+    out[(size_t)n * Hout * Wout * C + i] = gact(acc, act, alpha);
+}
+
+// global pool over H x W: one lane per (window, channel), sequential over pixels
+__global__ __launch_bounds__(256) void ggpool(const float* __restrict__ in, float* __restrict__ out, int HW, int C,
+                                              int avg, int act, float alpha) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    const int n = blockIdx.y;
+    if (c >= C) return;
+    const float* p = in + (size_t)n * HW * C + c;
+    float m = avg ? 0.f : -INFINITY;
+    for (int i = 0; i < HW; ++i) m = avg ? m + p[(size_t)i * C] : fmaxf(m, p[(size_t)i * C]);
+    if (avg) m = m / (float)HW;
+    out[(size_t)n * C + c] = gact(m, act, alpha);
+}
+
+// a (+|*) b; b_bcast: b is [n][C] broadcast over the pixels
+__global__ __launch_bounds__(256) void gbinary(const float* __restrict__ a, const float* __restrict__ b,
+                                               float* __restrict__ out, size_t per_win, int C, int mul,
+                                               int b_bcast, int act, float alpha) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const int n = blockIdx.y;
+    if (i >= per_win) return;
+    const size_t o = (size_t)n * per_win + i;
+    const float y = b_bcast ? b[(size_t)n * C + (int)(i % C)] : b[o];
+    out[o] = gact(mul ? a[o] * y : a[o] + y, act, alpha);
+}
+
+__global__ __launch_bounds__(256) void gaffine(const float* __restrict__ in, const float* __restrict__ scale,
+                                               const float* __restrict__ shift, float* __restrict__ out,
+                                               size_t total, int C, int act, float alpha) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;
+    const int c = (int)(i % C);
+    float v = in[i];
+    if (scale) v = fmaf(v, scale[c], shift ? shift[c] : 0.f);
+    else if (shift) v += shift[c];
+    out[i] = gact(v, act, alpha);
+}
+
+__global__ __launch_bounds__(256) void gpow(const float* __restrict__ in, float* __restrict__ out, size_t total,
+                                            float e) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < total) out[i] = powf(in[i], e);
+}
+
+// [n][K] x [K][Cout] + bias: one lane per (window, output)
+__global__ __launch_bounds__(256) void gdense(const float* __restrict__ in, const float* __restrict__ w,
+                                              const float* __restrict__ bias, float* __restrict__ out, int K,
+                                              int Cout, int act, float alpha) {
+    const int o = blockIdx.x * 256 + threadIdx.x;
+    const int n = blockIdx.y;
+    if (o >= Cout) return;
+    const float* x = in + (size_t)n * K;
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc = fmaf(x[k], w[(size_t)k * Cout + o], acc);
+    if (bias) acc += bias[o];
+    out[(size_t)n * Cout + o] = gact(acc, act, alpha);
+}
+
+__global__ __launch_bounds__(256) void gfinal(const float* __restrict__ x, float* __restrict__ logits,
+                                              float* __restrict__ probs, size_t total, int sigmoid) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;
+    const float v = x[i];
+    logits[i] = v;
+    if (probs) probs[i] = sigmoid ? 1.f / (1.f + expf(-v)) : v;
+}
+
+struct GNode {
+    aa_node d;
+    int H = 0, W = 0, C = 0;  // output shape
+    int mfma = 0;             // conv on gconv_x3
+    ConvGeom g{};
+    int cout_pad = 0;
+    void* d_w = nullptr;
+    float* d_b = nullptr;
+    float* d_b2 = nullptr;    // affine shift
+    size_t off = 0;           // workspace offset (f32 elements per window)
+    int last_use = 0;
+    std::string name;
+    double flops = 0, bytes = 0;
+};
+
+struct Graph {
+    int prec = AA_PREC_BF16X3;
+    int in_h = 0, in_w = 0, in_c = 0;
+    std::vector<GNode> nodes;
+    size_t per_win = 0;  // workspace f32 elements per window
+    int L = 0;
+    int sigmoid_out = 0;
+};
+
+static void free_graph(Graph* g) {
+    if (!g) return;
+    for (auto& nd : g->nodes) {
+        (void)hipFree(nd.d_w);
+        (void)hipFree(nd.d_b);
+        (void)hipFree(nd.d_b2);
+    }
+    delete g;
+}
+
+static int gupload(void** dst, const void* src, size_t bytes) {
+    if (!bytes) return AA_OK;
+    AA_HIP(hipMalloc(dst, bytes));
+    AA_HIP(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    return AA_OK;
+}
+
+static const char* gop_name(int op) {
+    switch (op) {
+        case AA_G_CONV: return "conv";
+        case AA_G_DWCONV: return "dwconv";
+        case AA_G_MAXPOOL: return "maxpool";
+        case AA_G_AVGPOOL: return "avgpool";
+        case AA_G_GMAXPOOL: return "gmaxpool";
+        case AA_G_GAVGPOOL: return "gavgpool";
+        case AA_G_ADD: return "add";
+        case AA_G_MUL: return "mul";
+        case AA_G_AFFINE: return "affine";
+        case AA_G_DENSE: return "dense";
+        case AA_G_POW: return "pow";
+        default: return "?";
+    }
+}
+
+static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float* blob, int64_t blob_len) {
+    auto get = [&](int64_t off, int64_t n) -> const float* {
+        if (off < 0 || n < 0 || off + n > blob_len) return nullptr;
+        return blob + off;
+    };
+    G->nodes.resize(n_nodes);
+    for (int i = 0; i < n_nodes; ++i) {
+        GNode& N = G->nodes[i];
+        N.d = nodes[i];
+        const aa_node& d = N.d;
+        AA_CHECK(d.in0 >= -1 && d.in0 < i && d.in1 >= -1 && d.in1 < i, AA_ERR_INVALID,
+                 "aa_graph_create: node %d reads a later node", i);
+        AA_CHECK(d.act >= AA_GACT_NONE && d.act <= AA_GACT_SWISH, AA_ERR_INVALID, "node %d: activation %d", i, d.act);
+        auto shape = [&](int k, int& H, int& W, int& C) {
+            if (k < 0) { H = G->in_h; W = G->in_w; C = G->in_c; }
+            else { H = G->nodes[k].H; W = G->nodes[k].W; C = G->nodes[k].C; }
+        };
+        int H, W, C;
+        shape(d.in0, H, W, C);
+        const bool windowed = d.op == AA_G_CONV || d.op == AA_G_DWCONV || d.op == AA_G_MAXPOOL || d.op == AA_G_AVGPOOL;
+        if (windowed) {
+            AA_CHECK(d.kh >= 1 && d.kw >= 1 && d.sh >= 1 && d.sw >= 1 && d.pt >= 0 && d.pb >= 0 && d.pl >= 0 &&
+                         d.pr >= 0, AA_ERR_INVALID, "node %d: window / strides / pads", i);
+            N.H = (H + d.pt + d.pb - d.kh) / d.sh + 1;
+            N.W = (W + d.pl + d.pr - d.kw) / d.sw + 1;
+            AA_CHECK(H + d.pt + d.pb >= d.kh && W + d.pl + d.pr >= d.kw, AA_ERR_INVALID,
+                     "node %d: input %dx%d smaller than the window", i, H, W);
+        }
+        char nm[96];
+        switch (d.op) {
+            case AA_G_CONV: {
+                AA_CHECK(d.filters >= 1, AA_ERR_INVALID, "node %d: filters", i);
+                N.C = d.filters;
+                const int K = d.kh * d.kw * C;
+                const float* k = get(d.off[0], (int64_t)K * d.filters);
+                AA_CHECK(k, AA_ERR_INVALID, "node %d: conv kernel outside the blob", i);
+                const float* b = d.off[1] >= 0 ? get(d.off[1], d.filters) : nullptr;
+                AA_CHECK(d.off[1] < 0 || b, AA_ERR_INVALID, "node %d: bias outside the blob", i);
+                N.g = ConvGeom{H, W, C, N.H, N.W, N.C, d.kh, d.kw, d.sh, d.sw, d.pt, d.pl, (C + 31) / 32 * 32};
+                N.mfma = G->prec == AA_PREC_BF16X3 && C >= 16;
+                const int ntap = d.kh * d.kw;
+                int rc;
+                if (N.mfma) {
+                    N.cout_pad = (N.C + 63) / 64 * 64;
+                    std::vector<float> w_tco((size_t)ntap * N.C * C);
+                    for (int t = 0; t < ntap; ++t)
+                        for (int o = 0; o < N.C; ++o)
+                            for (int c = 0; c < C; ++c) w_tco[((size_t)t * N.C + o) * C + c] = k[((size_t)t * C + c) * N.C + o];
+                    const std::vector<uint16_t> h = gconv_pack_x3(w_tco, ntap, N.C, C, N.cout_pad, N.g.cin_pad);
+                    if ((rc = gupload(&N.d_w, h.data(), h.size() * 2)) != AA_OK) return rc;
+                    std::vector<float> bias(N.cout_pad, 0.f);
+                    for (int o = 0; o < N.C; ++o) bias[o] = b ? b[o] : 0.f;
+                    if ((rc = gupload((void**)&N.d_b, bias.data(), bias.size() * 4)) != AA_OK) return rc;
+                } else {
+                    std::vector<float> w_ohwc((size_t)N.C * K);
+                    for (int o = 0; o < N.C; ++o)
+                        for (int kk = 0; kk < K; ++kk) w_ohwc[(size_t)o * K + kk] = k[(size_t)kk * N.C + o];
+                    if ((rc = gupload(&N.d_w, w_ohwc.data(), w_ohwc.size() * 4)) != AA_OK) return rc;
+                    std::vector<float> bias(N.C, 0.f);
+                    for (int o = 0; o < N.C; ++o) bias[o] = b ? b[o] : 0.f;
+                    if ((rc = gupload((void**)&N.d_b, bias.data(), bias.size() * 4)) != AA_OK) return rc;
+                }
+                N.flops = 2.0 * N.H * N.W * K * N.C;
+                N.bytes = 4.0 * (H * W * C + N.H * N.W * N.C);
+                snprintf(nm, sizeof nm, "%s_%dx%d_s%d_%d_%d", N.mfma ? "conv_gx3" : "conv_gf32", d.kh, d.kw, d.sh, C, N.C);
+                break;
+            }
+            case AA_G_DWCONV: {
+                N.C = C;
+                const float* k = get(d.off[0], (int64_t)d.kh * d.kw * C);
+                AA_CHECK(k, AA_ERR_INVALID, "node %d: depthwise kernel outside the blob", i);
+                const float* b = d.off[1] >= 0 ? get(d.off[1], C) : nullptr;
+                AA_CHECK(d.off[1] < 0 || b, AA_ERR_INVALID, "node %d: bias outside the blob", i);
+                int rc;
+                if ((rc = gupload(&N.d_w, k, (size_t)d.kh * d.kw * C * 4)) != AA_OK) return rc;
+                if (b && (rc = gupload((void**)&N.d_b, b, (size_t)C * 4)) != AA_OK) return rc;
+                N.flops = 2.0 * N.H * N.W * d.kh * d.kw * C;
+                N.bytes = 4.0 * (H * W * C + N.H * N.W * N.C);
+                snprintf(nm, sizeof nm, "dwconv_%dx%d_s%d_%d", d.kh, d.kw, d.sh, C);
+                break;
+            }
+            case AA_G_MAXPOOL:
+            case AA_G_AVGPOOL:
+                N.C = C;
+                N.bytes = 4.0 * (H * W * C + N.H * N.W * N.C);
+                snprintf(nm, sizeof nm, "%s_%dx%d_s%d_%d", gop_name(d.op), d.kh, d.kw, d.sh, C);
+                break;
+            case AA_G_GMAXPOOL:
+            case AA_G_GAVGPOOL:
+                N.H = N.W = 1;
+                N.C = C;
+                N.bytes = 4.0 * (H * W * C + C);
+                snprintf(nm, sizeof nm, "%s_%d", gop_name(d.op), C);
+                break;
+            case AA_G_ADD:
+            case AA_G_MUL: {
+                int H1, W1, C1;
+                shape(d.in1, H1, W1, C1);
+                const bool same = H1 == H && W1 == W && C1 == C;
+                const bool bc = d.op == AA_G_MUL && H1 == 1 && W1 == 1 && C1 == C;
+                AA_CHECK(same || bc, AA_ERR_UNSUPPORTED, "node %d: %s of %dx%dx%d and %dx%dx%d", i, gop_name(d.op), H,
+                         W, C, H1, W1, C1);
+                N.H = H; N.W = W; N.C = C;
+                N.bytes = 4.0 * (2 * H * W * C + H * W * C);
+                snprintf(nm, sizeof nm, "%s_%d", gop_name(d.op), C);
+                break;
+            }
+            case AA_G_AFFINE: {
+                N.H = H; N.W = W; N.C = C;
+                int rc;
+                if (d.off[0] >= 0) {
+                    const float* sc = get(d.off[0], C);
+                    AA_CHECK(sc, AA_ERR_INVALID, "node %d: scale outside the blob", i);
+                    if ((rc = gupload((void**)&N.d_b, sc, (size_t)C * 4)) != AA_OK) return rc;
+                }
+                if (d.off[1] >= 0) {
+                    const float* sh = get(d.off[1], C);
+                    AA_CHECK(sh, AA_ERR_INVALID, "node %d: shift outside the blob", i);
+                    if ((rc = gupload((void**)&N.d_b2, sh, (size_t)C * 4)) != AA_OK) return rc;
+                }
+                N.bytes = 8.0 * H * W * C;
+                snprintf(nm, sizeof nm, "affine_%d", C);
+                break;
+            }
+            case AA_G_POW:
+                N.H = H; N.W = W; N.C = C;
+                N.bytes = 8.0 * H * W * C;
+                snprintf(nm, sizeof nm, "pow_%d", C);
+                break;
+            case AA_G_DENSE: {
+                AA_CHECK(d.filters >= 1, AA_ERR_INVALID, "node %d: units", i);
+                const int K = H * W * C;
+                const float* k = get(d.off[0], (int64_t)K * d.filters);
+                AA_CHECK(k, AA_ERR_INVALID, "node %d: dense kernel outside the blob", i);
+                const float* b = d.off[1] >= 0 ? get(d.off[1], d.filters) : nullptr;
+                AA_CHECK(d.off[1] < 0 || b, AA_ERR_INVALID, "node %d: bias outside the blob", i);
+                int rc;
+                if ((rc = gupload(&N.d_w, k, (size_t)K * d.filters * 4)) != AA_OK) return rc;
+                if (b && (rc = gupload((void**)&N.d_b, b, (size_t)d.filters * 4)) != AA_OK) return rc;
+                N.H = N.W = 1;
+                N.C = d.filters;
+                N.flops = 2.0 * K * d.filters;
+                N.bytes = 4.0 * (K + (double)K * d.filters + d.filters);
+                snprintf(nm, sizeof nm, "dense_%d_%d", K, d.filters);
+                break;
+            }
+            default:
+                AA_CHECK(false, AA_ERR_UNSUPPORTED, "node %d: op %d", i, d.op);
+        }
+        AA_CHECK(N.H >= 1 && N.W >= 1 && N.C >= 1, AA_ERR_INVALID, "node %d: empty output", i);
+        N.name = nm;
+    }
+    // liveness: a node's buffer is free after its last consumer; first fit
+    const int last = n_nodes - 1;
+    for (int i = 0; i < n_nodes; ++i) G->nodes[i].last_use = i;
+    for (int i = 0; i < n_nodes; ++i) {
+        for (int k : {G->nodes[i].d.in0, G->nodes[i].d.in1})
+            if (k >= 0) G->nodes[k].last_use = std::max(G->nodes[k].last_use, i);
+    }
+    G->nodes[last].last_use = n_nodes;  // the output survives the forward
+    std::vector<std::pair<size_t, size_t>> live;  // [begin, end) of buffers in use
+    size_t peak = 0;
+    std::vector<std::vector<int>> frees(n_nodes + 1);
+    for (int i = 0; i < n_nodes; ++i) {
+        GNode& N = G->nodes[i];
+        const size_t sz = (size_t)N.H * N.W * N.C;
+        std::sort(live.begin(), live.end());
+        size_t at = 0;
+        for (auto& iv : live) {
+            if (iv.first >= at + sz) break;
+            at = std::max(at, iv.second);
+        }
+        N.off = at;
+        peak = std::max(peak, at + sz);
+        live.emplace_back(at, at + sz);
+        // release the inputs whose last use is this node
+        for (int k : {N.d.in0, N.d.in1}) {
+            if (k < 0 || G->nodes[k].last_use != i) continue;
+            auto it = std::find(live.begin(), live.end(),
+                                std::make_pair(G->nodes[k].off, G->nodes[k].off + (size_t)G->nodes[k].H * G->nodes[k].W * G->nodes[k].C));
+            if (it != live.end()) live.erase(it);
+        }
+        // a node nobody reads (a dangling branch) frees itself
+        if (N.last_use == i && i != last) {
+            auto it = std::find(live.begin(), live.end(), std::make_pair(at, at + sz));
+            if (it != live.end()) live.erase(it);
+        }
+    }
+    G->per_win = (peak + 63) / 64 * 64;
+    const GNode& O = G->nodes[last];
+    G->L = O.H * O.W * O.C;
+    G->sigmoid_out = O.d.act == AA_GACT_SIGMOID;
+    return AA_OK;
+}
+
+static int graph_run_node(const Graph& G, const GNode& N, const float* x, float* ws, int n, hipStream_t st) {
+    const aa_node& d = N.d;
+    auto buf = [&](int k) -> const float* {
+        return k < 0 ? x : ws + G.nodes[k].off * (size_t)n;
+    };
+    float* out = ws + N.off * (size_t)n;
+    const float* a = buf(d.in0);
+    int Hin, Win, Cin;
+    if (d.in0 < 0) { Hin = G.in_h; Win = G.in_w; Cin = G.in_c; }
+    else { Hin = G.nodes[d.in0].H; Win = G.nodes[d.in0].W; Cin = G.nodes[d.in0].C; }
+    // the output node's sigmoid is applied by gfinal (logits before it)
+    const bool last = &N == &G.nodes.back();
+    const int act = last && G.sigmoid_out ? AA_GACT_NONE : d.act;
+    const size_t per = (size_t)N.H * N.W * N.C;
+    switch (d.op) {
+        case AA_G_CONV:
+            if (N.mfma) {
+                hipLaunchKernelGGL(gconv_x3, dim3((N.H * N.W + 63) / 64, N.cout_pad / 64, n), dim3(256), 0, st, a,
+                                   (const uint16_t*)N.d_w, N.d_b, out, N.g, N.cout_pad, act, d.alpha);
+            } else {
+                hipLaunchKernelGGL(gconv_f32, dim3((N.H * N.W + 255) / 256, (N.C + 7) / 8, n), dim3(256), 0, st, a,
+                                   (const float*)N.d_w, N.d_b, out, N.g, act, d.alpha);
+            }
+            break;
+        case AA_G_DWCONV:
+            hipLaunchKernelGGL(gdwconv, dim3((unsigned)((per + 255) / 256), n), dim3(256), 0, st, a,
+                               (const float*)N.d_w, N.d_b, out, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw, d.pt,
+                               d.pl, act, d.alpha);
+            break;
+        case AA_G_MAXPOOL:
+        case AA_G_AVGPOOL:
+            hipLaunchKernelGGL(gpool2d, dim3((unsigned)((per + 255) / 256), n), dim3(256), 0, st, a, out, Hin, Win, Cin,
+                               N.H, N.W, d.kh, d.kw, d.sh, d.sw, d.pt, d.pl, d.op == AA_G_AVGPOOL ? 1 : 0, act,
+                               d.alpha);
+            break;
+        case AA_G_GMAXPOOL:
+        case AA_G_GAVGPOOL:
+            hipLaunchKernelGGL(ggpool, dim3((Cin + 255) / 256, n), dim3(256), 0, st, a, out, Hin * Win, Cin,
+                               d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
+            break;
+        case AA_G_ADD:
+        case AA_G_MUL: {
+            const GNode* B = d.in1 >= 0 ? &G.nodes[d.in1] : nullptr;
+            const int bc = B ? (B->H == 1 && B->W == 1 && (N.H != 1 || N.W != 1)) : 0;
+            hipLaunchKernelGGL(gbinary, dim3((unsigned)((per + 255) / 256), n), dim3(256), 0, st, a, buf(d.in1), out,
+                               per, N.C, d.op == AA_G_MUL ? 1 : 0, bc, act, d.alpha);
+            break;
+        }
+        case AA_G_AFFINE:
+            hipLaunchKernelGGL(gaffine, dim3((unsigned)((per * n + 255) / 256)), dim3(256), 0, st, a, N.d_b, N.d_b2,
+                               out, per * n, N.C, act, d.alpha);
+            break;
+        case AA_G_POW:
+            hipLaunchKernelGGL(gpow, dim3((unsigned)((per * n + 255) / 256)), dim3(256), 0, st, a, out, per * n,
+                               d.alpha);
+            break;
+        case AA_G_DENSE:
+            hipLaunchKernelGGL(gdense, dim3((N.C + 255) / 256, n), dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
+                               out, Hin * Win * Cin, N.C, act, d.alpha);
+            break;
+        default:
+            return AA_ERR_UNSUPPORTED;
+    }
+    AA_LAUNCH_CHECK();
+    return AA_OK;
+}
+
+}  // namespace aa
+
+using namespace aa;
+
+extern "C" int aa_graph_create(const aa_node* nodes, int32_t n_nodes, const float* blob, int64_t blob_len,
+                               int32_t in_h, int32_t in_w, int32_t in_c, int32_t precision, void** graph) {
+    AA_CHECK(nodes && blob && graph && n_nodes > 0, AA_ERR_INVALID, "aa_graph_create: null argument");
+    AA_CHECK(precision == AA_PREC_BF16X3 || precision == AA_PREC_F32, AA_ERR_UNSUPPORTED,
+             "aa_graph_create: graphs run in split-bf16 or f32 (precision %d)", precision);
+    AA_CHECK(in_h >= 1 && in_w >= 1 && in_c >= 1, AA_ERR_INVALID, "aa_graph_create: input shape");
+    Graph* G = new Graph();
+    G->prec = precision;
+    G->in_h = in_h;
+    G->in_w = in_w;
+    G->in_c = in_c;
+    const int rc = graph_build(G, nodes, n_nodes, blob, blob_len);
+    if (rc != AA_OK) {
+        free_graph(G);
+        return rc;
+    }
+    *graph = G;
+    return AA_OK;
+}
+
+extern "C" int aa_graph_destroy(void* graph) {
+    free_graph(static_cast<Graph*>(graph));
+    return AA_OK;
+}
+
+extern "C" int aa_graph_n_outputs(const void* graph) { return graph ? static_cast<const Graph*>(graph)->L : -1; }
+
+extern "C" size_t aa_graph_workspace_bytes(const void* graph, int32_t max_batch) {
+    if (!graph || max_batch < 0) return 0;
+    const Graph* G = static_cast<const Graph*>(graph);
+    return align_up(G->per_win * 4 * (size_t)std::min<int32_t>(max_batch, 32768), 256);
+}
+
+extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* logits, float* probs, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+    Graph* G = static_cast<Graph*>(graph);
+    AA_CHECK(G && x && logits, AA_ERR_INVALID, "aa_graph_forward: null argument");
+    if (n <= 0) return AA_OK;
+    constexpr int32_t CHUNK = 32768;  // grids carry the window in blockIdx.y / z
+    const int32_t nc0 = std::min(n, CHUNK);
+    AA_CHECK(workspace && workspace_bytes >= aa_graph_workspace_bytes(G, nc0), AA_ERR_WORKSPACE,
+             "aa_graph_forward: workspace %zu < %zu", workspace_bytes, aa_graph_workspace_bytes(G, nc0));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t in_per = (size_t)G->in_h * G->in_w * G->in_c;
+    for (int32_t c0 = 0; c0 < n; c0 += CHUNK) {
+        const int32_t nc = std::min(CHUNK, n - c0);
+        float* ws = static_cast<float*>(workspace);
+        for (const GNode& N : G->nodes) {
+            const int rc = graph_run_node(*G, N, x + (size_t)c0 * in_per, ws, nc, st);
+            if (rc != AA_OK) return rc;
+        }
+        const GNode& O = G->nodes.back();
+        const size_t total = (size_t)G->L * nc;
+        hipLaunchKernelGGL(gfinal, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ws + O.off * (size_t)nc,
+                           logits + (size_t)c0 * G->L, probs ? probs + (size_t)c0 * G->L : nullptr, total,
+                           G->sigmoid_out);
+        AA_LAUNCH_CHECK();
+    }
+    return AA_OK;
+}
+
+extern "C" int aa_graph_n_stages(const void* graph) {
+    return graph ? (int)static_cast<const Graph*>(graph)->nodes.size() : -1;
+}
+
+extern "C" int aa_graph_stage_info(const void* graph, int32_t stage, char* name, int32_t name_len,
+                                   double* flops_per_item, double* bytes_per_item) {
+    const Graph* G = static_cast<const Graph*>(graph);
+    AA_CHECK(G && stage >= 0 && stage < (int)G->nodes.size(), AA_ERR_INVALID, "aa_graph_stage_info: bad stage");
+    const GNode& N = G->nodes[stage];
+    if (name && name_len > 0) snprintf(name, name_len, "%s", N.name.c_str());
+    if (flops_per_item) *flops_per_item = N.flops;
+    if (bytes_per_item) *bytes_per_item = N.bytes;
+    return AA_OK;
+}

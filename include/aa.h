@@ -178,6 +178,64 @@ int aa_model_stage_info(const void* model, int32_t stage, char* name, int32_t na
 int aa_model_set_timing(void* model, uint32_t stage_mask);
 int aa_model_stage_time(void* model, int32_t stage, double* total_ms, int64_t* count);
 
+/* ---------------- CNN graphs (DAG models: residual / squeeze-excite / depthwise) ---------------- */
+/* Models that are not a single conv chain -- Keras Functional graphs such as
+ * the EfficientNet family classify() routes by name (src/identify_tracks.py:
+ * 539-540) -- as a node list in topological order.  Each node reads the
+ * outputs of in0 / in1 (node indices; -1 = the model input) and writes one
+ * NHWC f32 tensor per window.  The host folds BatchNormalization into a
+ * preceding conv, resolves "same" padding into explicit pads and folds
+ * ZeroPadding2D into the consumer's pads; activations are fused into their
+ * producer where it is the only consumer.  Convs with C_in >= 16 run on the
+ * runtime-shaped split-bf16 MFMA kernel (AA_PREC_BF16X3) or exact f32
+ * (AA_PREC_F32); the rest is f32 VALU. */
+typedef enum aa_gop {
+    AA_G_CONV = 1,      /* off[0] = kernel HWIO [kh][kw][cin][filters], off[1] = bias (or -1) */
+    AA_G_DWCONV = 2,    /* depthwise, depth multiplier 1: off[0] = kernel [kh][kw][C], off[1] = bias */
+    AA_G_MAXPOOL = 3,   /* window kh x kw, strides, pads */
+    AA_G_AVGPOOL = 4,   /* the average over the taps inside the image */
+    AA_G_GMAXPOOL = 5,  /* -> [1][1][C] */
+    AA_G_GAVGPOOL = 6,  /* -> [1][1][C] */
+    AA_G_ADD = 7,       /* in0 + in1 (same shape) */
+    AA_G_MUL = 8,       /* in0 * in1; in1 may be [1][1][C] (broadcast over H, W) */
+    AA_G_AFFINE = 9,    /* x * off[0][c] + off[1][c] (standalone BatchNormalization, Rescaling,
+                         * Normalization); off = -1: identity (activation only) */
+    AA_G_DENSE = 10,    /* [1][1][C] (or any H x W, flattened) -> [1][1][filters]:
+                         * off[0] = kernel [C][filters], off[1] = bias */
+    AA_G_POW = 11,      /* x ** alpha (MagTransform: alpha = sigmoid(a)) */
+} aa_gop;
+
+typedef enum aa_gact {
+    AA_GACT_NONE = 0, AA_GACT_RELU = 1, AA_GACT_LEAKY = 2, AA_GACT_SIGMOID = 3, AA_GACT_SWISH = 4
+} aa_gact;
+
+typedef struct aa_node {
+    int32_t op;                  /* aa_gop */
+    int32_t in0, in1;            /* producer nodes (-1: the model input; in1 unused: -1) */
+    int32_t kh, kw, sh, sw;      /* window / kernel, strides */
+    int32_t pt, pb, pl, pr;      /* explicit zero padding (top, bottom, left, right) */
+    int32_t filters;             /* conv / dense outputs */
+    int32_t act;                 /* aa_gact, applied last */
+    float alpha;                 /* leaky slope (AA_G_POW: the exponent) */
+    int64_t off[2];              /* weight blob offsets (floats), -1 when absent */
+} aa_node;
+
+/* The last node is the output [n][1][1][L] (or [n][H][W][L], flattened);
+ * logits are its values before a sigmoid activation (equal to probs
+ * otherwise). */
+int aa_graph_create(const aa_node* nodes, int32_t n_nodes, const float* blob, int64_t blob_len, int32_t in_h,
+                    int32_t in_w, int32_t in_c, int32_t precision, void** graph);
+int aa_graph_destroy(void* graph);
+int aa_graph_n_outputs(const void* graph);
+size_t aa_graph_workspace_bytes(const void* graph, int32_t max_batch);
+int aa_graph_forward(void* graph, const float* x, int32_t n, float* logits, float* probs, void* workspace,
+                     size_t workspace_bytes, void* stream);
+/* launches of one forward ("conv_gx3_*", "dwconv_*", ...), their algorithmic
+ * flops / bytes per window */
+int aa_graph_n_stages(const void* graph);
+int aa_graph_stage_info(const void* graph, int32_t stage, char* name, int32_t name_len, double* flops_per_item,
+                        double* bytes_per_item);
+
 /* ---------------- ensemble + window mean ---------------- */
 /* probs: device float32, model m / window w at probs[m * model_stride + w * n_labels].
  * Track t averages windows [win_begin[t], win_begin[t] + win_count[t]) after

@@ -39,6 +39,140 @@ def load_arch(path):
     return json.loads(meta["arch"]), load_file(str(path))
 
 
+_GRAPH_TYPES = {"depthwise_conv2d", "add", "multiply", "globalavgpool2d", "avgpool2d", "zeropad2d", "rescaling",
+                "normalization", "reshape", "flatten", "dropout"}
+
+
+def _is_graph(arch):
+    for ly in arch:
+        if "inputs" in ly or ly["type"] in _GRAPH_TYPES or ly.get("padding", "valid") != "valid":
+            return True
+        if ly["type"] == "conv2d" and (list(ly.get("strides", [1, 1])) != [1, 1] or
+                                       ly.get("activation") not in (None, "linear")):
+            return True
+        if ly["type"] == "maxpool2d" and list(ly.get("strides") or ly["pool"]) != list(ly["pool"]):
+            return True
+        if ly["type"] == "activation" and ly.get("fn") != "sigmoid":
+            return True
+    return False
+
+
+def _tf_same(n, k, s):
+    """TF "same" padding: (before, after), the odd pixel after."""
+    out = -(-n // s)
+    total = max((out - 1) * s + k - n, 0)
+    return total // 2, total - total // 2
+
+
+def _act(x, fn, alpha=0.2):
+    fn = None if fn is None else str(fn).lower()
+    if fn in (None, "linear"):
+        return x
+    if fn == "relu":
+        return F.relu(x)
+    if fn == "sigmoid":
+        return torch.sigmoid(x)
+    if fn in ("swish", "silu"):
+        return x * torch.sigmoid(x)
+    if fn in ("leaky_relu", "leaky"):
+        return F.leaky_relu(x, alpha)
+    raise ValueError(f"activation {fn}")
+
+
+@torch.no_grad()
+def _forward_graph(arch, tensors, x, dtype, capture=None):
+    """Keras Functional semantics, literally (NCHW torch, un-fused): each entry
+    reads the layers named in "inputs" (default: the previous entry; "input":
+    the model input).  logits: the last layer's input to a final sigmoid."""
+    t = lambda k: torch.from_numpy(np.asarray(tensors[k])).to(dtype)
+    outs = {"input": x}
+    prev = "input"
+    logits = None
+    for i, ly in enumerate(arch):
+        kind = ly["type"]
+        name = ly.get("name") or f"_l{i}"
+        ins = [outs[s] for s in (ly.get("inputs") or [prev])]
+        h = ins[0]
+        if kind in ("conv2d", "depthwise_conv2d", "maxpool2d", "avgpool2d"):
+            k = list(ly["kernel"] if kind != "maxpool2d" and kind != "avgpool2d" else ly["pool"])
+            s = list(ly.get("strides") or ([1, 1] if kind.endswith("conv2d") else k))
+            if ly.get("padding", "valid") == "same":
+                pt, pb = _tf_same(h.shape[2], k[0], s[0])
+                pl, pr = _tf_same(h.shape[3], k[1], s[1])
+            else:
+                pt = pb = pl = pr = 0
+            if kind == "conv2d":
+                w = t(name + ".kernel").reshape(k[0], k[1], h.shape[1], -1).permute(3, 2, 0, 1)
+                b = t(name + ".bias") if ly.get("use_bias", True) else None
+                y = F.conv2d(F.pad(h, (pl, pr, pt, pb)), w, b, stride=s)
+                y = _act(y, ly.get("activation"))
+            elif kind == "depthwise_conv2d":
+                C = h.shape[1]
+                w = t(name + ".kernel").reshape(k[0], k[1], C).permute(2, 0, 1)[:, None]
+                b = t(name + ".bias") if ly.get("use_bias", True) else None
+                y = F.conv2d(F.pad(h, (pl, pr, pt, pb)), w, b, stride=s, groups=C)
+                y = _act(y, ly.get("activation"))
+            elif kind == "maxpool2d":
+                y = F.max_pool2d(F.pad(h, (pl, pr, pt, pb), value=-float("inf")), k, s)
+            else:  # TF AvgPool: the mean over the taps inside the image
+                ones = torch.ones_like(h[:, :1])
+                num = F.avg_pool2d(F.pad(h, (pl, pr, pt, pb)), k, s, divisor_override=1)
+                den = F.avg_pool2d(F.pad(ones, (pl, pr, pt, pb)), k, s, divisor_override=1)
+                y = num / den
+        elif kind == "zeropad2d":
+            (a, b_), (l_, r_) = ly["pad"]
+            y = F.pad(h, (l_, r_, a, b_))
+        elif kind == "batchnorm":
+            g, be = t(name + ".gamma"), t(name + ".beta")
+            mu, var = t(name + ".moving_mean"), t(name + ".moving_variance")
+            y = (h - mu[None, :, None, None]) / torch.sqrt(var[None, :, None, None] + float(ly.get("eps", 1e-3)))
+            y = y * g[None, :, None, None] + be[None, :, None, None]
+        elif kind == "activation":
+            if ly["fn"] == "sigmoid" and i == len(arch) - 1:
+                logits = h
+            y = _act(h, ly["fn"])
+        elif kind == "relu":
+            y = F.relu(h)
+        elif kind == "leakyrelu":
+            y = F.leaky_relu(h, float(ly.get("alpha", 0.3)))
+        elif kind in ("globalavgpool2d", "globalmaxpool2d"):
+            y = (h.mean(dim=(2, 3)) if kind == "globalavgpool2d" else torch.amax(h, dim=(2, 3)))[:, :, None, None]
+        elif kind == "add":
+            y = ins[0] + ins[1]
+        elif kind == "multiply":
+            y = ins[0] * ins[1]
+        elif kind == "rescaling":
+            y = h * float(ly.get("scale", 1.0)) + float(ly.get("offset", 0.0))
+        elif kind == "normalization":
+            mean = t(name + ".mean").reshape(1, -1, 1, 1)
+            var = t(name + ".variance").reshape(1, -1, 1, 1)
+            y = (h - mean) / torch.clamp(torch.sqrt(var), min=1e-7)
+        elif kind in ("reshape", "flatten", "dropout"):
+            y = h
+        elif kind == "magtransform":
+            y = torch.pow(h, torch.sigmoid(t(name + ".a").reshape(-1)[0]))
+        elif kind == "dense":
+            flat = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)  # Keras Flatten of NHWC
+            y = flat @ t(name + ".kernel").reshape(flat.shape[1], -1)
+            if ly.get("use_bias", True):
+                y = y + t(name + ".bias")
+            if ly.get("activation") == "sigmoid" and i == len(arch) - 1:
+                logits = y
+            y = _act(y, ly.get("activation"))
+            y = y[:, :, None, None]
+        else:
+            raise ValueError(f"unknown layer type {kind}")
+        outs[name] = y
+        prev = name
+    if capture is not None:
+        capture.update(outs)
+    out = outs[prev].reshape(x.shape[0], -1) if outs[prev].dim() == 4 and outs[prev].shape[2:] == (1, 1) else \
+        outs[prev].permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+    lg = out if logits is None else (logits.reshape(x.shape[0], -1) if logits.dim() == 2 else
+                                     logits.permute(0, 2, 3, 1).reshape(x.shape[0], -1))
+    return lg.cpu().numpy(), out.cpu().numpy()
+
+
 @torch.no_grad()
 def forward(path_or_arch, x_nhwc: np.ndarray, dtype=torch.float32, tensors=None):
     """Run the CNN on ``x_nhwc`` [W, H, T, C]; returns (logits, probs) numpy."""
@@ -46,6 +180,9 @@ def forward(path_or_arch, x_nhwc: np.ndarray, dtype=torch.float32, tensors=None)
         arch, tensors = load_arch(path_or_arch)
     else:
         arch = path_or_arch
+    if _is_graph(arch):
+        x = torch.from_numpy(np.ascontiguousarray(x_nhwc)).to(dtype).permute(0, 3, 1, 2)
+        return _forward_graph(arch, tensors, x, dtype)
     t = lambda k: torch.from_numpy(np.asarray(tensors[k])).to(dtype)
     x = torch.from_numpy(np.ascontiguousarray(x_nhwc)).to(dtype).permute(0, 3, 1, 2)
     logits = None

@@ -192,3 +192,27 @@ def test_fp8_kernel_chains_match_emulation(gpu, tmp_path, chain):
           f"(max abs {d.max():.3e}, logit range {elg.min():.2f}..{elg.max():.2f})")
     assert np.isfinite(lg).all()
     assert exact >= 0.97 and rel.max() <= 0.135
+
+
+# ---- runtime-shaped MFMA conv (aa_gconv.h gconv_x3) ----
+GCONV_CHAIN = [(48, (3, 3), None), (96, (3, 3), (2, 2)), (64, (5, 3), None), (40, (3, 3), (3, 2))]
+
+
+@pytest.mark.parametrize("T", [226, 513])
+def test_untuned_shapes_run_on_mfma(gpu, tmp_path, T):
+    """Conv shapes outside the tuned tables (3x3/48->96 + 2x2 pool, 5x3/96->64,
+    3x3/64->40 + 3x2 pool) run on the runtime-shaped split-bf16 MFMA kernel
+    in the default precision, within the 1e-3 logit gate of the fp32 oracle."""
+    from aa_amd.model import Model
+    from tools.make_models import make_chain
+    path = make_chain(tmp_path / "gx", GCONV_CHAIN, seed=9, T=T)
+    x = calibration_input(4, 160, T, True, np.random.default_rng(4))
+    m = Model(path, x.shape[1:], precision="bf16x3")
+    names = [m.stage_info(i)[0] for i in range(m.n_stages())]
+    lg, _ = m.forward(torch.from_numpy(x).cuda())
+    lg = lg.cpu().numpy()
+    rlg, _ = cnn_oracle.forward(path, x)
+    err = np.abs(lg - rlg).max()
+    print(f"T={T} stages {names} max|dlogit| {err:.3e} (logit range {rlg.min():.2f}..{rlg.max():.2f})")
+    assert sum(n.startswith("conv_gx3_") for n in names) == 3, names
+    assert err <= LOGIT_TOL

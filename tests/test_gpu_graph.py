@@ -1,0 +1,52 @@
+"""Graph models on the GPU (aa_graph_*, csrc/aa_graph.hip): EfficientNet-like
+(depthwise conv, squeeze-excite, residual add, ZeroPadding2D + stride-2 valid
+conv, swish, global average pooling, Dense) and ResNet-like (Rescaling,
+Normalization, "same" stride-2 convs, max / average pools, residual add)
+networks against the fp32 oracle (oracle/cnn_oracle.py, Keras semantics),
+in split-bf16 (convs with C_in >= 16 on the runtime-shaped MFMA kernel) and
+exact f32; gate max |delta logit| <= 1e-3."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cnn_oracle
+from tools.make_models import calibration_input, make_graph
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-3
+
+
+@pytest.mark.parametrize("kind,ch,T", [("effnet", 1, 226), ("effnet", 3, 513), ("resnet", 3, 226)])
+@pytest.mark.parametrize("precision", ["bf16x3", "f32"])
+def test_graph_model_matches_oracle(gpu, tmp_path, kind, ch, T, precision):
+    from aa_amd.model import Model
+    p = make_graph(tmp_path / kind, kind, in_channels=ch, T=T, seed=3)
+    x = calibration_input(5, 160, T, True, np.random.default_rng(T))
+    if ch > 1:
+        x = np.repeat(x, ch, axis=3)
+    m = Model(p, x.shape[1:], precision=precision)
+    assert m.graph
+    names = [m.stage_info(i)[0] for i in range(m.n_stages())]
+    lg, pr = m.forward(torch.from_numpy(x).cuda())
+    lg, pr = lg.cpu().numpy(), pr.cpu().numpy()
+    rlg, rpr = cnn_oracle.forward(p, x)
+    err = np.abs(lg - rlg).max()
+    print(f"{kind} ch={ch} T={T} {precision}: max|dlogit| {err:.3e} (range {rlg.min():.2f}..{rlg.max():.2f}); "
+          f"stages {names}")
+    assert err <= LOGIT_TOL and np.abs(pr - rpr).max() <= LOGIT_TOL
+    if precision == "bf16x3":
+        assert any(n.startswith("conv_gx3_") for n in names)
+    if kind == "effnet":
+        assert sum(n.startswith("dwconv_") for n in names) == 3
+
+
+def test_graph_model_large_batch_is_batch_invariant(gpu, tmp_path):
+    from aa_amd.model import Model
+    p = make_graph(tmp_path / "e", "effnet", in_channels=1, T=226, seed=4)
+    x = calibration_input(40, 160, 226, True, np.random.default_rng(9))
+    m = Model(p, x.shape[1:])
+    xt = torch.from_numpy(x).cuda()
+    a = m.forward(xt)[0].cpu().numpy()
+    b = np.concatenate([m.forward(xt[i:i + 7])[0].cpu().numpy() for i in range(0, 40, 7)])
+    assert np.array_equal(a, b)

@@ -252,3 +252,165 @@ if __name__ == "__main__":
     root = sys.argv[1] if len(sys.argv) > 1 else "models"
     for p in make_ensemble(root):
         print(p)
+
+
+def graph_arch(kind="effnet", n_labels=len(LABELS)):
+    """Keras-Functional-style archs for the graph executor (aa_amd.graph):
+    "effnet": an EfficientNet-like stem + three MBConv blocks (depthwise conv,
+    squeeze-and-excite, residual add, ZeroPadding2D + valid stride-2 conv,
+    swish) + head, global average pooling, Dense + sigmoid;
+    "resnet": Rescaling + Normalization, "same" stride-2 convs, ReLU, max /
+    average pools, a residual add, GlobalAveragePooling2D, Dense."""
+    L = []
+
+    def add(d):
+        L.append(d)
+        return d["name"]
+
+    def bn(x, n):
+        return add({"type": "batchnorm", "name": n, "eps": 1e-3, "inputs": [x]})
+
+    def act(x, n, fn="swish"):
+        return add({"type": "activation", "name": n, "fn": fn, "inputs": [x]})
+
+    def conv(x, n, f, k, s=1, pad="same", bias=False, activation=None):
+        d = {"type": "conv2d", "name": n, "filters": f, "kernel": list(k), "strides": [s, s], "padding": pad,
+             "use_bias": bias, "inputs": [x]}
+        if activation:
+            d["activation"] = activation
+        return add(d)
+
+    def dw(x, n, k, s=1, pad="same"):
+        return add({"type": "depthwise_conv2d", "name": n, "kernel": [k, k], "strides": [s, s], "padding": pad,
+                    "use_bias": False, "inputs": [x]})
+
+    def se(x, n, c, r):
+        g = add({"type": "globalavgpool2d", "name": n + "_squeeze", "inputs": [x]})
+        g = add({"type": "reshape", "name": n + "_reshape", "target": [1, 1, c], "inputs": [g]})
+        g = conv(g, n + "_reduce", r, (1, 1), bias=True, activation="swish")
+        g = conv(g, n + "_expand", c, (1, 1), bias=True, activation="sigmoid")
+        return add({"type": "multiply", "name": n + "_excite", "inputs": [x, g]})
+
+    if kind == "effnet":
+        x = conv("input", "stem_conv", 32, (3, 3), s=2)
+        x = act(bn(x, "stem_bn"), "stem_act")
+        # block 1: depthwise 3x3, SE, project (no expansion)
+        y = act(bn(dw(x, "b1_dw", 3), "b1_bn"), "b1_act")
+        y = se(y, "b1_se", 32, 8)
+        y = bn(conv(y, "b1_project", 16, (1, 1)), "b1_project_bn")
+        y = add({"type": "maxpool2d", "name": "b1_pool", "pool": [3, 3], "strides": [1, 1], "padding": "same",
+                 "inputs": [y]})
+        # block 2: expand x4, ZeroPadding2D + valid 5x5 stride 2 (keras correct_pad), SE, project
+        z = act(bn(conv(y, "b2_expand", 64, (1, 1)), "b2_expand_bn"), "b2_expand_act")
+        z = add({"type": "zeropad2d", "name": "b2_pad", "pad": [[1, 2], [1, 2]], "inputs": [z]})
+        z = act(bn(dw(z, "b2_dw", 5, s=2, pad="valid"), "b2_bn"), "b2_act")
+        z = se(z, "b2_se", 64, 4)
+        z = bn(conv(z, "b2_project", 24, (1, 1)), "b2_project_bn")
+        # block 3: expand x4, depthwise 3x3, SE, project, dropout, residual add
+        u = act(bn(conv(z, "b3_expand", 96, (1, 1)), "b3_expand_bn"), "b3_expand_act")
+        u = act(bn(dw(u, "b3_dw", 3), "b3_bn"), "b3_act")
+        u = se(u, "b3_se", 96, 6)
+        u = bn(conv(u, "b3_project", 24, (1, 1)), "b3_project_bn")
+        u = add({"type": "dropout", "name": "b3_drop", "inputs": [u]})
+        u = add({"type": "add", "name": "b3_add", "inputs": [u, z]})
+        h = act(bn(conv(u, "top_conv", 64, (1, 1)), "top_bn"), "top_act")
+        h = add({"type": "globalavgpool2d", "name": "avg_pool", "inputs": [h]})
+        h = add({"type": "dropout", "name": "top_dropout", "inputs": [h]})
+        add({"type": "dense", "name": "predictions", "units": n_labels, "use_bias": True, "activation": "sigmoid",
+             "inputs": [h]})
+    elif kind == "resnet":
+        x = add({"type": "rescaling", "name": "rescale", "scale": 1.0 / 80.0, "offset": 1.0, "inputs": ["input"]})
+        x = add({"type": "normalization", "name": "norm", "inputs": [x]})
+        x = conv(x, "conv1", 24, (5, 5), s=2, bias=True)
+        x = add({"type": "relu", "name": "relu1", "inputs": [bn(x, "bn1")]})
+        x = add({"type": "maxpool2d", "name": "pool1", "pool": [3, 3], "strides": [2, 2], "padding": "same",
+                 "inputs": [x]})
+        y = conv(x, "conv2a", 24, (3, 3), bias=False)
+        y = add({"type": "relu", "name": "relu2a", "inputs": [bn(y, "bn2a")]})
+        y = bn(conv(y, "conv2b", 24, (3, 3)), "bn2b")
+        y = add({"type": "add", "name": "res2", "inputs": [x, y]})
+        y = add({"type": "relu", "name": "relu2", "inputs": [y]})
+        y = add({"type": "avgpool2d", "name": "pool2", "pool": [3, 3], "strides": [2, 2], "padding": "same",
+                 "inputs": [y]})
+        y = conv(y, "conv3", 48, (3, 1), s=2, bias=True, activation="relu")
+        y = add({"type": "globalavgpool2d", "name": "gap", "inputs": [y]})
+        add({"type": "dense", "name": "fc", "units": n_labels, "use_bias": True, "inputs": [y]})
+        add({"type": "activation", "name": "out", "fn": "sigmoid", "inputs": ["fc"]})
+    else:
+        raise ValueError(kind)
+    return L
+
+
+def _graph_weights(arch, in_ch, rng):
+    shapes = {"input": in_ch}
+    tensors = {}
+    for ly in arch:
+        src = (ly.get("inputs") or ["input"])[0]
+        c = shapes[src]
+        n, kind = ly["name"], ly["type"]
+        if kind == "conv2d":
+            kh, kw = ly["kernel"]
+            f = ly["filters"]
+            tensors[n + ".kernel"] = (rng.standard_normal((kh, kw, c, f)) * np.sqrt(2.0 / (kh * kw * c))).astype(np.float32)
+            if ly.get("use_bias"):
+                tensors[n + ".bias"] = (rng.standard_normal(f) * 0.1).astype(np.float32)
+            c = f
+        elif kind == "depthwise_conv2d":
+            kh, kw = ly["kernel"]
+            tensors[n + ".kernel"] = (rng.standard_normal((kh, kw, c, 1)) * np.sqrt(2.0 / (kh * kw))).astype(np.float32)
+        elif kind == "batchnorm":
+            tensors[n + ".gamma"] = rng.uniform(0.7, 1.3, c).astype(np.float32)
+            tensors[n + ".beta"] = rng.normal(0.0, 0.2, c).astype(np.float32)
+            tensors[n + ".moving_mean"] = np.zeros(c, np.float32)
+            tensors[n + ".moving_variance"] = np.ones(c, np.float32)
+        elif kind == "normalization":
+            tensors[n + ".mean"] = np.full(c, 0.45, np.float32)
+            tensors[n + ".variance"] = np.full(c, 0.04, np.float32)
+        elif kind == "dense":
+            tensors[n + ".kernel"] = (rng.standard_normal((c, ly["units"])) * np.sqrt(1.0 / c)).astype(np.float32)
+            tensors[n + ".bias"] = np.zeros(ly["units"], np.float32)
+            c = ly["units"]
+        shapes[n] = c
+    return tensors
+
+
+def make_graph(out_dir, kind="effnet", name=None, seed=1, in_channels=1, n_mels=160, T=226, labels=None,
+               meta_overrides=None):
+    """A graph model (graph_arch) with seeded weights, BatchNormalization
+    statistics calibrated layer by layer on dB-like inputs (float64, through
+    the oracle's graph semantics) and centred logits; writes
+    audioModel.safetensors + metadata.txt like make_model."""
+    import torch
+    from safetensors.numpy import save_file
+    from oracle.cnn_oracle import _forward_graph
+    labels = list(labels or LABELS)
+    arch = graph_arch(kind, len(labels))
+    rng = np.random.default_rng(seed)
+    tensors = _graph_weights(arch, in_channels, rng)
+    x = calibration_input(6, n_mels, T, True, rng)
+    if in_channels > 1:
+        x = np.repeat(x, in_channels, axis=3)
+    xt = torch.from_numpy(x).double().permute(0, 3, 1, 2)
+    for i, ly in enumerate(arch):
+        if ly["type"] != "batchnorm":
+            continue
+        outs = {}
+        _forward_graph(arch[:i], tensors, xt, torch.float64, capture=outs)
+        h = outs[ly["inputs"][0]]
+        tensors[ly["name"] + ".moving_mean"] = h.mean(dim=(0, 2, 3)).float().numpy()
+        tensors[ly["name"] + ".moving_variance"] = h.var(dim=(0, 2, 3), unbiased=False).float().numpy()
+    dense = [ly for ly in arch if ly["type"] == "dense"][-1]["name"]
+    lg, _ = _forward_graph(arch, tensors, xt, torch.float64)
+    shift = lg.mean(axis=0) - rng.normal(-0.8, 1.2, lg.shape[1])
+    tensors[dense + ".bias"] = (tensors[dense + ".bias"] - shift).astype(np.float32)
+    out = Path(out_dir)
+    out.mkdir(parents=True, exist_ok=True)
+    save_file({k: np.ascontiguousarray(v) for k, v in tensors.items()},
+              str(out / "audioModel.safetensors"), metadata={"arch": json.dumps(arch)})
+    meta = dict(DEFAULT_META)
+    meta.update({"name": name or f"{kind}-graph", "labels": labels,
+                 "ebird_ids": [EBIRD.get(l, []) for l in labels], "channels": in_channels})
+    meta.update(meta_overrides or {})
+    with open(out / "metadata.txt", "w") as f:
+        json.dump(meta, f, indent=2)
+    return out / "audioModel.safetensors"
