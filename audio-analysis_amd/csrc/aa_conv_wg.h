@@ -37,7 +37,7 @@ __host__ __device__ constexpr size_t wg_patch_bytes() {
 template <int KH, int BN, int TH, int TW>
 constexpr size_t wg_lds_bytes() {
     const size_t main = wg_patch_bytes<KH, TH, TW>();
-    const size_t epi = (size_t)TH * TW * (BN + 4) * 4;
+    const size_t epi = (size_t)TH * TW * BN * 4;
     return main > epi ? main : epi;
 }
 
@@ -199,12 +199,12 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     }
     __syncthreads();  // planes no longer needed: the f32 tile reuses LDS
 
-    // ---- epilogue: output transform into the f32 tile [TH*TW][BN+4] ----
-    constexpr int ESTR = BN + 4;
+    // ---- epilogue: output transform into the f32 tile (x3_store's swizzled
+    // layout, PSH = 1: a store's 8 lanes hold every other pixel) ----
     float* E = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
-        const int c0 = wn * NF * 16 + j * 16 + 4 * q;
+        const int u = wn * NF * 4 + j * 4 + q;
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             const int p = (wm * MF + i) * 16 + (lane & 15);
@@ -212,15 +212,15 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 const int r = p / NP, jp = p - (p / NP) * NP;
                 const f32x4 y0 = acc[0][i][j] + acc[1][i][j] + acc[2][i][j];
                 const f32x4 y1 = acc[1][i][j] - acc[2][i][j] - acc[3][i][j];
-                float* e0 = E + (r * TW + 2 * jp) * ESTR + c0;
-                *reinterpret_cast<float4*>(e0) = make_float4(y0[0], y0[1], y0[2], y0[3]);
-                *reinterpret_cast<float4*>(e0 + ESTR) = make_float4(y1[0], y1[1], y1[2], y1[3]);
+                const int px = r * TW + 2 * jp;
+                *reinterpret_cast<float4*>(E + x3_eoff<BN, 1>(px, u)) = make_float4(y0[0], y0[1], y0[2], y0[3]);
+                *reinterpret_cast<float4*>(E + x3_eoff<BN, 1>(px + 1, u)) = make_float4(y1[0], y1[1], y1[2], y1[3]);
             }
         }
     }
     __syncthreads();
-    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, false>(E, bias, out, n, cb, oh0, ow0, Hout, Wout, cout_store, act,
-                                                      alpha);
+    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, false, 1>(E, bias, out, n, cb, oh0, ow0, Hout, Wout, cout_store, act,
+                                                         alpha);
 }
 
 }  // namespace aa

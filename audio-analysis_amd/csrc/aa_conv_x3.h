@@ -75,7 +75,7 @@ __host__ __device__ constexpr size_t x3_patch_bytes() {
 template <int KH, int KW, int BN, int TH, int TW, bool FUSED>
 constexpr size_t x3_lds_bytes_nb(int nb) {  // nb = 0: no LDS ring (B fragments from global)
     const size_t main = x3_patch_bytes<KH, KW, TH, TW, FUSED>() + (size_t)nb * BN * 128;
-    const size_t epi = (size_t)TH * TW * (BN + 4) * 4;
+    const size_t epi = (size_t)TH * TW * BN * 4;
     return main > epi ? main : epi;
 }
 
@@ -175,65 +175,89 @@ __device__ __forceinline__ bf16x8 x3_wload(__amdgpu_buffer_rsrc_t rs, int voff, 
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
 }
 
-// Epilogue shared by the split-bf16 kernels: the f32 tile E [TH*TW][BN+4]
-// (bias not yet added) -> POOL x POOL max, bias, activation, and the NHWC
-// store (f32, or the grouped-split layout when OUT_SPLIT).  One thread per
-// (pooled pixel, 8-channel group).
-template <int TH, int TW, int POOL, int BN, int NTHR, bool OUT_SPLIT, bool NOSTORE>
+// Epilogue shared by the split-bf16 kernels.  The f32 tile E holds TH*TW
+// pixels of BN channels (bias not yet added), no padding: the 16-B unit u
+// (channels 4u..4u+3) of pixel p sits in slot (u + (p >> PSH)) mod U of the
+// pixel's row, U = BN / 4.  A producer lane writes one unit of 8 pixels p
+// (PSH = 0: consecutive; PSH = 1: every other one, the Winograd pairs) per
+// 8-lane ds_write_b128 group, so the 8 units land in 8 distinct 16-B bank
+// groups.  The reader takes one (pooled pixel, unit) item per lane and lays
+// the items out along ds_read_b128's 16-lane groups ({0-3,12-15,20-27},
+// {4-11,16-19,28-31} and the same +32): one group reads U units of 16 / U
+// pooled pixels whose rows alternate between the two 128-B halves of the
+// 256-B bank space (their pixel indices differ by an odd count for POOL 1 and
+// 3), so every read is conflict-free.  Then POOL x POOL max, bias,
+// activation, and the NHWC store (f32, or the grouped-split layout when
+// OUT_SPLIT).
+template <int BN, int PSH>
+__device__ __forceinline__ int x3_eoff(int p, int u) {  // float offset of unit u of pixel p
+    constexpr int U = BN / 4;
+    return p * BN + (((u + (p >> PSH)) & (U - 1)) << 2);
+}
+
+template <int TH, int TW, int POOL, int BN, int NTHR, bool OUT_SPLIT, bool NOSTORE, int PSH>
 __device__ __forceinline__ void x3_store(const float* E, const float* __restrict__ bias, float* __restrict__ out, int n,
                                          int cb, int oh0, int ow0, int Hout, int Wout, int cout_store, int act,
                                          float alpha) {
-    constexpr int ESTR = BN + 4;
-    constexpr int PHo = TH / POOL, PWo = TW / POOL;
-    constexpr int G = BN / 8;
-    static_assert(NTHR % G == 0, "fixed channel group per thread");
+    constexpr int U = BN / 4;
+    static_assert(U >= 8 && (U & (U - 1)) == 0, "a power-of-two count (>= 8) of units per pixel");
+    static_assert(POOL == 1 || POOL % 2 == 1, "odd pool: neighbouring items alternate row parity");
+    constexpr int PHo = TH / POOL, PWo = TW / POOL, NPO = PHo * PWo;
+    // a 16-lane read group covers 2 pooled pixels x 8 units (U = 8) or 16
+    // units of one pooled pixel (U >= 16: GPP groups per pooled pixel)
+    constexpr int NG16 = NTHR / 16, GPP = U >= 16 ? U / 16 : 1;
+    static_assert(NG16 % GPP == 0, "a lane keeps its unit across passes");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int a = (lane >> 2) & 7;
+    const int gi = 4 * wave + (__builtin_popcount(a) & 1) + 2 * (lane >> 5);
+    const int k = ((a >> 1) << 2) | (lane & 3);
+    const int u = U >= 16 ? (gi % GPP) * 16 + k : (k & 7);
+    const int qo0 = U >= 16 ? gi / GPP : 2 * gi + (k >> 3);
+    constexpr int QSTEP = U >= 16 ? NG16 / GPP : 2 * NG16;
+    const int ch0 = cb * BN + u * 4;
+    const float4 bv = *reinterpret_cast<const float4*>(bias + ch0);  // bias is padded to cout_pad
     const int oh0s = oh0 / POOL, ow0s = ow0 / POOL;
-    const int col = (threadIdx.x % G) * 8;
-    const int ch0 = cb * BN + col;
-    float bv[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) bv[c] = bias[ch0 + c];  // bias is padded to cout_pad
-    float* dst = out + (size_t)n * Hout * Wout * cout_store;
-    for (int qo = threadIdx.x / G; qo < PHo * PWo; qo += NTHR / G) {
+    for (int qo = qo0; qo < NPO; qo += QSTEP) {
         const int pr = qo / PWo, pc = qo - (qo / PWo) * PWo;
         const int gh = oh0s + pr, gw = ow0s + pc;
-        float v[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = -INFINITY;
+        // whole-vector max: per-component fmaxf lets the compiler scalarise
+        // the loads into ds_read2_b32 pairs
+        f32x4 m = *reinterpret_cast<const f32x4*>(E + x3_eoff<BN, PSH>(pr * POOL * TW + pc * POOL, u));
 #pragma unroll
         for (int dy = 0; dy < POOL; ++dy)
 #pragma unroll
-            for (int dx = 0; dx < POOL; ++dx) {
-                const float* e = E + ((pr * POOL + dy) * TW + pc * POOL + dx) * ESTR + col;
-                const float4 a = reinterpret_cast<const float4*>(e)[0], b = reinterpret_cast<const float4*>(e)[1];
-                v[0] = fmaxf(v[0], a.x); v[1] = fmaxf(v[1], a.y); v[2] = fmaxf(v[2], a.z); v[3] = fmaxf(v[3], a.w);
-                v[4] = fmaxf(v[4], b.x); v[5] = fmaxf(v[5], b.y); v[6] = fmaxf(v[6], b.z); v[7] = fmaxf(v[7], b.w);
+            for (int dx = (dy == 0); dx < POOL; ++dx) {
+                const int p = (pr * POOL + dy) * TW + pc * POOL + dx;
+                m = __builtin_elementwise_max(m, *reinterpret_cast<const f32x4*>(E + x3_eoff<BN, PSH>(p, u)));
             }
+        float4 v = make_float4(m[0], m[1], m[2], m[3]);
         if (gh >= Hout || gw >= Wout) continue;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = apply_act(v[c] + bv[c], act, alpha);
+        v.x = apply_act(v.x + bv.x, act, alpha);
+        v.y = apply_act(v.y + bv.y, act, alpha);
+        v.z = apply_act(v.z + bv.z, act, alpha);
+        v.w = apply_act(v.w + bv.w, act, alpha);
         if constexpr (NOSTORE) {
-            if (v[0] != 12345.f) continue;  // keep the values live, store (almost) never
+            if (v.x != 12345.f) continue;  // keep the values live, store (almost) never
         }
         if constexpr (OUT_SPLIT) {
-            // grouped split: 8 channels of group ch0 / 32 -> one 16-B hi unit and
-            // one 16-B lo unit (cout_store % 32 == 0, planner-checked)
+            // grouped split: 4 channels of group ch0 / 32 -> 8 B of the hi half
+            // and 8 B of the lo half (cout_store % 32 == 0, planner-checked)
             if (ch0 < cout_store) {
                 char* o = reinterpret_cast<char*>(out) + ((size_t)n * Hout * Wout + (size_t)gh * Wout + gw) * cout_store * 4 +
                           (ch0 >> 5) * 128 + (ch0 & 31) * 2;
-                uint32_t h[4], l[4];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) split2(v[2 * c], v[2 * c + 1], h[c], l[c]);
-                *reinterpret_cast<uint4*>(o) = make_uint4(h[0], h[1], h[2], h[3]);
-                *reinterpret_cast<uint4*>(o + 64) = make_uint4(l[0], l[1], l[2], l[3]);
+                uint32_t h0, l0, h1, l1;
+                split2(v.x, v.y, h0, l0);
+                split2(v.z, v.w, h1, l1);
+                *reinterpret_cast<uint2*>(o) = make_uint2(h0, h1);
+                *reinterpret_cast<uint2*>(o + 64) = make_uint2(l0, l1);
             }
         } else {
-            float* o = dst + ((size_t)gh * Wout + gw) * cout_store + ch0;
-            if (ch0 + 8 <= cout_store) {
-                reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
-                reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+            float* o = out + ((size_t)n * Hout * Wout + (size_t)gh * Wout + gw) * cout_store + ch0;
+            if (ch0 + 4 <= cout_store) {
+                *reinterpret_cast<float4*>(o) = v;
             } else {
-                for (int c = 0; c < 8 && ch0 + c < cout_store; ++c) o[c] = v[c];
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+                for (int c = 0; c < 4 && ch0 + c < cout_store; ++c) o[c] = vv[c];
             }
         }
     }
@@ -680,23 +704,22 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
 #undef X3_GLDS
     __syncthreads();  // patch and ring no longer needed: the f32 tile reuses LDS
 
-    // ---- epilogue: f32 tile [TH*TW][BN+4], pool, bias, activation, NHWC f32 ----
-    constexpr int ESTR = BN + 4;
+    // ---- epilogue: f32 tile (x3_store's swizzled layout), pool, bias, activation, store ----
     float* E = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
-        const int c0 = wn * NF * 16 + j * 16 + 4 * q;
+        const int u = wn * NF * 4 + j * 4 + q;
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             const int p = (wm * MF + i) * 16 + (lane & 15);
             if (p < TH * TW)
-                *reinterpret_cast<float4*>(E + p * ESTR + c0) =
+                *reinterpret_cast<float4*>(E + x3_eoff<BN, 0>(p, u)) =
                     make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
         }
     }
     __syncthreads();
-    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, (DIAG & 4) != 0>(E, bias, out, n, cb, oh0, ow0, Hout, Wout, cout_store, act,
-                                                               alpha);
+    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, (DIAG & 4) != 0, 0>(E, bias, out, n, cb, oh0, ow0, Hout, Wout,
+                                                                  cout_store, act, alpha);
 }
 
 }  // namespace aa

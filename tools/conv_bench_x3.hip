@@ -161,6 +161,18 @@ int main(int argc, char** argv) {
 #define W4(WM, WN, MF, NF, TH, TW, O, D) time_wg<3, 64, WM, WN, MF, NF, 1, TH, TW, O, true, true, D>("c4", n, 50, 72, 64, in, w, b, out, it);
 #define W3(WM, WN, MF, NF, TH, TW, O, D) time_wg<3, 32, WM, WN, MF, NF, 1, TH, TW, O, true, true, D>("c3", n, 52, 74, 64, in, w, b, out, it);
 #define W6(WM, WN, MF, NF, TH, TW, O, D) time_wg<1, 128, WM, WN, MF, NF, 1, TH, TW, O, true, false, D>("c6", n, 13, 22, 256, in, w, b, out, it);
+    if (which == 19) {  // the shipped split-bf16 tiles (aa_cnn.hip AA_X3_CFGS / AA_WG_CFGS), then fused-kernel ablations
+#define FS(D) time_one<3, 3, 32, 4, 1, 4, 2, 3, 12, 21, true, D, false, true, 0, false, true>("c1+c2 d" #D, n, 158, 224, 32, in, w, b, out, f1, it);
+        FS(0) S3(4, 2, 3, 2, 10, 18, true, false, 4) S4(2, 2, 3, 2, 12, 8, true, true, 0)
+        W5(2, 2, 4, 2, 39, 6, 2, 0) S6(2, 2, 3, 2, 7, 12, true, true, 0)
+        FS(2) FS(64) FS(4) FS(128) FS(16) FS(512) FS(576) FS(0)
+        return 0;
+    }
+    if (which == 20) {  // the shipped fused kernel once (PMC passes)
+        time_one<3, 3, 32, 4, 1, 4, 2, 3, 12, 21, true, 0, false, true, 0, false, true>("c1+c2", n, 158, 224, 32, in, w, b, out, f1, 1);
+        W5(2, 2, 4, 2, 39, 6, 2, 0)
+        return 0;
+    }
     if (which == 18) {  // LDS bank conflicts of the fused kernel by phase (PMC): full, no conv1 compute, no MFMA loop
         ABL2(66) ABL2(70) ABL2(578) ABL2(582)
         return 0;
