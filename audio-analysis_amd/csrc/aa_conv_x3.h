@@ -48,6 +48,17 @@ constexpr int X3_CG = 32;  // channels per staged group
 #ifndef AA_X3_REMAP
 #define AA_X3_REMAP 1
 #endif
+// AA_F1_KPACK: the fused first layer's 27 split products (hi.hi, hi.lo,
+// lo.hi over 9 taps) in 2 MFMAs instead of 3; AA_X3_SCALAR_SPLIT: its
+// activation / split in scalar f32 ops (packed f32 VALU costs extra issue
+// beside MFMAs).  Together: fused conv 136 -> 126 us in the pipeline
+// (harness 140 -> 132 us; each alone within the noise).
+#ifndef AA_F1_KPACK
+#define AA_F1_KPACK 1
+#endif
+#ifndef AA_X3_SCALAR_SPLIT
+#define AA_X3_SCALAR_SPLIT 1
+#endif
 
 // Scheduling pins for the kernels whose waves load their own B fragments
 // from global memory (conv_x3 with RING = false, conv_wg).  Bit 0: the next
@@ -123,6 +134,18 @@ __device__ __forceinline__ void split2(float x0, float x1, uint32_t& hi, uint32_
 __device__ __forceinline__ void leaky_split2(float x0, float x1, float a, uint32_t& hi, uint32_t& lo) {
     typedef __attribute__((ext_vector_type(2))) float f2;
     typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+#if AA_X3_SCALAR_SPLIT
+    // scalar f32 ops only (packed f32 VALU costs extra issue beside MFMAs)
+    float o0, o1, r0, r1;
+    asm("v_mul_f32 %0, %1, %2" : "=v"(r0) : "v"(x0), "v"(a));
+    asm("v_mul_f32 %0, %1, %2" : "=v"(r1) : "v"(x1), "v"(a));
+    asm("v_max_f32 %0, %1, %2" : "=v"(o0) : "v"(x0), "v"(r0));
+    asm("v_max_f32 %0, %1, %2" : "=v"(o1) : "v"(x1), "v"(r1));
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{o0, o1}, b2));
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r0) : "v"(o0), "v"(__uint_as_float(hi << 16)));
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r1) : "v"(o1), "v"(__uint_as_float(hi & 0xffff0000u)));
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{r0, r1}, b2));
+#else
     const f2 s = f2{x0, x1} * a;
     float o0, o1;
     asm("v_max_f32 %0, %1, %2" : "=v"(o0) : "v"(x0), "v"(s.x));
@@ -131,6 +154,7 @@ __device__ __forceinline__ void leaky_split2(float x0, float x1, float a, uint32
     hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(o, b2));
     const f2 hf = f2{__uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
     lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(o - hf, b2));
+#endif
 }
 
 // byte offset of unit u of patch pixel (R, C)
@@ -300,6 +324,10 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     char* patch = smem;
     char* Bs = smem + x3_patch_bytes<KH, KW, TH, TW, FUSED>();
 
+    // DIAG 4096 (tools/conv_bench_x3.hip): per-wave phase timestamps
+    // (s_memtime) and hardware ids after the output, for timeline analysis
+    unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if constexpr (DIAG & 4096) ts[0] = __builtin_amdgcn_s_memtime();
     const BlockPos bp = x3_block<AA_X3_REMAP != 0>();
     const int n = bp.n, cb = bp.cb;
     const int th = bp.tile / tiles_w, tw = bp.tile - (bp.tile / tiles_w) * tiles_w;
@@ -463,6 +491,45 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         }
     };
 
+    // The fused first layer's weights and bias (f32 -> bf16 hi / lo), loaded
+    // before the log-mel staging so their L2 latency overlaps the log-mel's.
+    // MFMA row m (A operand lane m) computes first-layer channel
+    // 16 ((m >> 2) & 1) + 4 (m >> 3) + (m & 3), so that the D register r
+    // of a k-group kg lane (row 8 (r / 4) + 4 kg + r % 4) holds channel
+    // 16 kg + r: each lane owns two whole 8-channel units of its pixel
+    // and writes them as ds_write_b128 (eight consecutive pixels per
+    // lane group: conflict-free), not as eight half units
+    bf16x8 f1_wa{}, f1_wal{};
+    f32x16 f1_cb{};  // D register r: channel 16 kg + r
+    if constexpr (FUSED) {
+        const int l32 = lane & 31, kg = lane >> 5;
+        const int ch1 = 16 * ((l32 >> 2) & 1) + 4 * (l32 >> 3) + (l32 & 3);
+        if constexpr (AA_F1_KPACK) {
+            // the 27 products of a pixel (hi.hi, hi.lo, lo.hi over 9 taps) in the
+            // 32 k-slots of two MFMAs: MFMA 1 = wh.xh (k-group 0) and wh.xl
+            // (k-group 1) over taps 0-7; MFMA 2 = wl.xh over taps 0-7 (k-group
+            // 0) and wh8.xh8, wh8.xl8, wl8.xh8 (k-group 1)
+            float w9[9];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) w9[t] = fc.w[ch1 * 9 + t];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                f1_wa[j] = bf_hi(w9[j]);
+                f1_wal[j] = kg == 0 ? bf_lo(w9[j]) : j < 2 ? bf_hi(w9[8]) : j == 2 ? bf_lo(w9[8]) : (bf16)0.f;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int tap = 8 * kg + j;
+                const float wv = fc.w[ch1 * 9 + min(tap, 8)];
+                f1_wa[j] = tap < 9 ? bf_hi(wv) : (bf16)0.f;
+                f1_wal[j] = tap < 9 ? bf_lo(wv) : (bf16)0.f;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) f1_cb[r] = fc.b[16 * kg + r];
+    }
+
     if constexpr (!RING) read_b(F0, 0);  // its latency hides behind the first staging
     for (int g = 0; g < NG; ++g) {
         // ---- stage channel group g of the patch (hi / lo planes, swizzled) ----
@@ -576,27 +643,13 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 }
             }
             const int l32 = lane & 31, kg = lane >> 5;
-            // MFMA row m (A operand lane m) computes first-layer channel
-            // 16 ((m >> 2) & 1) + 4 (m >> 3) + (m & 3), so that the D register r
-            // of a k-group kg lane (row 8 (r / 4) + 4 kg + r % 4) holds channel
-            // 16 kg + r: each lane owns two whole 8-channel units of its pixel
-            // and writes them as ds_write_b128 (eight consecutive pixels per
-            // lane group: conflict-free), not as eight half units
-            const int ch1 = 16 * ((l32 >> 2) & 1) + 4 * (l32 >> 3) + (l32 & 3);
-            bf16x8 wa, wal;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int tap = 8 * kg + j;
-                const float wv = tap < 9 ? fc.w[ch1 * 9 + tap] : 0.f;
-                wa[j] = bf_hi(wv);
-                wal[j] = bf_lo(wv);
-            }
-            f32x16 cb;  // D register r: channel 16 kg + r
-#pragma unroll
-            for (int r = 0; r < 16; ++r) cb[r] = fc.b[16 * kg + r];
+            const bf16x8 wa = f1_wa, wal = f1_wal;
+            const f32x16 cb = f1_cb;
             const float ae = fc.alpha;  // host: act folded to a slope in [0, 1]
             const int off0 = kg ? 2 * XW + 2 : 0;  // k-group 1 only needs tap 8 (j = 0)
+            if constexpr (DIAG & 4096) ts[4] = __builtin_amdgcn_s_memtime();
             __syncthreads();
+            if constexpr (DIAG & 4096) ts[5] = __builtin_amdgcn_s_memtime();
             constexpr int NPX = PH * PW;
             constexpr int NGRP = (NPX + 31) / 32;
             // NU groups of 32 pixels per wave and pass (groups g0 + NW u): all
@@ -610,7 +663,27 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 for (int u = 0; u < NU; ++u) {
                     pix[u] = min((g0 + NW * u) * 32 + l32, NPX - 1);
                     const int r = pix[u] / PW, c = pix[u] - r * PW;
-                    if constexpr (AA_X3_XSPLIT) {
+                    if constexpr (AA_F1_KPACK) {
+                        // taps 2k, 2k+1 -> one dword of MFMA 1's operand: their
+                        // hi halves in k-group 0, lo halves in k-group 1; MFMA 2
+                        // takes the same (k-group 0) or tap 8's hi, lo, hi
+                        const uint32_t* xp = Xs + r * XW + c;
+                        uint32_t xv[9];
+#pragma unroll
+                        for (int j = 0; j < 9; ++j) xv[j] = xp[(j / 3) * XW + j % 3];
+                        const uint32_t psel = kg ? 0x07060302u : 0x05040100u;
+                        uint4 b1, b2;
+                        b1.x = __builtin_amdgcn_perm(xv[1], xv[0], psel);
+                        b1.y = __builtin_amdgcn_perm(xv[3], xv[2], psel);
+                        b1.z = __builtin_amdgcn_perm(xv[5], xv[4], psel);
+                        b1.w = __builtin_amdgcn_perm(xv[7], xv[6], psel);
+                        b2.x = kg ? xv[8] : b1.x;
+                        b2.y = kg ? (xv[8] & 0xffffu) : b1.y;
+                        b2.z = kg ? 0u : b1.z;
+                        b2.w = kg ? 0u : b1.w;
+                        xh[u] = __builtin_bit_cast(bf16x8, b1);
+                        xl[u] = __builtin_bit_cast(bf16x8, b2);
+                    } else if constexpr (AA_X3_XSPLIT) {
                         // taps 2k, 2k+1 of the pre-split patch -> one dword of
                         // the hi fragment (low halves) and one of the lo (high halves)
                         const uint32_t* xp = Xs + r * XW + c;
@@ -643,12 +716,25 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                     }
                 }
                 f32x16 d[NU];
+                if constexpr (DIAG & 8192) {  // ablation: no first-layer MFMAs
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        d[u] = cb;
+                        d[u][0] += __builtin_bit_cast(float, __builtin_bit_cast(uint4, xh[u]).x ^ __builtin_bit_cast(uint4, xl[u]).y);
+                    }
+                } else if constexpr (AA_F1_KPACK) {
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xh[u], cb, 0, 0, 0);
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wal, xl[u], d[u], 0, 0, 0);
+                } else {
 #pragma unroll
                 for (int u = 0; u < NU; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xh[u], cb, 0, 0, 0);
 #pragma unroll
                 for (int u = 0; u < NU; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xl[u], d[u], 0, 0, 0);
 #pragma unroll
                 for (int u = 0; u < NU; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wal, xh[u], d[u], 0, 0, 0);
+                }
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
                     if ((g0 + NW * u) * 32 + l32 < NPX) {
@@ -657,9 +743,16 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                         for (int h = 0; h < 2; ++h) {  // channels 16 kg + 8 h + e: unit 2 kg + h
                             uint32_t hw[4], lw[4];
 #pragma unroll
-                            for (int e = 0; e < 8; e += 2)
-                                leaky_split2(d[u][8 * h + e], d[u][8 * h + e + 1], ae, hw[e >> 1], lw[e >> 1]);
+                            for (int e = 0; e < 8; e += 2) {
+                                if constexpr (DIAG & 16384) {  // ablation: no activation / split VALU
+                                    hw[e >> 1] = __builtin_bit_cast(uint32_t, d[u][8 * h + e]);
+                                    lw[e >> 1] = __builtin_bit_cast(uint32_t, d[u][8 * h + e + 1]);
+                                } else {
+                                    leaky_split2(d[u][8 * h + e], d[u][8 * h + e + 1], ae, hw[e >> 1], lw[e >> 1]);
+                                }
+                            }
                             const int a = x3_addr(R, C, 2 * kg + h, PW, TW);
+                            if ((DIAG & 32768) && hw[0] != 0x12345u) continue;  // ablation: no patch writes
                             *reinterpret_cast<uint4*>(patch + a) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
                             *reinterpret_cast<uint4*>(patch + (a ^ 64)) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
                         }
@@ -667,6 +760,7 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 }
             }
         }
+        if constexpr (DIAG & 4096) ts[6] = __builtin_amdgcn_s_memtime();
 
         // ---- the group's taps: one 32-deep K chunk each, through the ring.
         // Software-pipelined by one step: the barrier at the top of step s
@@ -695,11 +789,13 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         // (the bottom tile row of a tall tile) skips its MFMAs: those outputs
         // are discarded by the epilogue
         const bool wave_idle = oh0 + (wm * MF * 16) / TW >= Hout * POOL;
+        if constexpr (DIAG & 4096) ts[1] = __builtin_amdgcn_s_memtime();
 #pragma unroll
         for (int t = 0; t < ((DIAG & 2) || wave_idle ? 0 : NTAP); t += 2) {
             step(F0, F1, g, t);
             if (t + 1 < NTAP) step(F1, F0, g, t + 1);
         }
+        if constexpr (DIAG & 4096) ts[2] = __builtin_amdgcn_s_memtime();
     }
 #undef X3_GLDS
     __syncthreads();  // patch and ring no longer needed: the f32 tile reuses LDS
@@ -720,6 +816,16 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     __syncthreads();
     x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, (DIAG & 4) != 0, 0>(E, bias, out, n, cb, oh0, ow0, Hout, Wout,
                                                                   cout_store, act, alpha);
+    if constexpr (DIAG & 4096) {
+        ts[3] = __builtin_amdgcn_s_memtime();
+        if (lane == 0) {
+            const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+            unsigned long long* d = reinterpret_cast<unsigned long long*>(out + (64u << 20)) + ((size_t)L * NW + wave0) * 10;
+            for (int k = 0; k < 8; ++k) d[k] = ts[k];
+            d[8] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+            d[9] = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+        }
+    }
 }
 
 }  // namespace aa

@@ -168,6 +168,21 @@ int main(int argc, char** argv) {
         FS(2) FS(64) FS(4) FS(128) FS(16) FS(512) FS(576) FS(0)
         return 0;
     }
+    if (which == 21) {  // the shipped fused kernel, three timings (variant A/B across builds)
+        FS(0) FS(0) FS(0)
+        return 0;
+    }
+    if (which == 22) {  // per-wave phase timestamps of the shipped fused kernel -> gpurun_out/fused_ts.bin
+        FS(0)
+        const size_t cnt = (size_t)9152 * 4 * 10;
+        std::vector<unsigned long long> ts(cnt);
+#define TSD(D)                                                                                                        \
+        time_one<3, 3, 32, 4, 1, 4, 2, 3, 12, 21, true, 4096 | D, false, true, 0, false, true>("c1+c2 ts" #D, n, 158, 224, 32, in, w, b, out, f1, 1); \
+        (void)hipMemcpy(ts.data(), (char*)out + (64u << 22), cnt * 8, hipMemcpyDeviceToHost);                         \
+        { FILE* f = fopen("gpurun_out/fused_ts_" #D ".bin", "wb"); fwrite(ts.data(), 8, cnt, f); fclose(f); }
+        TSD(0) TSD(8192) TSD(16384) TSD(32768) TSD(57344) TSD(64) TSD(2)
+        return 0;
+    }
     if (which == 20) {  // the shipped fused kernel once (PMC passes)
         time_one<3, 3, 32, 4, 1, 4, 2, 3, 12, 21, true, 0, false, true, 0, false, true>("c1+c2", n, 158, 224, 32, in, w, b, out, f1, 1);
         W5(2, 2, 4, 2, 39, 6, 2, 0)
