@@ -24,6 +24,7 @@
 #include "aa_common.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -1084,6 +1085,7 @@ __global__ void track_mean(const float* __restrict__ probs, int n_models, long l
 #include "aa_conv_x3.h"
 #include "aa_conv_wg.h"
 #include "aa_gconv.h"
+#include "aa_conv_tail.h"
 
 namespace aa {
 
@@ -1121,6 +1123,8 @@ struct Stage {
     int out_split = 0;
     int wg = 0;           // split-bf16 Winograd F(2,3)-along-W kernel (aa_conv_wg.h) and its weight packing
     int cin_pad = 0;      // ST_GCONV: C_in rounded up to 32
+    int tail = 0;         // ST_HEAD, split-bf16: computes the previous conv stage itself (aa_conv_tail.h)
+    void* d_tw = nullptr;  // tail: head weights packed per wave / label fragment, hi then lo
 };
 
 struct Model {
@@ -1360,6 +1364,34 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
         AA_LAUNCH_CHECK();
         return AA_OK;
     }
+    if (s.kind == ST_HEAD && s.tail) {
+        if constexpr (is_split<T>()) {
+            // the last conv stage and the head in one launch (aa_conv_tail.h):
+            // per-tile label maxima into `out`, then head_final over the tiles
+            const Stage& c = *first;
+            constexpr int TH = 13, TW = 5;
+            const int tiles_h = (c.Hc + TH - 1) / TH, tiles_w = (c.Wc + TW - 1) / TW;
+            auto k = conv_tail_x3<1, 3, 128, 5, TH, TW>;
+            constexpr size_t lds = tail_lds_bytes<1, 3, 128, TH, TW>();
+            static bool attr = false;
+            if (!attr) {
+                AA_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                attr = true;
+            }
+            float* part = static_cast<float*>(out);
+            hipLaunchKernelGGL(k, dim3(tiles_h * tiles_w, 1, n), dim3(TAIL_NW * 64), lds, st, (const float*)in, c.Hin,
+                               c.Win, (const bf16*)c.d_w, c.d_b, c.Hc, c.Wc, tiles_w, c.act, c.alpha,
+                               (const bf16*)s.d_tw, part);
+            AA_LAUNCH_CHECK();
+            hipLaunchKernelGGL(head_final, dim3(n), dim3(64), 0, st, part, tiles_h * tiles_w, 32, s.d_b, s.cout, s.act,
+                               s.alpha, s.sigmoid, logits, probs, (const float*)nullptr);
+            AA_LAUNCH_CHECK();
+            return AA_OK;
+        } else {
+            set_error("%s: the fused tail is split-bf16 only", s.name.c_str());
+            return AA_ERR_UNSUPPORTED;
+        }
+    }
     if (s.kind == ST_HEAD) {
         // pixel ranges of 64 spread over blocks (a window alone is too little
         // work for one block's dependent load chain), 32 labels per block;
@@ -1443,6 +1475,7 @@ static void free_model(Model* m) {
     for (auto& s : m->st) {
         (void)hipFree(s.d_w);
         (void)hipFree(s.d_b);
+        (void)hipFree(s.d_tw);
     }
     delete m;
 }
@@ -1868,6 +1901,46 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             b.in_split = 1;
         }
     }
+    // split-bf16: the 1x3/128 -> 256 conv before a 1x1 head (<= 32 labels) and
+    // the head in one kernel (aa_conv_tail.h); the conv's 13 x 20 x 256
+    // activations never reach HBM.  AA_NO_TAIL=1 keeps them separate.
+    if (precision == AA_PREC_BF16X3 && m->st.size() >= 2 && !getenv("AA_NO_TAIL")) {
+        Stage& h = m->st.back();
+        Stage& c = m->st[m->st.size() - 2];
+        if (h.kind == ST_HEAD && h.cout <= 32 && h.cout_pad == 32 && h.cin == 256 && c.kind == ST_MFMA && !c.skipped &&
+            !c.fused_first && !c.wg && c.in_split && !c.out_split && c.kh == 1 && c.kw == 3 && c.cin == 128 &&
+            c.cout == 256 && c.cout_pad == 256 && c.pool == 1 && c.ph == 1 && c.pw == 1) {
+            // head weights f32 [cout_pad][256] -> per (wave w, label fragment lf,
+            // hi / lo, lane l) 8 bf16: label 16 lf + (l & 15), k-slot e <-> channel
+            // 32 w + (e < 4 ? 4 (l >> 4) + e : 16 + 4 (l >> 4) + e - 4)
+            std::vector<float> hwf((size_t)h.cout_pad * h.cin);
+            hipError_t e = hipMemcpy(hwf.data(), h.d_w, hwf.size() * 4, hipMemcpyDeviceToHost);
+            std::vector<uint16_t> pk((size_t)TAIL_NW * 2 * 2 * 64 * 8, 0);
+            for (int w = 0; w < TAIL_NW; ++w)
+                for (int lf = 0; lf < 2; ++lf)
+                    for (int l = 0; l < 64; ++l)
+                        for (int k = 0; k < 8; ++k) {
+                            const int lab = lf * 16 + (l & 15), qq = l >> 4;
+                            const int co = 32 * w + (k < 4 ? 4 * qq + k : 16 + 4 * qq + k - 4);
+                            const float v = lab < h.cout ? hwf[(size_t)lab * h.cin + co] : 0.f;
+                            const uint16_t hi = f2bf(v);
+                            pk[((((size_t)w * 2 + lf) * 2 + 0) * 64 + l) * 8 + k] = hi;
+                            pk[((((size_t)w * 2 + lf) * 2 + 1) * 64 + l) * 8 + k] = f2bf(v - bf2f(hi));
+                        }
+            if (e == hipSuccess) e = hipMalloc(&h.d_tw, pk.size() * 2);
+            if (e == hipSuccess) e = hipMemcpy(h.d_tw, pk.data(), pk.size() * 2, hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                set_error("aa_model_create: %s", hipGetErrorString(e));
+                free_model(m);
+                return AA_ERR_HIP;
+            }
+            c.skipped = 1;
+            h.tail = 1;
+            h.flops += c.flops;
+            h.bytes = 4.0 * c.Hin * c.Win * c.cin + 4.0 * h.cout;
+            h.name = c.name + "+" + h.name;
+        }
+    }
     // ping-pong activation buffers: stage s writes buffer s % 2
     for (size_t k = 0; k + 1 < m->st.size(); ++k) {
         const Stage& s = m->st[k];
@@ -1881,6 +1954,11 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         const size_t parts = ((size_t)h.Hin * h.Win + 63) / 64;
         const size_t k = m->st.size() - 1;
         m->act_elems[k % 2] = std::max(m->act_elems[k % 2], (parts * h.cout_pad * sizeof(float) + es - 1) / es);
+        if (h.tail) {  // the fused tail's per-tile maxima go to the skipped conv stage's buffer
+            const Stage& c = m->st[k - 1];
+            const size_t tiles = (size_t)((c.Hc + 12) / 13) * ((c.Wc + 4) / 5);
+            m->act_elems[(k - 1) % 2] = std::max(m->act_elems[(k - 1) % 2], (tiles * 32 * sizeof(float) + es - 1) / es);
+        }
     }
     *model = m;
     return AA_OK;
@@ -1945,8 +2023,10 @@ extern "C" int aa_model_forward(void* model, const void* x, int32_t n, float* lo
     for (size_t k = 0; k < m->st.size(); ++k) {
         Stage& s = m->st[k];
         if (s.skipped) continue;  // computed inside stage k + 1 (reads x directly)
-        void* out = buf[k % 2];
-        const Stage* first = s.fused_first ? &m->st[k - 1] : nullptr;
+        // (a fused tail writes its per-tile maxima into the skipped conv stage's
+        // buffer: its own would be the one its input lives in)
+        void* out = buf[(s.tail ? k - 1 : k) % 2];
+        const Stage* first = (s.fused_first || s.tail) ? &m->st[k - 1] : nullptr;
         hipEvent_t e0;
         int rc = m->timer.begin((int)k, st, &e0);
         if (rc != AA_OK) return rc;
