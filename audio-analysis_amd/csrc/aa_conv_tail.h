@@ -35,6 +35,9 @@ namespace aa {
 
 constexpr int TAIL_NW = 8;     // waves per block
 constexpr int TAIL_COUT = 256;  // conv output channels (32 per wave)
+#ifndef TAIL_BD
+#define TAIL_BD 2  // B register sets in flight (prefetch distance + 1; 4 measured neutral)
+#endif
 constexpr int TAIL_SSTR = 36;   // floats per pixel row of a partial-sum slot (32 labels + 4: conflict-free)
 
 template <int KH, int KW, int CIN, int TH, int TW>
@@ -118,14 +121,20 @@ __global__ __launch_bounds__(TAIL_NW * 64) void conv_tail_x3(
 #pragma unroll
     for (int i = 0; i < MF; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    BSet B0, B1;
-    read_b(B0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's patch pieces (and B of step 0) landed
+    // B fragments BD - 1 steps ahead in a register ring (two waves per SIMD
+    // leave few other waves to hide the L2 latency of the per-step loads)
+    constexpr int BD = TAIL_BD;
+    BSet Bq[BD];
+#pragma unroll
+    for (int s = 0; s < BD - 1; ++s)
+        if (s < NSTEP) read_b(Bq[s], s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's patch pieces (and the first B sets) landed
     __syncthreads();
 
-    auto step = [&](BSet& cur, BSet& nxt, int s) {
+    auto step = [&](int s) {
+        BSet& cur = Bq[s % BD];
         const int g = s / NTAP, t = s - (s / NTAP) * NTAP;
-        if (s + 1 < NSTEP) read_b(nxt, s + 1);
+        if (s + BD - 1 < NSTEP) read_b(Bq[(s + BD - 1) % BD], s + BD - 1);
         const int kh = t / KW, kw = t - (t / KW) * KW;
         const int toff = g * GIMG + (kh * PW + kw) * 128, tv = kh * TW + kw;
         bf16x8 h2[2], l2[2];
@@ -149,10 +158,7 @@ __global__ __launch_bounds__(TAIL_NW * 64) void conv_tail_x3(
         }
     };
 #pragma unroll
-    for (int s = 0; s < NSTEP; s += 2) {
-        step(B0, B1, s);
-        if (s + 1 < NSTEP) step(B1, B0, s + 1);
-    }
+    for (int s = 0; s < NSTEP; ++s) step(s);
 
     // ---- head: bias + activation + split of the accumulators = B operand ----
     // lane k-slot 8 q + e <-> channel 32 wave + (e < 4 ? 4 q + e : 16 + 4 q + e - 4)
