@@ -261,17 +261,28 @@ def main_step(args, world, rank, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # calibration (untimed): every launch bracketed by events, to find the
-    # dominant kernel; the timed region then carries events around that one only
+    # calibration (untimed): one pass with every launch bracketed finds the
+    # stages that launch (a fused stage launches nothing); then each stage is
+    # timed on its own -- events around that launch only, 5 steps each -- so no
+    # stage pays for its neighbours' events (bracketing them all inflates the
+    # sum past the step).  The dominant stage gets the events of the timed region.
     fe.set_timing(True)
     model.set_timing(True)
-    for _ in range(5):
+    for _ in range(2):
         step()
     torch.cuda.synchronize()
-    calib = [c for c in collect(step.launches(), n_win) if c["count"] > 0]  # a fused stage launches nothing
-    launches = [(c["owner"], c["idx"]) for c in calib]
+    launched = [c for c in collect(step.launches(), n_win) if c["count"] > 0]
     fe.set_timing(False)
     model.set_timing(False)
+    launches = [(c["owner"], c["idx"]) for c in launched]
+    calib = []
+    for owner, idx in launches:
+        owner.set_timing(True, stages=[idx])
+        for _ in range(5):
+            step()
+        torch.cuda.synchronize()
+        calib.append(collect([(owner, idx)], n_win)[0])
+        owner.set_timing(False)
     dom = max(calib, key=lambda x: x["avg_ms"])
     dom["owner"].set_timing(True, stages=[dom["idx"]])
     elapsed = timed(step, args.steps, 0, world)
@@ -307,7 +318,8 @@ def main_step(args, world, rank, dev):
                 "algorithmic_bytes": round(dom["bytes"]), "algorithmic_flops": round(dom["flops"]),
                 "avg_ms": round(dom_live["avg_ms"], 4), "launches_timed": dom_live["count"],
                 "traffic_source": traffic_src,
-                "stages_ms": {c["name"]: round(c["avg_ms"], 4) for c in calib}}
+                "stages_ms": {c["name"]: round(c["avg_ms"], 4) for c in calib},
+                "stages_sum_ms": round(sum(c["avg_ms"] for c in calib), 4)}
     # every stage against its own bound (the dominant one above): algorithmic
     # flops or bytes of the calibration pass / its event-timed average
     per = {}
@@ -357,12 +369,16 @@ def main_step(args, world, rank, dev):
                 continue
             s2 = Step(dev, rank, model_path, prec, pairs=COLD_POOL if mode == "cold" else 1, first=first,
                       lm16=mode.endswith("_f16mel") or (mode == "cold" and args.logmel == "f16"))
-            el = timed(s2, max(10, args.steps // 2), 5, 1)
-            n2 = max(10, args.steps // 2)
+            n2 = args.steps if mode == "cold" else max(10, args.steps // 2)
+            el = timed(s2, n2, 5, 1)
             e = {"value": round(n2 * s2.n_win * SECONDS_PER_WINDOW / el, 1), "ms_per_step": round(1e3 * el / n2, 4),
                  "steps": n2, "dtype": prec + (" (fp16 log-mel)" if s2.logmel.dtype == torch.float16 else "")}
             if mode == "cold":
                 e["note"] = f"fresh clip pair per step from {COLD_POOL} resident pairs (> Infinity Cache)"
+                # the headline step re-timed right after, same step count: the
+                # cold/warm ratio without the clock drift between the two runs
+                el_w = timed(step, n2, 5, 1)
+                e["warm_same_run"] = round(n2 * n_win * SECONDS_PER_WINDOW / el_w, 1)
             elif ref is not None:
                 s2.k = 0
                 s2()
