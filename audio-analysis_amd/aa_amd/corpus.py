@@ -65,7 +65,7 @@ def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world
     if examine_fn is None and batch and torch.cuda.is_available():
         from .batch import BatchAnalyser
         ba = BatchAnalyser(bird_models, analyse_tracks, device=torch.device("cuda", torch.cuda.current_device()),
-                           batch=batch, lanes=int(os.environ.get("AA_BATCH_LANES", "2")))
+                           batch=batch, lanes=int(os.environ.get("AA_BATCH_LANES", "3")))
         return gather_documents(ba.run([(i, str(f)) for i, f in mine]), device=device)
     if examine_fn is None:
         from .analyse import examine as examine_fn

@@ -8,17 +8,22 @@
 //                 the lane holding Z[k] and its mirror Z[2048 - k] forms
 //                 X[k] = E + W^k O and X[2048 - k] = conj(E - W^k O).  Writes
 //                 the frame-major magnitude S[f][0..2048] and the maximum.
+//   sn_zero       the per-run counters (global max, run count, status) = 0
 //   sn_colmed     the frame's median over bins: radix select on the f32 bit
 //                 patterns of the S row, values in registers, digits below the
-//                 row's common min/max prefix, 4 LDS histograms per wave
+//                 row's common min/max prefix, 4 LDS histograms per wave; and
+//                 the frame's threshold c3 = 3 (colmed / a) (numpy's f32 steps)
 //   sn_transpose  S -> ST[bin][frame] (64 x 64 tiles through LDS)
 //   sn_select     per-bin median over frames: radix select over the ST row
-//                 (staged in LDS), both middle elements for an even count
-//   sn_thresholds 3 colmed/a per frame, 3 rowmed/a per bin (numpy's f32 steps)
-//   sn_mask       (S/a > 3 colmed/a) & (S/a > 3 rowmed/a) (:656-669),
+//                 (staged in LDS), both middle elements for an even count;
+//                 then the row's threshold r3 = 3 rowmed / a and its mask bits
+//                 (S/a > c3) & (S/a > r3) (:656-669) from the staged row,
 //                 bit-packed along time by ballot
-//   sn_morph_h/v  cv2 erode / dilate with rectangles (:670-684), separable,
-//                 64 frames per 64-bit word
+//   sn_morph      cv2 erode / dilate with a rectangle (:670-684): the
+//                 vertical reduction of three neighbouring 64-frame words,
+//                 then the horizontal one on the reduced words (a rectangle
+//                 is separable and the two orders give the same bits), one
+//                 launch per structuring element
 //   sn_runs, sn_unite, sn_stats, sn_emit
 //                 8-connected components over row runs (:686): union-find with
 //                 atomicMin hooking, bounding box, area and OpenCV's label-order
@@ -84,6 +89,15 @@ __device__ __forceinline__ unsigned hist_pick(const unsigned* hist, unsigned ran
     *below = __shfl(bl, src, 64);
     *cnt = __shfl(cn, src, 64);
     return __shfl(dig, src, 64);
+}
+
+// sn_zero: the counters a run accumulates into (atomicMax / atomicAdd), one
+// launch instead of a memset per buffer
+__global__ void sn_zero(unsigned* __restrict__ gmax, int* __restrict__ counters, int32_t* __restrict__ n_out) {
+    const int i = threadIdx.x;
+    if (gmax && i < 16) gmax[i] = 0u;
+    if (i < 16) counters[i] = 0;
+    if (i < 2) n_out[i] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -198,7 +212,11 @@ __global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(3, 
 // in registers (33 per lane), 8-bit digits counted in a per-wave LDS histogram.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, int n_frames,
-                                                 unsigned* __restrict__ colmed) {
+                                                 unsigned* __restrict__ colmed, const unsigned* __restrict__ gmax,
+                                                 float* __restrict__ c3) {
+    // c3[f] = 3 * (colmed[f] / a) in numpy's float32 steps (:656-667); division
+    // is monotone, so the median of S / a is the quotient of S's middle element
+    const float a = __uint_as_float(*gmax);
     // per wave 4 copies of the histogram (lane & 3 picks one): a frame's
     // values crowd a few buckets, and same-address LDS atomics serialise
     __shared__ unsigned hists[4][4][kSnHist];
@@ -231,7 +249,10 @@ __global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, in
         mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
     }
     if (mn == mx) {
-        if (lane == 0) colmed[fi] = mn;
+        if (lane == 0) {
+            colmed[fi] = mn;
+            c3[fi] = __fmul_rn(3.f, __fdiv_rn(__uint_as_float(mn), a));
+        }
         return;
     }
     const int hb = 31 - __clz(mn ^ mx);
@@ -265,7 +286,10 @@ __global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, in
         wave_sync();
         if (shift == 0) break;
     }
-    if (lane == 0) colmed[fi] = prefix;
+    if (lane == 0) {
+        colmed[fi] = prefix;
+        c3[fi] = __fmul_rn(3.f, __fdiv_rn(__uint_as_float(prefix), a));
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -292,7 +316,8 @@ __global__ __launch_bounds__(256) void sn_transpose(const float* __restrict__ S,
 // ---------------------------------------------------------------------------
 // sn_select: numpy median of each row of X ([rows][ld], first n entries,
 // non-negative f32) as bit patterns: lo = element of rank (n - 1) / 2, hi =
-// element of rank n / 2 (equal for odd n).  One block per row.  The row is
+// element of rank n / 2 (equal for odd n); then the row's mask (below).  One
+// block per row.  The row is
 // staged in LDS when it fits (STAGE; otherwise every pass re-reads it from
 // L2).  Radix select on the bit patterns: the bits above the highest bit where
 // the row's min and max differ are common to every element, so the 8-bit
@@ -303,8 +328,9 @@ __global__ __launch_bounds__(256) void sn_transpose(const float* __restrict__ S,
 constexpr int kSnStageMax = 12288;  // values staged in LDS (48 KiB)
 
 template <bool STAGE>
-__global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, int ld, int n, unsigned* __restrict__ lo,
-                                                 unsigned* __restrict__ hi) {
+__global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, int ld, int n,
+                                                 const unsigned* __restrict__ gmax, const float* __restrict__ c3,
+                                                 int words, unsigned long long* __restrict__ M) {
     extern __shared__ unsigned srow[];
     __shared__ unsigned hist[4][kSnHist];
     __shared__ unsigned pick[3];
@@ -328,10 +354,8 @@ __global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, in
     mn = min(min(red[0], red[1]), min(red[2], red[3]));
     mx = max(max(red[4], red[5]), max(red[6], red[7]));
     const unsigned* row = STAGE ? srow : grow;
-    if (mn == mx) {  // block-uniform: a constant row
-        if (tid == 0) { lo[blockIdx.x] = mn; hi[blockIdx.x] = mn; }
-        return;
-    }
+    unsigned rlo = mn, rhi = mn;  // a constant row (block-uniform): its value
+    if (mn != mx) {
     const int hb = 31 - __clz(mn ^ mx);  // highest bit that differs
     unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
     unsigned prefix = mn & pmask, rank = (unsigned)(n - 1) / 2, cnt = 0;
@@ -373,56 +397,26 @@ __global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, in
         __syncthreads();
         second = min(min(red[0], red[1]), min(red[2], red[3]));
     }
-    if (tid == 0) {
-        lo[blockIdx.x] = prefix;
-        hi[blockIdx.x] = second;
+    rlo = prefix;
+    rhi = second;
     }
-}
-
-// ---------------------------------------------------------------------------
-// sn_thresholds: c3[f] = 3 * (colmed[f] / a) per frame and r3[b] = 3 *
-// rowmed_b per bin, in numpy's float32 rounding (:656-667).  Division is
-// monotone, so the medians of S / a are the quotients of S's middle elements;
-// an even count takes numpy's f32 mean of the two middle quotients.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sn_thresholds(const unsigned* __restrict__ gmax,
-                                                     const unsigned* __restrict__ colmed, int n_frames,
-                                                     const unsigned* __restrict__ rlo,
-                                                     const unsigned* __restrict__ rhi, float* __restrict__ c3,
-                                                     float* __restrict__ r3) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    // ---- the row's mask: r3 = 3 * rowmed / a in numpy's float32 steps (an
+    // even count takes the f32 mean of the two middle quotients), then bit
+    // f % 64 of word (b, f / 64) = S[b][f] / a > c3[f] and > r3 (false
+    // throughout when a == 0: NaN quotients, like numpy) ----
     const float a = __uint_as_float(*gmax);
-    if (i < n_frames) c3[i] = __fmul_rn(3.f, __fdiv_rn(__uint_as_float(colmed[i]), a));
-    if (i < kSnBins) {
-        float dr = __fdiv_rn(__uint_as_float(rlo[i]), a);
-        if ((n_frames & 1) == 0) dr = __fmul_rn(__fadd_rn(dr, __fdiv_rn(__uint_as_float(rhi[i]), a)), 0.5f);
-        r3[i] = __fmul_rn(3.f, dr);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// sn_mask: bit f % 64 of word (b, f / 64) = S[b][f] / a > c3[f] and
-// S[b][f] / a > r3[b] (false throughout when a == 0: NaN quotients, like
-// numpy).  One block per bin row, each wave a run of 64-frame words, packed by
-// ballot.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sn_mask(const float* __restrict__ ST, int ldt, int n_frames, int words,
-                                               const unsigned* __restrict__ gmax, const float* __restrict__ c3,
-                                               const float* __restrict__ r3, unsigned long long* __restrict__ M) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int b = blockIdx.x;
-    const float a = __uint_as_float(*gmax);
-    const float rb = r3[b];
-    const float* row = ST + (size_t)b * ldt;
+    float dr = __fdiv_rn(__uint_as_float(rlo), a);
+    if ((n & 1) == 0) dr = __fmul_rn(__fadd_rn(dr, __fdiv_rn(__uint_as_float(rhi), a)), 0.5f);
+    const float rb = __fmul_rn(3.f, dr);
     for (int w = wv; w < words; w += 4) {
         const int f = 64 * w + lane;
         bool bit = false;
-        if (f < n_frames) {
-            const float d = __fdiv_rn(row[f], a);
+        if (f < n) {
+            const float d = __fdiv_rn(__uint_as_float(row[f]), a);
             bit = d > c3[f] && d > rb;
         }
         const unsigned long long m = __ballot(bit);
-        if (lane == 0) M[(size_t)b * words + w] = m;
+        if (lane == 0) M[(size_t)blockIdx.x * words + w] = m;
     }
 }
 
@@ -430,28 +424,41 @@ __global__ __launch_bounds__(256) void sn_mask(const float* __restrict__ ST, int
 // Morphology on the bit image (row = bin, bit = frame).  cv2's erode/dilate
 // with a rectangle of ones and the default anchor (kw / 2, kh / 2): out(x, y)
 // = min / max over the kernel of in(x + i - ax, y + j - ay), taps outside the
-// image ignored.  Separable: sn_morph_h along time (offsets lo..hi, |d| < 64,
-// from the word and its two neighbours), sn_morph_v across bins.
+// image ignored.  Separable, one launch per rectangle: each thread reduces
+// its word and the two neighbouring words over the rows y + vlo .. y + vhi
+// (across bins), then along time over the offsets hlo .. hhi (|d| < 64) of
+// the three reduced words -- the same bits as the horizontal pass followed by
+// the vertical one (both are a min / max over the rectangle's in-image taps).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sn_morph_h(const unsigned long long* __restrict__ src,
-                                                  unsigned long long* __restrict__ dst, int words, int n_frames,
-                                                  int lo, int hi, int erode) {
+__global__ __launch_bounds__(256) void sn_morph(const unsigned long long* __restrict__ src,
+                                                unsigned long long* __restrict__ dst, int rows, int words, int n_frames,
+                                                int vlo, int vhi, int hlo, int hhi, int erode) {
     const int w = blockIdx.x * 256 + threadIdx.x;
     const int y = blockIdx.y;
     if (w >= words) return;
     const unsigned long long ident = erode ? ~0ull : 0ull;
-    const unsigned long long* r = src + (size_t)y * words;
-    auto word = [&](int i) -> unsigned long long {  // bits past the image read as the identity
+    // vertical: rows y + vlo .. y + vhi inside the image, words w - 1 .. w + 1
+    unsigned long long vm = ident, v0 = ident, vp = ident;
+    const int y0 = max(0, y + vlo), y1 = min(rows - 1, y + vhi);
+    for (int yy = y0; yy <= y1; ++yy) {
+        const unsigned long long* r = src + (size_t)yy * words;
+        const unsigned long long a = w > 0 ? r[w - 1] : ident, b = r[w], c = w + 1 < words ? r[w + 1] : ident;
+        if (erode) { vm &= a; v0 &= b; vp &= c; }
+        else { vm |= a; v0 |= b; vp |= c; }
+    }
+    // bits past the image read as the identity (a frame position outside the
+    // image is the identity in every row, so this commutes with the vertical pass)
+    auto fix = [&](unsigned long long v, int i) -> unsigned long long {
         if (i < 0 || i >= words) return ident;
-        const unsigned long long v = r[i];
         const int valid = n_frames - 64 * i;
         if (valid >= 64) return v;
         const unsigned long long keep = (1ull << valid) - 1;
         return (v & keep) | (ident & ~keep);
     };
-    const unsigned long long wm = word(w - 1), w0 = word(w), wp = word(w + 1);
+    const unsigned long long wm = fix(vm, w - 1), w0 = fix(v0, w), wp = fix(vp, w + 1);
+    // horizontal: offsets hlo .. hhi (|d| < 64) from the word and its neighbours
     unsigned long long acc = ident;
-    for (int d = lo; d <= hi; ++d) {
+    for (int d = hlo; d <= hhi; ++d) {
         unsigned long long s;  // bit i = in(64 w + i + d)
         if (d == 0) s = w0;
         else if (d > 0) s = (w0 >> d) | (wp << (64 - d));
@@ -460,21 +467,6 @@ __global__ __launch_bounds__(256) void sn_morph_h(const unsigned long long* __re
     }
     const int valid = n_frames - 64 * w;
     if (valid < 64) acc &= (1ull << valid) - 1;
-    dst[(size_t)y * words + w] = acc;
-}
-
-__global__ __launch_bounds__(256) void sn_morph_v(const unsigned long long* __restrict__ src,
-                                                  unsigned long long* __restrict__ dst, int rows, int words, int lo,
-                                                  int hi, int erode) {
-    const int w = blockIdx.x * 256 + threadIdx.x;
-    const int y = blockIdx.y;
-    if (w >= words) return;
-    unsigned long long acc = erode ? ~0ull : 0ull;
-    const int y0 = max(0, y + lo), y1 = min(rows - 1, y + hi);
-    for (int yy = y0; yy <= y1; ++yy) {
-        const unsigned long long v = src[(size_t)yy * words + w];
-        acc = erode ? (acc & v) : (acc | v);
-    }
     dst[(size_t)y * words + w] = acc;
 }
 
@@ -545,6 +537,7 @@ __global__ __launch_bounds__(256) void sn_runs(const unsigned long long* __restr
     base = __shfl(base, 0, 64);
     if (base + total > max_runs) {  // cannot happen within the host's bound; flagged, row dropped
         if (lane == 0) atomicOr(counters + 1, AA_SN_RUN_OVERFLOW);
+        for (int i = base + lane; i < min(base + total, max_runs); i += 64) R[(size_t)R_Y * max_runs + i] = -1;
         total = 0;
     }
     if (lane == 0) {
@@ -589,12 +582,12 @@ __global__ __launch_bounds__(256) void sn_runs(const unsigned long long* __restr
 __global__ __launch_bounds__(256) void sn_unite(int* __restrict__ R, int max_runs, const int* __restrict__ row_off,
                                                 const int* __restrict__ row_cnt, const int* __restrict__ counters,
                                                 int rows) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= min(counters[0], max_runs)) return;
+    const int nr = min(counters[0], max_runs);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < nr; i += gridDim.x * 256) {
     const int* X0 = R + (size_t)R_X0 * max_runs;
     const int* X1 = R + (size_t)R_X1 * max_runs;
     const int y = R[(size_t)R_Y * max_runs + i];
-    if (y <= 0 || y >= rows) return;  // row 0, or a slot of a dropped row (y = -1)
+    if (y <= 0 || y >= rows) continue;  // row 0, or a slot of a dropped row (y = -1)
     int* P = R + (size_t)R_P * max_runs;
     const int a = X0[i] - 1, b = X1[i] + 1;  // 8-connectivity: diagonal neighbours touch
     const int first = row_off[y - 1], end = first + row_cnt[y - 1];
@@ -605,14 +598,15 @@ __global__ __launch_bounds__(256) void sn_unite(int* __restrict__ R, int max_run
         else hi = m;
     }
     for (int j = lo; j < end && X0[j] <= b; ++j) uf_union(P, i, j);
+    }
 }
 
 __global__ __launch_bounds__(256) void sn_stats(int* __restrict__ R, int max_runs, int kx,
                                                 const int* __restrict__ counters) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= min(counters[0], max_runs)) return;
+    const int nr = min(counters[0], max_runs);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < nr; i += gridDim.x * 256) {
     const int y = R[(size_t)R_Y * max_runs + i];
-    if (y < 0) return;
+    if (y < 0) continue;
     const int root = uf_find(R + (size_t)R_P * max_runs, i);
     const int x0 = R[(size_t)R_X0 * max_runs + i], x1 = R[(size_t)R_X1 * max_runs + i];
     atomicMin(R + (size_t)R_LEFT * max_runs + root, x0);
@@ -621,24 +615,25 @@ __global__ __launch_bounds__(256) void sn_stats(int* __restrict__ R, int max_run
     atomicMax(R + (size_t)R_BOT * max_runs + root, y);
     atomicAdd(R + (size_t)R_AREA * max_runs + root, x1 - x0 + 1);
     atomicMin(R + (size_t)R_KEY * max_runs + root, (y >> 1) * kx + (x0 >> 1));
+    }
 }
 
 __global__ __launch_bounds__(256) void sn_emit(const int* __restrict__ R, int max_runs, int wmin, int hmin,
                                                const int* __restrict__ counters, const unsigned* __restrict__ gmax,
                                                aa_sn_component* __restrict__ out, int max_out,
                                                int32_t* __restrict__ n_out) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         int st = counters[1];
         if (gmax && (*gmax & 0x7FFFFFFFu) >= 0x7F800000u) st |= AA_SN_NONFINITE;
         n_out[1] = st;
     }
-    if (i >= min(counters[0], max_runs)) return;
-    if (R[(size_t)R_Y * max_runs + i] < 0 || R[(size_t)R_P * max_runs + i] != i) return;
+    const int nr = min(counters[0], max_runs);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < nr; i += gridDim.x * 256) {
+    if (R[(size_t)R_Y * max_runs + i] < 0 || R[(size_t)R_P * max_runs + i] != i) continue;
     const int left = R[(size_t)R_LEFT * max_runs + i], top = R[(size_t)R_TOP * max_runs + i];
     const int w = R[(size_t)R_RIGHT * max_runs + i] - left + 1;
     const int hgt = R[(size_t)R_BOT * max_runs + i] - top + 1;
-    if (w < wmin || hgt < hmin) return;
+    if (w < wmin || hgt < hmin) continue;
     const int k = atomicAdd(n_out, 1);
     if (k < max_out) {
         aa_sn_component c;
@@ -650,6 +645,7 @@ __global__ __launch_bounds__(256) void sn_emit(const int* __restrict__ R, int ma
         c.order = R[(size_t)R_KEY * max_runs + i];
         out[k] = c;
     }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -659,10 +655,7 @@ struct SnWs {
     float* S;
     float* ST;
     unsigned* colmed;
-    unsigned* rlo;
-    unsigned* rhi;
     float* c3;
-    float* r3;
     unsigned* gmax;
     int* counters;  // [0] runs allocated, [1] status flags
     unsigned long long* M0;
@@ -696,10 +689,7 @@ static SnWs sn_ws_layout(const SnPlan& p, int F, char* base) {
     w.S = reinterpret_cast<float*>(take(sizeof(float) * (size_t)F * kSnLd));
     w.ST = reinterpret_cast<float*>(take(sizeof(float) * (size_t)kSnBins * ldt));
     w.colmed = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * (size_t)F));
-    w.rlo = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * kSnBins));
-    w.rhi = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * kSnBins));
     w.c3 = reinterpret_cast<float*>(take(sizeof(float) * (size_t)F));
-    w.r3 = reinterpret_cast<float*>(take(sizeof(float) * kSnBins));
     w.gmax = reinterpret_cast<unsigned*>(take(64));
     w.counters = reinterpret_cast<int*>(take(64));
     w.M0 = reinterpret_cast<unsigned long long*>(take(8 * (size_t)kSnBins * words));
@@ -720,31 +710,25 @@ static int sn_components(const SnPlan& p, const SnWs& ws, int F, const unsigned*
     const dim3 gm((words + 255) / 256, kSnBins);
     unsigned long long* a = ws.M0;
     unsigned long long* b = ws.M1;
-    auto horiz = [&](int kw, int erode) -> int {
-        const int ax = kw / 2;
-        hipLaunchKernelGGL(sn_morph_h, gm, dim3(256), 0, st, a, b, words, F, -ax, kw - 1 - ax, erode);
-        AA_LAUNCH_CHECK();
-        std::swap(a, b);
-        return AA_OK;
-    };
-    auto vert = [&](int kh, int erode) -> int {
-        const int ay = kh / 2;
-        hipLaunchKernelGGL(sn_morph_v, gm, dim3(256), 0, st, a, b, kSnBins, words, -ay, kh - 1 - ay, erode);
+    // one launch per structuring element: rectangle kh x kw, anchor (kw / 2, kh / 2)
+    auto morph = [&](int kh, int kw, int erode) -> int {
+        const int ax = kw / 2, ay = kh / 2;
+        hipLaunchKernelGGL(sn_morph, gm, dim3(256), 0, st, a, b, kSnBins, words, F, -ay, kh - 1 - ay, -ax, kw - 1 - ax,
+                           erode);
         AA_LAUNCH_CHECK();
         std::swap(a, b);
         return AA_OK;
     };
     int rc = AA_OK;
-    // MORPH_OPEN with ones(4, 4): erode, then dilate
-    if ((rc = horiz(4, 1)) || (rc = vert(4, 1)) || (rc = horiz(4, 0)) || (rc = vert(4, 0))) return rc;
-    if ((rc = horiz(p.kw_d, 0)) || (rc = vert(p.kh_d, 0))) return rc;
-    if ((rc = horiz(p.kw_e, 1)) || (rc = vert(p.kh_e, 1))) return rc;
-    AA_HIP(hipMemsetAsync(ws.counters, 0, 64, st));
-    AA_HIP(hipMemsetAsync(ws.R + (size_t)R_Y * ws.max_runs, 0xFF, sizeof(int) * (size_t)ws.max_runs, st));
+    // MORPH_OPEN with ones(4, 4): erode, then dilate; dilate; erode
+    if ((rc = morph(4, 4, 1)) || (rc = morph(4, 4, 0))) return rc;
+    if ((rc = morph(p.kh_d, p.kw_d, 0)) || (rc = morph(p.kh_e, p.kw_e, 1))) return rc;
+    // (counters were zeroed by sn_zero; sn_runs marks the slots of a dropped row)
     hipLaunchKernelGGL(sn_runs, dim3((kSnBins + 3) / 4), dim3(256), 0, st, a, kSnBins, words, ws.R, ws.max_runs,
                        ws.row_off, ws.row_cnt, ws.counters);
     AA_LAUNCH_CHECK();
-    const int gr = (ws.max_runs + 255) / 256;
+    // grid-stride over the runs actually allocated (counters[0] of max_runs)
+    const int gr = std::min((ws.max_runs + 255) / 256, 512);
     hipLaunchKernelGGL(sn_unite, dim3(gr), dim3(256), 0, st, ws.R, ws.max_runs, ws.row_off, ws.row_cnt, ws.counters,
                        kSnBins);
     AA_LAUNCH_CHECK();
@@ -866,8 +850,8 @@ extern "C" int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* 
     AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE, "aa_sn_run: workspace %zu < %zu bytes",
              workspace_bytes, ws.bytes);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    AA_HIP(hipMemsetAsync(ws.gmax, 0, 64, st));
-    AA_HIP(hipMemsetAsync(n_out, 0, 2 * sizeof(int32_t), st));
+    hipLaunchKernelGGL(sn_zero, dim3(1), dim3(64), 0, st, ws.gmax, ws.counters, n_out);
+    AA_LAUNCH_CHECK();
     const size_t lds = sizeof(float2) * kSnWpb * kHalf;
     static bool attr_set = false;
     if (!attr_set) {
@@ -879,21 +863,17 @@ extern "C" int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* 
     hipLaunchKernelGGL(sn_stft, dim3(grid), dim3(64 * kSnWpb), lds, st, pcm, (int)n_samples, p->cfg.hop_length, F,
                        p->d_tw, p->d_tw4096, ws.S, ws.gmax);
     AA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sn_colmed, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, F, ws.colmed);
+    hipLaunchKernelGGL(sn_colmed, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, F, ws.colmed, ws.gmax, ws.c3);
     AA_LAUNCH_CHECK();
     const int words = (F + 63) / 64, ldt = words * 64;
     hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST);
     AA_LAUNCH_CHECK();
     if (F <= kSnStageMax)
-        hipLaunchKernelGGL(sn_select<true>, dim3(kSnBins), dim3(256), sizeof(unsigned) * F, st, ws.ST, ldt, F, ws.rlo,
-                           ws.rhi);
+        hipLaunchKernelGGL(sn_select<true>, dim3(kSnBins), dim3(256), sizeof(unsigned) * F, st, ws.ST, ldt, F, ws.gmax,
+                           ws.c3, words, ws.M0);
     else
-        hipLaunchKernelGGL(sn_select<false>, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, ws.rlo, ws.rhi);
-    AA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sn_thresholds, dim3((std::max(F, kSnBins) + 255) / 256), dim3(256), 0, st, ws.gmax, ws.colmed, F,
-                       ws.rlo, ws.rhi, ws.c3, ws.r3);
-    AA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sn_mask, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, words, ws.gmax, ws.c3, ws.r3, ws.M0);
+        hipLaunchKernelGGL(sn_select<false>, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, ws.gmax, ws.c3, words,
+                           ws.M0);
     AA_LAUNCH_CHECK();
     if (mask_out)
         AA_HIP(hipMemcpyAsync(mask_out, ws.M0, 8 * (size_t)kSnBins * words, hipMemcpyDeviceToDevice, st));
@@ -912,7 +892,8 @@ extern "C" int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int6
     AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE,
              "aa_sn_components_from_mask: workspace %zu < %zu bytes", workspace_bytes, ws.bytes);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    AA_HIP(hipMemsetAsync(n_out, 0, 2 * sizeof(int32_t), st));
+    hipLaunchKernelGGL(sn_zero, dim3(1), dim3(64), 0, st, nullptr, ws.counters, n_out);
+    AA_LAUNCH_CHECK();
     AA_HIP(hipMemcpyAsync(ws.M0, mask, 8 * (size_t)kSnBins * ((F + 63) / 64), hipMemcpyDeviceToDevice, st));
     return sn_components(*p, ws, F, nullptr, out, max_out, n_out, st);
 }

@@ -82,7 +82,7 @@ def parse(argv=None):
                          "4: a corpus of 60 s WAV files through the whole analyse path (configs[3])")
     ap.add_argument("--clips", type=int, default=1000, help="--config 3: clips per rank")
     ap.add_argument("--files", type=int, default=32, help="--config 4: files per rank")
-    ap.add_argument("--batch", type=int, default=16,
+    ap.add_argument("--batch", type=int, default=32,
                     help="--config 4: recordings per device pass (aa_amd.batch); 0 = one file at a time")
     return ap.parse_args(argv)
 
