@@ -2,18 +2,18 @@
 // (reference src/identify_tracks.py:650-706), run on every recording (:420).
 //
 // Launches (one stream, no host synchronisation inside aa_sn_run):
+//   sn_zero       the per-run counters (global max, run count, status) = 0
 //   sn_stft       |STFT| of the recording (n_fft 4096, centre zero padding,
 //                 periodic Hann), one wave per frame through the front end's
 //                 wave FFT (aa_wavefft.h).  The real split yields every bin:
 //                 the lane holding Z[k] and its mirror Z[2048 - k] forms
 //                 X[k] = E + W^k O and X[2048 - k] = conj(E - W^k O).  Writes
-//                 the frame-major magnitude S[f][0..2048] and the maximum.
-//   sn_zero       the per-run counters (global max, run count, status) = 0
-//   sn_colmed     the frame's median over bins: radix select on the f32 bit
-//                 patterns of the S row, values in registers, digits below the
-//                 row's common min/max prefix, 4 LDS histograms per wave; and
-//                 the frame's threshold c3 = 3 (colmed / a) (numpy's f32 steps)
-//   sn_transpose  S -> ST[bin][frame] (64 x 64 tiles through LDS)
+//                 the frame-major magnitude S[f][0..2048] and the maximum,
+//                 and the frame's median over bins: radix select on the f32
+//                 bit patterns of the row still in registers, digits below the
+//                 row's common min/max prefix, 4 LDS histograms per wave
+//   sn_transpose  S -> ST[bin][frame] (64 x 64 tiles through LDS), and the
+//                 frame thresholds c3 = 3 (colmed / a) (numpy's f32 steps)
 //   sn_select     per-bin median over frames: radix select over the ST row
 //                 (staged in LDS), both middle elements for an even count;
 //                 then the row's threshold r3 = 3 rowmed / a and its mask bits
@@ -101,6 +101,69 @@ __global__ void sn_zero(unsigned* __restrict__ gmax, int* __restrict__ counters,
 }
 
 // ---------------------------------------------------------------------------
+// The median over bins of one frame (numpy, odd count 2049: the middle
+// element) by radix select on the bit patterns, by the wave that holds the
+// frame: v[i] = bin lane + 64 i (i < 32), v[32] = bin 2048 (lane 0 only).
+// 8-bit digits start below the bits the frame's min and max share (a
+// spectrum spans a few binades: the first histogram then spreads over the
+// exponents present instead of piling onto a handful of counters), counted
+// in 4 LDS histogram copies (lane & 3 picks one: a frame's values crowd a
+// few buckets, and same-address LDS atomics serialise).  hists: the wave's
+// 4 x 256 unsigned.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned wave_median_2049(const unsigned (&v)[33], unsigned* hists, int lane) {
+    unsigned* myh = hists + (lane & 3) * kSnHist;
+    unsigned mn = v[0], mx = v[0];
+#pragma unroll
+    for (int i = 1; i < 32; ++i) {
+        mn = min(mn, v[i]);
+        mx = max(mx, v[i]);
+    }
+    if (lane == 0) {
+        mn = min(mn, v[32]);
+        mx = max(mx, v[32]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if (mn == mx) return mn;
+    const int hb = 31 - __clz(mn ^ mx);
+    unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
+    unsigned prefix = mn & pmask, rank = kSnBins / 2;
+#pragma unroll 1
+    for (int sh = hb - 7;; sh -= 8) {
+        const int shift = max(sh, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(hists + q * kSnHist)[lane] = make_uint4(0u, 0u, 0u, 0u);
+        wave_sync();
+#pragma unroll
+        for (int i = 0; i < 33; ++i)
+            if ((i < 32 || lane == 0) && (v[i] & pmask) == prefix) atomicAdd(&myh[(v[i] >> shift) & 255u], 1u);
+        wave_sync();
+        {  // fold the copies into copy 0 (lane owns buckets 4 lane .. 4 lane + 3)
+            uint4 t = reinterpret_cast<uint4*>(hists)[lane];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                const uint4 u = reinterpret_cast<uint4*>(hists + q * kSnHist)[lane];
+                t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+            }
+            reinterpret_cast<uint4*>(hists)[lane] = t;
+        }
+        wave_sync();
+        unsigned below, cnt;
+        const unsigned dig = hist_pick(hists, rank, lane, &below, &cnt);
+        prefix = (prefix & ~(255u << shift)) | (dig << shift);
+        pmask |= 255u << shift;
+        rank -= below;
+        wave_sync();
+        if (shift == 0) break;
+    }
+    return prefix;
+}
+
+// ---------------------------------------------------------------------------
 // sn_stft: one wave per frame, persistent over frames (XCD-contiguous ranges
 // of frames like fe_stft_mel_4096: neighbouring frames share 4096 - hop
 // samples through one L2).  Register budget 168 (3 waves per SIMD): the wave
@@ -109,7 +172,8 @@ __global__ void sn_zero(unsigned* __restrict__ gmax, int* __restrict__ counters,
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(3, 3))) void sn_stft(
     const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const float2* __restrict__ tw,
-    const float2* __restrict__ tw4096, float* __restrict__ S, unsigned* __restrict__ gmax) {
+    const float2* __restrict__ tw4096, float* __restrict__ S, unsigned* __restrict__ gmax,
+    unsigned* __restrict__ colmed) {
     extern __shared__ float lds[];
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -199,6 +263,11 @@ __global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(3, 
 #pragma unroll
         for (int i = 0; i < 32; ++i) wmax = max(wmax, v[i]);
         wmax = max(wmax, v[32]);
+        // ---- the frame's median over bins, from the registers the row
+        // came from (the wave's buffer, read above, holds the histograms) ----
+        wave_sync();
+        const unsigned med = wave_median_2049(v, reinterpret_cast<unsigned*>(wb), lane);
+        if (lane == 0) colmed[fi] = med;
         wave_sync();  // the buffer is rewritten by the next frame
     }
 #pragma unroll
@@ -207,99 +276,19 @@ __global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(3, 
 }
 
 // ---------------------------------------------------------------------------
-// sn_colmed: the median over bins of every frame (numpy, odd count 2049: the
-// middle element) by radix select, one wave per S row: the row's 2049 values
-// in registers (33 per lane), 8-bit digits counted in a per-wave LDS histogram.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, int n_frames,
-                                                 unsigned* __restrict__ colmed, const unsigned* __restrict__ gmax,
-                                                 float* __restrict__ c3) {
-    // c3[f] = 3 * (colmed[f] / a) in numpy's float32 steps (:656-667); division
-    // is monotone, so the median of S / a is the quotient of S's middle element
-    const float a = __uint_as_float(*gmax);
-    // per wave 4 copies of the histogram (lane & 3 picks one): a frame's
-    // values crowd a few buckets, and same-address LDS atomics serialise
-    __shared__ unsigned hists[4][4][kSnHist];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int fi = blockIdx.x * 4 + wv;
-    if (fi >= n_frames) return;  // wave-uniform
-    unsigned* hist = hists[wv][0];
-    unsigned* myh = hists[wv][lane & 3];
-    const unsigned* row = reinterpret_cast<const unsigned*>(S) + (size_t)fi * kSnLd;
-    unsigned v[33];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) v[i] = row[lane + 64 * i];
-    v[32] = row[2048];  // counted by lane 0 only
-    // digits start below the bits the row's min and max share (a spectrum
-    // spans a few binades: the first histogram then spreads over the exponents
-    // present instead of piling onto a handful of counters)
-    unsigned mn = v[0], mx = v[0];
-#pragma unroll
-    for (int i = 1; i < 32; ++i) {
-        mn = min(mn, v[i]);
-        mx = max(mx, v[i]);
-    }
-    if (lane == 0) {
-        mn = min(mn, v[32]);
-        mx = max(mx, v[32]);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
-        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
-    }
-    if (mn == mx) {
-        if (lane == 0) {
-            colmed[fi] = mn;
-            c3[fi] = __fmul_rn(3.f, __fdiv_rn(__uint_as_float(mn), a));
-        }
-        return;
-    }
-    const int hb = 31 - __clz(mn ^ mx);
-    unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
-    unsigned prefix = mn & pmask, rank = kSnBins / 2;
-#pragma unroll 1
-    for (int sh = hb - 7;; sh -= 8) {
-        const int shift = max(sh, 0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(hists[wv][q])[lane] = make_uint4(0u, 0u, 0u, 0u);
-        wave_sync();
-#pragma unroll
-        for (int i = 0; i < 33; ++i)
-            if ((i < 32 || lane == 0) && (v[i] & pmask) == prefix) atomicAdd(&myh[(v[i] >> shift) & 255u], 1u);
-        wave_sync();
-        {  // fold the copies into copy 0 (lane owns buckets 4 lane .. 4 lane + 3)
-            uint4 t = reinterpret_cast<uint4*>(hists[wv][0])[lane];
-#pragma unroll
-            for (int q = 1; q < 4; ++q) {
-                const uint4 u = reinterpret_cast<uint4*>(hists[wv][q])[lane];
-                t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
-            }
-            reinterpret_cast<uint4*>(hist)[lane] = t;
-        }
-        wave_sync();
-        unsigned below, cnt;
-        const unsigned dig = hist_pick(hist, rank, lane, &below, &cnt);
-        prefix = (prefix & ~(255u << shift)) | (dig << shift);
-        pmask |= 255u << shift;
-        rank -= below;
-        wave_sync();
-        if (shift == 0) break;
-    }
-    if (lane == 0) {
-        colmed[fi] = prefix;
-        c3[fi] = __fmul_rn(3.f, __fdiv_rn(__uint_as_float(prefix), a));
-    }
-}
-
-// ---------------------------------------------------------------------------
 // sn_transpose: S[f][b] (stride kSnLd) -> ST[b][f] (stride ldt)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void sn_transpose(const float* __restrict__ S, int n_frames, int ldt,
-                                                    float* __restrict__ ST) {
+                                                    float* __restrict__ ST, const unsigned* __restrict__ gmax,
+                                                    const unsigned* __restrict__ colmed, float* __restrict__ c3) {
     __shared__ float tile[64][65];
     const int b0 = blockIdx.x * 64, f0 = blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    // the first bin tile also forms its frames' thresholds c3 = 3 * (colmed /
+    // a) in numpy's float32 steps (:656-667); division is monotone, so the
+    // median of S / a is the quotient of S's middle element
+    if (blockIdx.x == 0 && ty == 0 && f0 + tx < n_frames)
+        c3[f0 + tx] = __fmul_rn(3.f, __fdiv_rn(__uint_as_float(colmed[f0 + tx]), __uint_as_float(*gmax)));
 #pragma unroll 4
     for (int r = ty; r < 64; r += 4) {
         const int f = f0 + r, b = b0 + tx;
@@ -861,12 +850,11 @@ extern "C" int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* 
     int grid = std::min((F + kSnWpb - 1) / kSnWpb, 256 * 3);  // persistent: 3 blocks per CU
     grid = (grid + 7) & ~7;
     hipLaunchKernelGGL(sn_stft, dim3(grid), dim3(64 * kSnWpb), lds, st, pcm, (int)n_samples, p->cfg.hop_length, F,
-                       p->d_tw, p->d_tw4096, ws.S, ws.gmax);
-    AA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sn_colmed, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, F, ws.colmed, ws.gmax, ws.c3);
+                       p->d_tw, p->d_tw4096, ws.S, ws.gmax, ws.colmed);
     AA_LAUNCH_CHECK();
     const int words = (F + 63) / 64, ldt = words * 64;
-    hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST);
+    hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST, ws.gmax,
+                       ws.colmed, ws.c3);
     AA_LAUNCH_CHECK();
     if (F <= kSnStageMax)
         hipLaunchKernelGGL(sn_select<true>, dim3(kSnBins), dim3(256), sizeof(unsigned) * F, st, ws.ST, ldt, F, ws.gmax,

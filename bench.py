@@ -84,6 +84,10 @@ def parse(argv=None):
     ap.add_argument("--files", type=int, default=32, help="--config 4: files per rank")
     ap.add_argument("--batch", type=int, default=32,
                     help="--config 4: recordings per device pass (aa_amd.batch); 0 = one file at a time")
+    ap.add_argument("--procs-per-gpu", type=int, default=1,
+                    help="--config 4: host processes feeding each GPU (the host steps the reference runs in "
+                         "Python -- decode, tracks, JSON -- scale with processes, not threads); ranks sharing "
+                         "a GPU gather over gloo")
     return ap.parse_args(argv)
 
 
@@ -490,24 +494,27 @@ def main_corpus(args, world, rank, dev):
     with ProcessPoolExecutor(max_workers=min(16, len(mine)), mp_context=mpc.get_context("spawn")) as ex:
         list(ex.map(_write_clip, [str(files[i]) for i in mine], [5000 + i for i in mine]))
     models = [str(model)]
+    ppg = max(1, args.procs_per_gpu)
+    cdev = dev if (world > 1 and dist.get_backend() == "nccl") else torch.device("cpu")  # collectives
+    n_gpus = max(1, world // ppg)
     # warm-up (untimed): plans, kernels, model upload, the pinned staging slots
     corpus.run([files[0]] * (4 * max(args.batch, 1)), models, rank=0, world=1, batch=args.batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    res = corpus.run(files, models, rank=rank, world=world, device=dev if world > 1 else None, batch=args.batch)
+    res = corpus.run(files, models, rank=rank, world=world, device=cdev if world > 1 else None, batch=args.batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     assert len(res) == n * world
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     n_pred = sum(len(r.get("species_identify", [])) for r in res.values())
-    out = {"metric": METRIC, "value": round(n * world * 60.0 / elapsed, 1), "unit": "audio-s/s", "n_gpus": world,
+    out = {"metric": METRIC, "value": round(n * world * 60.0 / elapsed, 1), "unit": "audio-s/s", "n_gpus": n_gpus,
            "steps": n, "warmup": 1, "ms_per_step": round(1e3 * elapsed / n, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "bf16x3",
            "data": "synthetic 60 s 48 kHz int16 WAV files (noise+chirps, seeded), seeded random-init model1",
@@ -515,7 +522,8 @@ def main_corpus(args, world, rank, dev):
                                   "signal_noise, tracks, classify, species JSON), files sharded over ranks, K per device pass, "
                                   "JSON all-gathered", "model": "model1", "global_batch": world * max(args.batch, 1),
                       "files_per_device_pass": max(args.batch, 1),
-                      "seq_len": 48000 * 60, "parallelism": f"dp{world}", "files_per_rank": n,
+                      "seq_len": 48000 * 60, "parallelism": f"dp{n_gpus}", "host_procs_per_gpu": ppg,
+                      "files_per_rank": n,
                       "documents_gathered": len(res), "tracks_classified": n_pred}}
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -527,10 +535,15 @@ def worker(local, world, args, port=None):
         os.environ.update(RANK=str(local), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     rank = int(os.environ.get("RANK", "0"))
+    ppg = max(1, args.procs_per_gpu) if args.config == 4 else 1
+    gpu = local // ppg
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if ppg > 1:  # ranks sharing a GPU: RCCL needs one rank per device
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     from aa_amd import _lib
     _lib.lib()  # fails loudly without the HIP library
     try:
@@ -555,10 +568,11 @@ def main(argv=None):
     args = parse(argv)
     if "WORLD_SIZE" in os.environ:  # torchrun: one process per GPU already
         worker(int(os.environ.get("LOCAL_RANK", "0")), int(os.environ["WORLD_SIZE"]), args)
-    elif args.gpus > 1:
+    elif args.gpus > 1 or (args.config == 4 and args.procs_per_gpu > 1):
         # spawn the ranks before this process touches the GPU
         import torch.multiprocessing as mp
-        mp.spawn(worker, args=(args.gpus, args, _free_port()), nprocs=args.gpus, join=True)
+        n = args.gpus * (max(1, args.procs_per_gpu) if args.config == 4 else 1)
+        mp.spawn(worker, args=(n, args, _free_port()), nprocs=n, join=True)
     else:
         worker(0, 1, args)
 
