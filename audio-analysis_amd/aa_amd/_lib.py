@@ -148,6 +148,10 @@ _SIGS = {
     "aa_sn_geometry": (C.c_int, [C.POINTER(SnConfig), C.POINTER(C.c_int32)]),
     "aa_sn_n_frames": (C.c_int64, [C.c_void_p, C.c_int64]),
     "aa_sn_workspace_bytes": (C.c_size_t, [C.c_void_p, C.c_int64]),
+    "aa_sn_batch_workspace_bytes": (C.c_size_t, [C.c_void_p, C.c_int64, C.c_int32]),
+    "aa_sn_run_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_int32,
+                                  C.c_void_p, C.c_size_t, C.c_void_p, C.c_int32, C.c_int64, C.c_void_p, C.c_int32,
+                                  C.c_void_p]),
     "aa_sn_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.c_void_p,
                             C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "aa_sn_components_from_mask": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t,
@@ -167,7 +171,12 @@ def lib():
             raise AAError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc gfx950)")
         h = C.CDLL(str(LIB_PATH))
         for name, (res, args) in _SIGS.items():
-            f = getattr(h, name)
+            try:
+                f = getattr(h, name)
+            except AttributeError:
+                if os.environ.get("AA_LIB"):
+                    continue  # an older A/B build (tools/ab_head.py) lacks newer entry points
+                raise
             f.restype = res
             f.argtypes = args
         v = h.aa_abi_version()

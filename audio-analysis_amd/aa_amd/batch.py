@@ -15,8 +15,10 @@ K at a time:
     device exactly as the host decode would;
   * get_end: one ``aa_span_nonzero`` launch over every file's chunk spans,
     one readback;
-  * signal_noise: one ``aa_sn_run`` per file back to back into per-file
-    result slots, one readback of the counts and component rows;
+  * signal_noise: ``aa_sn_run_batch`` -- per file the STFT / medians / mask
+    launches back to back, then one morphology + components pass for the
+    whole batch -- into per-file result slots, one readback of the counts and
+    component rows;
   * tracks: host, per file (as the reference);
   * classify: ``Classifier.classify_batch`` -- one front-end launch set over
     every file's windows, one forward per model, one track mean, one copy;
@@ -308,9 +310,11 @@ class BatchAnalyser:
 
     def _signal_noise(self, lane, pcm, recs):
         """signal_noise (src/identify_tracks.py:650-706) of every recording:
-        back-to-back aa_sn_run launches into per-recording slots
-        [1 + SN_CAP][6] int32 (row 0: count, status), one readback of every
-        slot's head."""
+        aa_sn_run_batch over up to 64 recordings at a time (per recording the
+        STFT / medians / mask launches, then one morphology + components pass
+        for all of them) into per-recording slots [1 + SN_CAP][6] int32 (row 0:
+        count, status), one readback of every slot's head."""
+        import ctypes as C
         from .identify_tracks import Signal
         from .signals import detector
         by_sr = {}
@@ -320,17 +324,20 @@ class BatchAnalyser:
         for sr, ks in by_sr.items():
             det = detector(sr, 281, self.dev)
             nsig = [int(sr * recs[k].length) for k in ks]
-            need = L.aa_sn_workspace_bytes(det._h, max(nsig))
+            K = min(len(ks), 64)
+            need = L.aa_sn_batch_workspace_bytes(det._h, max(nsig), K)
             if lane.sn_ws is None or lane.sn_ws.numel() < need:
                 lane.sn_ws = torch.empty(need, dtype=torch.uint8, device=self.dev)
             if lane.sn_buf is None or lane.sn_buf.shape[0] < len(ks):
                 lane.sn_buf = torch.empty((len(ks), 1 + SN_CAP, 6), dtype=torch.int32, device=self.dev)
             buf, ws = lane.sn_buf, lane.sn_ws
-            for j, k in enumerate(ks):
-                r = recs[k]
-                _lib.check(L.aa_sn_run(det._h, _lib.dptr(pcm) + 4 * r.off if nsig[j] else 0, nsig[j], _lib.dptr(ws),
-                                       ws.numel(), _lib.dptr(buf[j, 1:]), SN_CAP, _lib.dptr(buf[j, 0]), 0,
-                                       _lib.stream_ptr()), "aa_sn_run")
+            for c0 in range(0, len(ks), 64):
+                part = ks[c0:c0 + 64]
+                offs = (C.c_int64 * len(part))(*[recs[k].off if nsig[c0 + j] else 0 for j, k in enumerate(part)])
+                lens = (C.c_int64 * len(part))(*nsig[c0:c0 + len(part)])
+                _lib.check(L.aa_sn_run_batch(det._h, _lib.dptr(pcm), offs, lens, len(part), _lib.dptr(ws), ws.numel(),
+                                             _lib.dptr(buf[c0, 1:]), SN_CAP, 1 + SN_CAP, _lib.dptr(buf[c0, 0]),
+                                             (1 + SN_CAP) * 6, _lib.stream_ptr()), "aa_sn_run_batch")
             head = buf[:len(ks), :1 + SN_HEAD].cpu().numpy()
             for j, k in enumerate(ks):
                 c, status = int(head[j, 0, 0]), int(head[j, 0, 1])

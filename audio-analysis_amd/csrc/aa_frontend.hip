@@ -754,6 +754,15 @@ __global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melF, con
     const int w = blockIdx.y;
     const int t0 = blockIdx.x * tile_t;
     const int nt = min(tile_t, T - t0);
+    const int ld = n_mels + 1;
+    const float* src = melF + ((size_t)w * T + t0) * n_mels;  // nt contiguous frame rows
+    const int total = nt * n_mels;
+    constexpr int U = 8;  // loads in flight per thread before any is consumed
+    // the first batch of rows is issued before the window's reference max
+    // (independent loads: their latencies overlap instead of adding up)
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[min(u * 256 + (int)threadIdx.x, total - 1)];
     const float ref_db = window_ref_db(pmax + (size_t)w * nparts, nparts, amin, red);
     if (blockIdx.x == 0 && threadIdx.x == 0 && status) {
         float lo = INFINITY, hi = -INFINITY;
@@ -768,14 +777,11 @@ __global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melF, con
         if (normalize && !(hi - lo > 0.f)) bad = 1;
         status[w] = bad ? AA_WIN_NONFINITE : AA_WIN_OK;
     }
-    const int ld = n_mels + 1;
-    const float* src = melF + ((size_t)w * T + t0) * n_mels;  // nt contiguous frame rows
-    const int total = nt * n_mels;
-    constexpr int U = 8;  // loads in flight per thread before any is consumed
     for (int i0 = 0; i0 < total; i0 += U * 256) {
-        float v[U];
+        if (i0 > 0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = src[min(i0 + u * 256 + (int)threadIdx.x, total - 1)];
+            for (int u = 0; u < U; ++u) v[u] = src[min(i0 + u * 256 + (int)threadIdx.x, total - 1)];
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int idx = i0 + u * 256 + threadIdx.x;

@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <type_traits>
 
 namespace aa {
 
@@ -44,6 +45,20 @@ constexpr int kSnLd = 2080;    // S row stride in floats (128-B aligned rows)
 constexpr int kSnHist = 256;   // radix-select buckets (8 bits per pass)
 constexpr int kSnFields = 10;  // run table: x0 x1 y parent left right top bottom area key
 enum { R_X0 = 0, R_X1, R_Y, R_P, R_LEFT, R_RIGHT, R_TOP, R_BOT, R_AREA, R_KEY };
+
+// A batch of recordings for the launches that run once per batch (the
+// counters, morphology and components): their frame counts, passed by value;
+// recording k's buffers sit k * pf bytes after recording 0's (blockIdx.z or
+// .y = k).
+constexpr int kSnMaxBatch = 64;
+struct SnBatch {
+    int n;
+    int nf[kSnMaxBatch];
+};
+template <typename T>
+__host__ __device__ __forceinline__ T* sn_at(T* p, size_t pf, int k) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(const_cast<std::remove_const_t<T>*>(p)) + pf * k);
+}
 
 struct SnPlan {
     aa_sn_config cfg;
@@ -92,12 +107,13 @@ __device__ __forceinline__ unsigned hist_pick(const unsigned* hist, unsigned ran
 }
 
 // sn_zero: the counters a run accumulates into (atomicMax / atomicAdd), one
-// launch instead of a memset per buffer
-__global__ void sn_zero(unsigned* __restrict__ gmax, int* __restrict__ counters, int32_t* __restrict__ n_out) {
-    const int i = threadIdx.x;
-    if (gmax && i < 16) gmax[i] = 0u;
-    if (i < 16) counters[i] = 0;
-    if (i < 2) n_out[i] = 0;
+// launch for every recording of the batch instead of a memset per buffer
+__global__ void sn_zero(unsigned* __restrict__ gmax, int* __restrict__ counters, size_t pf, int32_t* __restrict__ n_out,
+                        int n_out_stride) {
+    const int i = threadIdx.x, k = blockIdx.x;
+    if (gmax && i < 16) sn_at(gmax, pf, k)[i] = 0u;
+    if (i < 16) sn_at(counters, pf, k)[i] = 0;
+    if (i < 2) n_out[(size_t)k * n_out_stride + i] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -420,11 +436,15 @@ __global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, in
 // the vertical one (both are a min / max over the rectangle's in-image taps).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void sn_morph(const unsigned long long* __restrict__ src,
-                                                unsigned long long* __restrict__ dst, int rows, int words, int n_frames,
+                                                unsigned long long* __restrict__ dst, int rows, SnBatch nb, size_t pf,
                                                 int vlo, int vhi, int hlo, int hhi, int erode) {
+    const int k = blockIdx.z;
+    const int n_frames = nb.nf[k], words = (n_frames + 63) / 64;
     const int w = blockIdx.x * 256 + threadIdx.x;
     const int y = blockIdx.y;
     if (w >= words) return;
+    src = sn_at(src, pf, k);
+    dst = sn_at(dst, pf, k);
     const unsigned long long ident = erode ? ~0ull : 0ull;
     // vertical: rows y + vlo .. y + vhi inside the image, words w - 1 .. w + 1
     unsigned long long vm = ident, v0 = ident, vp = ident;
@@ -501,12 +521,19 @@ __device__ __forceinline__ int wave_sum_int(int v) {
     return v;
 }
 
-__global__ __launch_bounds__(256) void sn_runs(const unsigned long long* __restrict__ M, int rows, int words,
-                                               int* __restrict__ R, int max_runs, int* __restrict__ row_off,
+__global__ __launch_bounds__(256) void sn_runs(const unsigned long long* __restrict__ M, int rows, SnBatch nb,
+                                               size_t pf, int* __restrict__ R, int max_runs, int* __restrict__ row_off,
                                                int* __restrict__ row_cnt, int* __restrict__ counters) {
     const int lane = threadIdx.x & 63;
     const int y = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.y;
     if (y >= rows) return;
+    const int words = (nb.nf[k] + 63) / 64;
+    M = sn_at(M, pf, k);
+    R = sn_at(R, pf, k);
+    row_off = sn_at(row_off, pf, k);
+    row_cnt = sn_at(row_cnt, pf, k);
+    counters = sn_at(counters, pf, k);
     const unsigned long long* r = M + (size_t)y * words;
     auto starts_of = [&](int w) -> unsigned long long {
         const unsigned long long v = r[w], prev = w > 0 ? r[w - 1] : 0ull;
@@ -570,7 +597,12 @@ __global__ __launch_bounds__(256) void sn_runs(const unsigned long long* __restr
 
 __global__ __launch_bounds__(256) void sn_unite(int* __restrict__ R, int max_runs, const int* __restrict__ row_off,
                                                 const int* __restrict__ row_cnt, const int* __restrict__ counters,
-                                                int rows) {
+                                                int rows, size_t pf) {
+    const int k = blockIdx.y;
+    R = sn_at(R, pf, k);
+    row_off = sn_at(row_off, pf, k);
+    row_cnt = sn_at(row_cnt, pf, k);
+    counters = sn_at(counters, pf, k);
     const int nr = min(counters[0], max_runs);
     for (int i = blockIdx.x * 256 + threadIdx.x; i < nr; i += gridDim.x * 256) {
     const int* X0 = R + (size_t)R_X0 * max_runs;
@@ -590,8 +622,12 @@ __global__ __launch_bounds__(256) void sn_unite(int* __restrict__ R, int max_run
     }
 }
 
-__global__ __launch_bounds__(256) void sn_stats(int* __restrict__ R, int max_runs, int kx,
-                                                const int* __restrict__ counters) {
+__global__ __launch_bounds__(256) void sn_stats(int* __restrict__ R, int max_runs, SnBatch nb,
+                                                const int* __restrict__ counters, size_t pf) {
+    const int k = blockIdx.y;
+    const int kx = (nb.nf[k] + 1) / 2;  // 2x2 blocks per block row (OpenCV's label order)
+    R = sn_at(R, pf, k);
+    counters = sn_at(counters, pf, k);
     const int nr = min(counters[0], max_runs);
     for (int i = blockIdx.x * 256 + threadIdx.x; i < nr; i += gridDim.x * 256) {
     const int y = R[(size_t)R_Y * max_runs + i];
@@ -609,8 +645,14 @@ __global__ __launch_bounds__(256) void sn_stats(int* __restrict__ R, int max_run
 
 __global__ __launch_bounds__(256) void sn_emit(const int* __restrict__ R, int max_runs, int wmin, int hmin,
                                                const int* __restrict__ counters, const unsigned* __restrict__ gmax,
-                                               aa_sn_component* __restrict__ out, int max_out,
-                                               int32_t* __restrict__ n_out) {
+                                               size_t pf, aa_sn_component* __restrict__ out, int max_out,
+                                               long long out_stride, int32_t* __restrict__ n_out, int n_out_stride) {
+    const int k = blockIdx.y;
+    R = sn_at(R, pf, k);
+    counters = sn_at(counters, pf, k);
+    if (gmax) gmax = sn_at(gmax, pf, k);
+    out += k * out_stride;
+    n_out += (size_t)k * n_out_stride;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         int st = counters[1];
         if (gmax && (*gmax & 0x7FFFFFFFu) >= 0x7F800000u) st |= AA_SN_NONFINITE;
@@ -641,8 +683,11 @@ __global__ __launch_bounds__(256) void sn_emit(const int* __restrict__ R, int ma
 // host side
 // ---------------------------------------------------------------------------
 struct SnWs {
+    // shared by the recordings of a batch (their per-recording launches run
+    // one after another on the stream)
     float* S;
     float* ST;
+    // recording 0's; recording k's sit k * pf bytes further
     unsigned* colmed;
     float* c3;
     unsigned* gmax;
@@ -653,6 +698,7 @@ struct SnWs {
     int* row_cnt;
     int* R;
     int max_runs;
+    size_t pf;
     size_t bytes;
 };
 
@@ -666,7 +712,8 @@ static int sn_max_runs(const SnPlan& p, int F) {
     return (int)std::min<long long>(per * kSnBins, INT_MAX / kSnFields);
 }
 
-static SnWs sn_ws_layout(const SnPlan& p, int F, char* base) {
+// F: the largest frame count of the batch; K recordings
+static SnWs sn_ws_layout(const SnPlan& p, int F, int K, char* base) {
     SnWs w{};
     size_t off = 0;
     auto take = [&](size_t bytes) -> char* {
@@ -677,6 +724,7 @@ static SnWs sn_ws_layout(const SnPlan& p, int F, char* base) {
     const int words = (F + 63) / 64, ldt = words * 64;
     w.S = reinterpret_cast<float*>(take(sizeof(float) * (size_t)F * kSnLd));
     w.ST = reinterpret_cast<float*>(take(sizeof(float) * (size_t)kSnBins * ldt));
+    const size_t per0 = off;
     w.colmed = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * (size_t)F));
     w.c3 = reinterpret_cast<float*>(take(sizeof(float) * (size_t)F));
     w.gmax = reinterpret_cast<unsigned*>(take(64));
@@ -687,23 +735,26 @@ static SnWs sn_ws_layout(const SnPlan& p, int F, char* base) {
     w.row_cnt = reinterpret_cast<int*>(take(sizeof(int) * kSnBins));
     w.max_runs = sn_max_runs(p, F);
     w.R = reinterpret_cast<int*>(take(sizeof(int) * (size_t)kSnFields * w.max_runs));
-    w.bytes = off;
+    w.pf = off - per0;
+    w.bytes = per0 + (size_t)K * w.pf;
     return w;
 }
 
 // morphology (:670-684), components (:686) and the size filter (:689-691)
-// from the mask in ws.M0
-static int sn_components(const SnPlan& p, const SnWs& ws, int F, const unsigned* gmax, aa_sn_component* out,
-                         int max_out, int32_t* n_out, hipStream_t st) {
-    const int words = (F + 63) / 64;
-    const dim3 gm((words + 255) / 256, kSnBins);
+// of every recording of the batch from its mask in M0, one launch per step
+// for the whole batch
+static int sn_components(const SnPlan& p, const SnWs& ws, const SnBatch& nb, bool with_gmax, aa_sn_component* out,
+                         int max_out, long long out_stride, int32_t* n_out, int n_out_stride, hipStream_t st) {
+    int maxw = 1;
+    for (int k = 0; k < nb.n; ++k) maxw = std::max(maxw, (nb.nf[k] + 63) / 64);
+    const dim3 gm((maxw + 255) / 256, kSnBins, nb.n);
     unsigned long long* a = ws.M0;
     unsigned long long* b = ws.M1;
     // one launch per structuring element: rectangle kh x kw, anchor (kw / 2, kh / 2)
     auto morph = [&](int kh, int kw, int erode) -> int {
         const int ax = kw / 2, ay = kh / 2;
-        hipLaunchKernelGGL(sn_morph, gm, dim3(256), 0, st, a, b, kSnBins, words, F, -ay, kh - 1 - ay, -ax, kw - 1 - ax,
-                           erode);
+        hipLaunchKernelGGL(sn_morph, gm, dim3(256), 0, st, a, b, kSnBins, nb, ws.pf, -ay, kh - 1 - ay, -ax,
+                           kw - 1 - ax, erode);
         AA_LAUNCH_CHECK();
         std::swap(a, b);
         return AA_OK;
@@ -713,20 +764,77 @@ static int sn_components(const SnPlan& p, const SnWs& ws, int F, const unsigned*
     if ((rc = morph(4, 4, 1)) || (rc = morph(4, 4, 0))) return rc;
     if ((rc = morph(p.kh_d, p.kw_d, 0)) || (rc = morph(p.kh_e, p.kw_e, 1))) return rc;
     // (counters were zeroed by sn_zero; sn_runs marks the slots of a dropped row)
-    hipLaunchKernelGGL(sn_runs, dim3((kSnBins + 3) / 4), dim3(256), 0, st, a, kSnBins, words, ws.R, ws.max_runs,
-                       ws.row_off, ws.row_cnt, ws.counters);
+    hipLaunchKernelGGL(sn_runs, dim3((kSnBins + 3) / 4, nb.n), dim3(256), 0, st, a, kSnBins, nb, ws.pf, ws.R,
+                       ws.max_runs, ws.row_off, ws.row_cnt, ws.counters);
     AA_LAUNCH_CHECK();
     // grid-stride over the runs actually allocated (counters[0] of max_runs)
-    const int gr = std::min((ws.max_runs + 255) / 256, 512);
-    hipLaunchKernelGGL(sn_unite, dim3(gr), dim3(256), 0, st, ws.R, ws.max_runs, ws.row_off, ws.row_cnt, ws.counters,
-                       kSnBins);
+    const dim3 gr(std::min((ws.max_runs + 255) / 256, 512), nb.n);
+    hipLaunchKernelGGL(sn_unite, gr, dim3(256), 0, st, ws.R, ws.max_runs, ws.row_off, ws.row_cnt, ws.counters, kSnBins,
+                       ws.pf);
     AA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sn_stats, dim3(gr), dim3(256), 0, st, ws.R, ws.max_runs, (F + 1) / 2, ws.counters);
+    hipLaunchKernelGGL(sn_stats, gr, dim3(256), 0, st, ws.R, ws.max_runs, nb, ws.counters, ws.pf);
     AA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sn_emit, dim3(gr), dim3(256), 0, st, ws.R, ws.max_runs, p.wmin, p.hmin, ws.counters, gmax, out,
-                       max_out, n_out);
+    hipLaunchKernelGGL(sn_emit, gr, dim3(256), 0, st, ws.R, ws.max_runs, p.wmin, p.hmin, ws.counters,
+                       with_gmax ? ws.gmax : nullptr, ws.pf, out, max_out, out_stride, n_out, n_out_stride);
     AA_LAUNCH_CHECK();
     return AA_OK;
+}
+
+// The whole detector over K recordings of one PCM buffer (recording k:
+// offs[k], lens[k] samples, host arrays): per recording the STFT (+ column
+// medians), transpose and row select (+ mask) into its own mask slot, then
+// the morphology and components of the whole batch.
+static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const int64_t* lens, int K,
+                       void* workspace, size_t workspace_bytes, aa_sn_component* out, int max_out,
+                       long long out_stride, int32_t* n_out, int n_out_stride, uint64_t* mask_out, hipStream_t st) {
+    SnBatch nb{};
+    nb.n = K;
+    int Fmax = 1;
+    for (int k = 0; k < K; ++k) {
+        AA_CHECK(lens[k] >= 0 && lens[k] <= (int64_t(1) << 29) && offs[k] >= 0, AA_ERR_UNSUPPORTED,
+                 "aa_sn_run: recording %d: %lld samples at %lld (at most 2^29)", k, (long long)lens[k],
+                 (long long)offs[k]);
+        AA_CHECK(pcm || lens[k] == 0, AA_ERR_INVALID, "aa_sn_run: null pcm");
+        nb.nf[k] = sn_frames(*p, lens[k]);
+        Fmax = std::max(Fmax, nb.nf[k]);
+    }
+    const SnWs ws = sn_ws_layout(*p, Fmax, K, static_cast<char*>(workspace));
+    AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE, "aa_sn_run: workspace %zu < %zu bytes",
+             workspace_bytes, ws.bytes);
+    hipLaunchKernelGGL(sn_zero, dim3(K), dim3(64), 0, st, ws.gmax, ws.counters, ws.pf, n_out, n_out_stride);
+    AA_LAUNCH_CHECK();
+    const size_t lds = sizeof(float2) * kSnWpb * kHalf;
+    static bool attr_set = false;
+    if (!attr_set) {
+        AA_HIP(hipFuncSetAttribute((const void*)sn_stft, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_set = true;
+    }
+    for (int k = 0; k < K; ++k) {
+        const int F = nb.nf[k];
+        unsigned* gmax = sn_at(ws.gmax, ws.pf, k);
+        unsigned* colmed = sn_at(ws.colmed, ws.pf, k);
+        float* c3 = sn_at(ws.c3, ws.pf, k);
+        unsigned long long* M0 = sn_at(ws.M0, ws.pf, k);
+        int grid = std::min((F + kSnWpb - 1) / kSnWpb, 256 * 3);  // persistent: 3 blocks per CU
+        grid = (grid + 7) & ~7;
+        hipLaunchKernelGGL(sn_stft, dim3(grid), dim3(64 * kSnWpb), lds, st, lens[k] ? pcm + offs[k] : pcm,
+                           (int)lens[k], p->cfg.hop_length, F, p->d_tw, p->d_tw4096, ws.S, gmax, colmed);
+        AA_LAUNCH_CHECK();
+        const int words = (F + 63) / 64, ldt = words * 64;
+        hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST, gmax,
+                           colmed, c3);
+        AA_LAUNCH_CHECK();
+        if (F <= kSnStageMax)
+            hipLaunchKernelGGL(sn_select<true>, dim3(kSnBins), dim3(256), sizeof(unsigned) * F, st, ws.ST, ldt, F, gmax,
+                               c3, words, M0);
+        else
+            hipLaunchKernelGGL(sn_select<false>, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, gmax, c3, words, M0);
+        AA_LAUNCH_CHECK();
+    }
+    if (mask_out)
+        AA_HIP(hipMemcpyAsync(mask_out, ws.M0, 8 * (size_t)kSnBins * ((nb.nf[0] + 63) / 64), hipMemcpyDeviceToDevice,
+                              st));
+    return sn_components(*p, ws, nb, true, out, max_out, out_stride, n_out, n_out_stride, st);
 }
 
 }  // namespace aa
@@ -825,47 +933,35 @@ extern "C" int64_t aa_sn_n_frames(const void* plan, int64_t n_samples) {
 extern "C" size_t aa_sn_workspace_bytes(const void* plan, int64_t max_samples) {
     const SnPlan* p = static_cast<const SnPlan*>(plan);
     if (!p || max_samples < 0) return 0;
-    return sn_ws_layout(*p, sn_frames(*p, max_samples), nullptr).bytes;
+    return sn_ws_layout(*p, sn_frames(*p, max_samples), 1, nullptr).bytes;
+}
+
+extern "C" size_t aa_sn_batch_workspace_bytes(const void* plan, int64_t max_samples, int32_t n_rec) {
+    const SnPlan* p = static_cast<const SnPlan*>(plan);
+    if (!p || max_samples < 0 || n_rec < 1 || n_rec > kSnMaxBatch) return 0;
+    return sn_ws_layout(*p, sn_frames(*p, max_samples), n_rec, nullptr).bytes;
 }
 
 extern "C" int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* workspace, size_t workspace_bytes,
                          aa_sn_component* out, int32_t max_out, int32_t* n_out, uint64_t* mask_out, void* stream) {
     SnPlan* p = static_cast<SnPlan*>(plan);
     AA_CHECK(p && out && n_out && (pcm || n_samples == 0), AA_ERR_INVALID, "aa_sn_run: null argument");
-    AA_CHECK(n_samples >= 0 && n_samples <= (int64_t(1) << 29), AA_ERR_UNSUPPORTED,
-             "aa_sn_run: %lld samples (at most 2^29)", (long long)n_samples);
-    const int F = sn_frames(*p, n_samples);
-    const SnWs ws = sn_ws_layout(*p, F, static_cast<char*>(workspace));
-    AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE, "aa_sn_run: workspace %zu < %zu bytes",
-             workspace_bytes, ws.bytes);
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(sn_zero, dim3(1), dim3(64), 0, st, ws.gmax, ws.counters, n_out);
-    AA_LAUNCH_CHECK();
-    const size_t lds = sizeof(float2) * kSnWpb * kHalf;
-    static bool attr_set = false;
-    if (!attr_set) {
-        AA_HIP(hipFuncSetAttribute((const void*)sn_stft, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr_set = true;
-    }
-    int grid = std::min((F + kSnWpb - 1) / kSnWpb, 256 * 3);  // persistent: 3 blocks per CU
-    grid = (grid + 7) & ~7;
-    hipLaunchKernelGGL(sn_stft, dim3(grid), dim3(64 * kSnWpb), lds, st, pcm, (int)n_samples, p->cfg.hop_length, F,
-                       p->d_tw, p->d_tw4096, ws.S, ws.gmax, ws.colmed);
-    AA_LAUNCH_CHECK();
-    const int words = (F + 63) / 64, ldt = words * 64;
-    hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST, ws.gmax,
-                       ws.colmed, ws.c3);
-    AA_LAUNCH_CHECK();
-    if (F <= kSnStageMax)
-        hipLaunchKernelGGL(sn_select<true>, dim3(kSnBins), dim3(256), sizeof(unsigned) * F, st, ws.ST, ldt, F, ws.gmax,
-                           ws.c3, words, ws.M0);
-    else
-        hipLaunchKernelGGL(sn_select<false>, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, ws.gmax, ws.c3, words,
-                           ws.M0);
-    AA_LAUNCH_CHECK();
-    if (mask_out)
-        AA_HIP(hipMemcpyAsync(mask_out, ws.M0, 8 * (size_t)kSnBins * words, hipMemcpyDeviceToDevice, st));
-    return sn_components(*p, ws, F, ws.gmax, out, max_out, n_out, st);
+    const int64_t off = 0;
+    return sn_run_impl(p, pcm, &off, &n_samples, 1, workspace, workspace_bytes, out, max_out, max_out, n_out, 2,
+                       mask_out, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int aa_sn_run_batch(void* plan, const float* pcm, const int64_t* offsets, const int64_t* lengths,
+                               int32_t n_rec, void* workspace, size_t workspace_bytes, aa_sn_component* out,
+                               int32_t max_out, int64_t out_stride, int32_t* n_out, int32_t n_out_stride,
+                               void* stream) {
+    SnPlan* p = static_cast<SnPlan*>(plan);
+    AA_CHECK(p && offsets && lengths && out && n_out, AA_ERR_INVALID, "aa_sn_run_batch: null argument");
+    AA_CHECK(n_rec >= 1 && n_rec <= kSnMaxBatch, AA_ERR_UNSUPPORTED, "aa_sn_run_batch: %d recordings (1..%d)", n_rec,
+             kSnMaxBatch);
+    AA_CHECK(out_stride >= max_out && n_out_stride >= 2, AA_ERR_INVALID, "aa_sn_run_batch: overlapping outputs");
+    return sn_run_impl(p, pcm, offsets, lengths, n_rec, workspace, workspace_bytes, out, max_out, out_stride, n_out,
+                       n_out_stride, nullptr, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int64_t n_frames, void* workspace,
@@ -876,12 +972,15 @@ extern "C" int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int6
     AA_CHECK(n_frames >= 1 && n_frames <= (int64_t(1) << 28), AA_ERR_INVALID,
              "aa_sn_components_from_mask: %lld frames", (long long)n_frames);
     const int F = (int)n_frames;
-    const SnWs ws = sn_ws_layout(*p, F, static_cast<char*>(workspace));
+    const SnWs ws = sn_ws_layout(*p, F, 1, static_cast<char*>(workspace));
     AA_CHECK(workspace && workspace_bytes >= ws.bytes, AA_ERR_WORKSPACE,
              "aa_sn_components_from_mask: workspace %zu < %zu bytes", workspace_bytes, ws.bytes);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(sn_zero, dim3(1), dim3(64), 0, st, nullptr, ws.counters, n_out);
+    hipLaunchKernelGGL(sn_zero, dim3(1), dim3(64), 0, st, nullptr, ws.counters, ws.pf, n_out, 2);
     AA_LAUNCH_CHECK();
     AA_HIP(hipMemcpyAsync(ws.M0, mask, 8 * (size_t)kSnBins * ((F + 63) / 64), hipMemcpyDeviceToDevice, st));
-    return sn_components(*p, ws, F, nullptr, out, max_out, n_out, st);
+    SnBatch nb{};
+    nb.n = 1;
+    nb.nf[0] = F;
+    return sn_components(*p, ws, nb, false, out, max_out, max_out, n_out, 2, st);
 }

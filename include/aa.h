@@ -305,6 +305,18 @@ size_t aa_sn_workspace_bytes(const void* plan, int64_t max_samples);
  * mask before morphology; bit f % 64 of word f / 64 is frame f. */
 int aa_sn_run(void* plan, const float* pcm, int64_t n_samples, void* workspace, size_t workspace_bytes,
               aa_sn_component* out, int32_t max_out, int32_t* n_out, uint64_t* mask_out, void* stream);
+/* signal_noise of n_rec (1..64) recordings in one device PCM buffer in one
+ * pass (the batched corpus path; the reference runs it once per file,
+ * src/identify_tracks.py:420): recording k is pcm[offsets[k] ..
+ * offsets[k] + lengths[k]) (offsets, lengths: HOST arrays).  Its components
+ * go to out + k * out_stride (out_stride >= max_out), its {count, status} to
+ * n_out + k * n_out_stride (>= 2).  The per-recording STFT / medians / mask
+ * launches run back to back; the morphology and components run once for the
+ * whole batch.  Workspace: aa_sn_batch_workspace_bytes(plan, longest, n_rec). */
+size_t aa_sn_batch_workspace_bytes(const void* plan, int64_t max_samples, int32_t n_rec);
+int aa_sn_run_batch(void* plan, const float* pcm, const int64_t* offsets, const int64_t* lengths, int32_t n_rec,
+                    void* workspace, size_t workspace_bytes, aa_sn_component* out, int32_t max_out,
+                    int64_t out_stride, int32_t* n_out, int32_t n_out_stride, void* stream);
 /* Morphology, components and filter of a given mask (mask_out's layout). */
 int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int64_t n_frames, void* workspace,
                                size_t workspace_bytes, aa_sn_component* out, int32_t max_out,

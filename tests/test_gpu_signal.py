@@ -115,3 +115,43 @@ def test_classify_builds_tracks_from_signals(gpu, model_root, tmp_path):
     assert raw_length == pytest.approx(12.0) and len(signals) > 0 and len(tracks) > 0
     for t in tracks:
         assert len(t.results) >= 1
+
+
+def test_sn_run_batch_matches_single(gpu):
+    """aa_sn_run_batch (the corpus path: per-recording STFT / medians / mask,
+    one batched morphology + components pass) gives every recording exactly
+    the components aa_sn_run gives it alone: lengths that differ (different
+    frame counts and mask widths in one batch), an empty recording, unaligned
+    offsets into one PCM buffer."""
+    import ctypes as C
+    from aa_amd import _lib
+    det = _det(gpu)
+    lens = [SR * 7 + 123, 0, SR * 3, HOP * 64 - 1, SR * 11 + 5, 4000]
+    clips = [_clip(n / SR, 40 + i) if n else np.zeros(0, np.float32) for i, n in enumerate(lens)]
+    offs, pos = [], 3  # unaligned start
+    for c in clips:
+        offs.append(pos)
+        pos += len(c) + 17
+    buf = np.zeros(pos, np.float32)
+    for o, c in zip(offs, clips):
+        buf[o:o + len(c)] = c
+    pcm = torch.from_numpy(buf).to(gpu)
+    K, cap = len(lens), 512
+    L = _lib.lib()
+    need = L.aa_sn_batch_workspace_bytes(det._h, max(lens), K)
+    ws = torch.empty(need, dtype=torch.uint8, device=gpu)
+    out = torch.zeros((K, cap + 1, 6), dtype=torch.int32, device=gpu)
+    rc = L.aa_sn_run_batch(det._h, _lib.dptr(pcm), (C.c_int64 * K)(*offs), (C.c_int64 * K)(*lens), K, _lib.dptr(ws),
+                           ws.numel(), _lib.dptr(out[0, 1:]), cap, cap + 1, _lib.dptr(out[0, 0]), (cap + 1) * 6, 0)
+    _lib.check(rc, "aa_sn_run_batch")
+    got = out.cpu().numpy()
+    n_nonempty = 0
+    for k in range(K):
+        want = det.components(pcm[offs[k]:offs[k] + lens[k]])
+        cnt, status = int(got[k, 0, 0]), int(got[k, 0, 1])
+        assert status == 0 and cnt == len(want), (k, cnt, status, len(want))
+        rows = got[k, 1:1 + cnt].astype(np.int64)
+        rows = rows[np.lexsort((rows[:, 5], rows[:, 0]))][:, :5]
+        assert np.array_equal(rows, want), k
+        n_nonempty += cnt > 0
+    assert n_nonempty >= 3
