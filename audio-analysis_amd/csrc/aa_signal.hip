@@ -438,11 +438,14 @@ __global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, in
 __global__ __launch_bounds__(256) void sn_morph(const unsigned long long* __restrict__ src,
                                                 unsigned long long* __restrict__ dst, int rows, SnBatch nb, size_t pf,
                                                 int vlo, int vhi, int hlo, int hhi, int erode) {
-    const int k = blockIdx.z;
+    // one thread per (row, word) of recording k = blockIdx.y, rows x words
+    // flattened over the blocks (a row is ~160 words: a block per row would
+    // idle a third of its lanes)
+    const int k = blockIdx.y;
     const int n_frames = nb.nf[k], words = (n_frames + 63) / 64;
-    const int w = blockIdx.x * 256 + threadIdx.x;
-    const int y = blockIdx.y;
-    if (w >= words) return;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= rows * words) return;
+    const int y = idx / words, w = idx - y * words;
     src = sn_at(src, pf, k);
     dst = sn_at(dst, pf, k);
     const unsigned long long ident = erode ? ~0ull : 0ull;
@@ -747,7 +750,7 @@ static int sn_components(const SnPlan& p, const SnWs& ws, const SnBatch& nb, boo
                          int max_out, long long out_stride, int32_t* n_out, int n_out_stride, hipStream_t st) {
     int maxw = 1;
     for (int k = 0; k < nb.n; ++k) maxw = std::max(maxw, (nb.nf[k] + 63) / 64);
-    const dim3 gm((maxw + 255) / 256, kSnBins, nb.n);
+    const dim3 gm((kSnBins * maxw + 255) / 256, nb.n);
     unsigned long long* a = ws.M0;
     unsigned long long* b = ws.M1;
     // one launch per structuring element: rectangle kh x kw, anchor (kw / 2, kh / 2)

@@ -5,7 +5,10 @@ analysis windows -- 39 windows of a 60 s clip + 25 windows of a second 60 s
 clip (48 kHz mono, synthetic, int16-quantised; reference stride 1.5 s / length
 3 s) -- through the GPU log-mel front end (htk custom mel, n_fft 4096, hop 640,
 160 bands, power_to_db) and the model1 CNN, then the per-track mean.  PCM and
-window tables are resident in HBM before the timed region.
+window tables are resident in HBM before the timed region; the steps rotate
+over 4 resident clip pairs (kernel times depend on the data).  The front end
+of step k+1 runs on a second stream beside the CNN of step k (--pipeline 0:
+back to back, the 'serial' secondary).
 
 Headline precision: split-bf16 ("bf16x3", classify()'s default), the fastest
 mode that holds the north-star gate max|delta logit| <= 1e-3 against the CPU
@@ -57,6 +60,10 @@ HBM_PEAK_GBS = 8000.0
 WORKLOAD = ("config2: 64 windows/step (39 of clip A + 25 of clip B, 60 s 48 kHz mono), "
             "htk log-mel n_fft 4096 hop 640 160 mel + model1 CNN")
 COLD_POOL = 16  # clip pairs of the cold-PCM variant: 16 x 23 MB > the 256 MiB Infinity Cache
+# clip pairs the headline rotates over (resident, 92 MB: inside the Infinity
+# Cache): kernel times depend on the data (MFMA power and clock), and one
+# pair alone measured 7 % faster than the average of four
+HEAD_PAIRS = 4
 
 
 def parse(argv=None):
@@ -69,13 +76,17 @@ def parse(argv=None):
                     help="bf16x3: split-bf16 (gated, default); fp8: OCP e4m3fn CNN (BASELINE configs[4])")
     ap.add_argument("--logmel", default="f32", choices=["f32", "f16"],
                     help="log-mel dtype between the front end and the CNN (f16: BASELINE configs[4])")
-    ap.add_argument("--secondary", default="f32,bf16,fp8,fp8_f16mel,cold",
+    ap.add_argument("--secondary", default="serial,f32,bf16,fp8,fp8_f16mel,cold",
                     help="N=1 only: extra modes measured into the same line ('' disables)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bound on the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="CPU-baseline processes for the numpy front end (the GPU box's CPU share is 16)")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1 (default): the front end of batch k+1 on its own stream beside the CNN of batch k "
+                         "(double-buffered log-mel; every step still runs one front end and one CNN pass); "
+                         "0: the two back to back on one stream (reported as the 'serial' secondary)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4],
                     help="2: the 64-window step (BASELINE configs[1], the headline); 3: streamed 60 s clips "
                          "through the model1+2+3 ensemble (configs[2]), PCM uploaded from pinned host memory; "
@@ -192,7 +203,7 @@ class Step:
     buffers of ``pairs`` resident clip pairs (1 = the headline; COLD_POOL =
     the cold-PCM variant, one pair per step in rotation)."""
 
-    def __init__(self, dev, rank, model_path, precision, pairs=1, first=None, lm16=False):
+    def __init__(self, dev, rank, model_path, precision, pairs=1, first=None, lm16=False, pipeline=False):
         from aa_amd.frontend import FrontEnd
         from aa_amd.model import Model
         self.fe_s = fe_settings()
@@ -214,9 +225,69 @@ class Step:
         self.fe_ws = torch.empty(max(self.fe.workspace_bytes(self.n_win), 256), dtype=torch.uint8, device=dev)
         self.m_ws = torch.empty(max(self.model.workspace_bytes(self.n_win), 256), dtype=torch.uint8, device=dev)
         self.k = 0
+        self.lanes = None
+        if pipeline == 2:
+            # two batches in flight, each on its own stream (front end -> CNN ->
+            # track mean), alternating steps: the kernels of one fill the other's
+            # tails and phases
+            self.lanes = []
+            for j in range(2):
+                self.lanes.append(dict(
+                    s=torch.cuda.Stream(device=dev), logmel=self.logmel if j == 0 else torch.empty_like(self.logmel),
+                    fe_ws=self.fe_ws if j == 0 else torch.empty_like(self.fe_ws),
+                    m_ws=self.m_ws if j == 0 else torch.empty_like(self.m_ws),
+                    logits=self.logits if j == 0 else torch.empty_like(self.logits),
+                    probs=self.probs if j == 0 else torch.empty_like(self.probs),
+                    tmean=self.tmean if j == 0 else torch.empty_like(self.tmean)))
+            self.pipeline = False
+            return
+        self.pipeline = bool(pipeline)
+        if self.pipeline:
+            # batch k+1's front end on s_fe into buffer (k+1) % 2 while the CNN
+            # of batch k reads buffer k % 2 on the current stream
+            self.s_fe = torch.cuda.Stream(device=dev)
+            self.lm2 = [self.logmel, torch.empty_like(self.logmel)]
+            self.ws2 = [self.fe_ws, torch.empty_like(self.fe_ws)]
+            self.fe_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self.cnn_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self.issued = -1  # last batch whose front end is issued
+
+    def _fe_ahead(self, j):
+        b = j % 2
+        cur = torch.cuda.current_stream()
+        self.s_fe.wait_event(self.cnn_done[b]) if j >= 2 else self.s_fe.wait_stream(cur)
+        with torch.cuda.stream(self.s_fe):
+            i = j % len(self.pcm)
+            self.fe.run(self.pcm[i], self.rows[i], out=self.lm2[b], workspace=self.ws2[b])
+            self.fe_done[b].record(self.s_fe)
+        self.issued = j
 
     def __call__(self):
         from aa_amd.model import track_mean
+        if self.lanes is not None:
+            k = self.k
+            self.k += 1
+            L = self.lanes[k % 2]
+            i = k % len(self.pcm)
+            with torch.cuda.stream(L["s"]):
+                self.fe.run(self.pcm[i], self.rows[i], out=L["logmel"], workspace=L["fe_ws"])
+                self.model.forward(L["logmel"], L["logits"], L["probs"], workspace=L["m_ws"])
+                track_mean(L["probs"][None], self.wb, self.wc, out=L["tmean"])
+            self.logits, self.tmean = L["logits"], L["tmean"]
+            return
+        if self.pipeline:
+            k = self.k
+            self.k += 1
+            if self.issued < k:
+                self._fe_ahead(k)
+            self._fe_ahead(k + 1)  # overlaps the CNN below
+            b = k % 2
+            cur = torch.cuda.current_stream()
+            cur.wait_event(self.fe_done[b])
+            self.model.forward(self.lm2[b], self.logits, self.probs, workspace=self.m_ws)
+            self.cnn_done[b].record(cur)
+            track_mean(self.probs[None], self.wb, self.wc, out=self.tmean)
+            return
         i = self.k % len(self.pcm)
         self.k += 1
         self.fe.run(self.pcm[i], self.rows[i], out=self.logmel, workspace=self.fe_ws)
@@ -259,7 +330,8 @@ def main_step(args, world, rank, dev):
     model_path = make_model(Path(tmp) / "model1", "model1", seed=1)
     first = make_batch(rank, fe_settings())
     pcm_np, _, views = first
-    step = Step(dev, rank, model_path, args.precision, first=first, lm16=args.logmel == "f16")
+    step = Step(dev, rank, model_path, args.precision, pairs=HEAD_PAIRS, first=first, lm16=args.logmel == "f16",
+                pipeline=args.pipeline)
     fe, model, n_win = step.fe, step.model, step.n_win
 
     for _ in range(args.warmup):
@@ -270,6 +342,9 @@ def main_step(args, world, rank, dev):
     # timed on its own -- events around that launch only, 5 steps each -- so no
     # stage pays for its neighbours' events (bracketing them all inflates the
     # sum past the step).  The dominant stage gets the events of the timed region.
+    # (the calibration runs serially: with the pipeline on, a stage's events
+    # would also time whatever of the other stream overlaps it)
+    pipelined, step.pipeline = step.pipeline, False
     fe.set_timing(True)
     model.set_timing(True)
     for _ in range(2):
@@ -287,6 +362,8 @@ def main_step(args, world, rank, dev):
         torch.cuda.synchronize()
         calib.append(collect([(owner, idx)], n_win)[0])
         owner.set_timing(False)
+    step.pipeline = pipelined
+    step.k, step.issued = 0, -1
     dom = max(calib, key=lambda x: x["avg_ms"])
     dom["owner"].set_timing(True, stages=[dom["idx"]])
     elapsed = timed(step, args.steps, 0, world)
@@ -350,7 +427,11 @@ def main_step(args, world, rank, dev):
         "dtype": args.precision + (" (fp16 log-mel)" if args.logmel == "f16" else ""),
         "data": "synthetic (48 kHz int16-quantised noise+chirps, seeded), seeded random-init model1",
         "config": {"workload": WORKLOAD, "model": "model1", "global_batch": n_win * world,
-                   "seq_len": step.fe_s.win_len, "parallelism": f"dp{world}"},
+                   "seq_len": step.fe_s.win_len, "parallelism": f"dp{world}",
+                   "pipeline": "two batches in flight on two streams" if step.lanes is not None else
+                               "front end of batch k+1 on a second stream beside the CNN of batch k"
+                               if step.pipeline else "serial",
+                   "clip_pairs": f"{HEAD_PAIRS} resident clip pairs in rotation, one per step"},
         "roofline": roofline,
     }
     gate_fail = None
@@ -359,6 +440,9 @@ def main_step(args, world, rank, dev):
         ref = None
         if not args.no_parity:
             ref = reference_logits(pcm_np, views, model_path, cfg)
+            step.k, step.issued = 0, -1  # one more step on pair 0, the one the oracle ran
+            step()
+            torch.cuda.synchronize()
             d = float(np.abs(step.logits.cpu().numpy() - ref).max())
             out["max_abs_dlogit"] = {args.precision: d}
             if args.precision in GATED:
@@ -368,23 +452,32 @@ def main_step(args, world, rank, dev):
         sec = {}
         for mode in [m for m in args.secondary.split(",") if m]:
             # "fp8_f16mel": BASELINE configs[4] (fp16 log-mel + fp8 CNN)
-            prec = args.precision if mode == "cold" else mode.split("_")[0]
+            prec = args.precision if mode in ("cold", "serial") else mode.split("_")[0]
             if mode == args.precision:
                 continue
-            s2 = Step(dev, rank, model_path, prec, pairs=COLD_POOL if mode == "cold" else 1, first=first,
-                      lm16=mode.endswith("_f16mel") or (mode == "cold" and args.logmel == "f16"))
-            n2 = args.steps if mode == "cold" else max(10, args.steps // 2)
+            pairs = COLD_POOL if mode == "cold" else int(mode[4:]) if mode.startswith("pool") else HEAD_PAIRS
+            if mode.startswith("pool"):
+                prec = args.precision
+            s2 = Step(dev, rank, model_path, prec, pairs=pairs, first=first,
+                      lm16=mode.endswith("_f16mel") or (mode in ("cold", "serial") and args.logmel == "f16"),
+                      pipeline=0 if mode == "serial" else args.pipeline)
+            n2 = args.steps if mode in ("cold", "serial") or mode.startswith("pool") else max(10, args.steps // 2)
             el = timed(s2, n2, 5, 1)
             e = {"value": round(n2 * s2.n_win * SECONDS_PER_WINDOW / el, 1), "ms_per_step": round(1e3 * el / n2, 4),
                  "steps": n2, "dtype": prec + (" (fp16 log-mel)" if s2.logmel.dtype == torch.float16 else "")}
+            e["pipeline"] = 2 if s2.lanes is not None else int(s2.pipeline)
+            if mode == "serial":
+                e["note"] = "front end and CNN back to back on one stream (no overlap across steps)"
             if mode == "cold":
                 e["note"] = f"fresh clip pair per step from {COLD_POOL} resident pairs (> Infinity Cache)"
                 # the headline step re-timed right after, same step count: the
                 # cold/warm ratio without the clock drift between the two runs
                 el_w = timed(step, n2, 5, 1)
                 e["warm_same_run"] = round(n2 * n_win * SECONDS_PER_WINDOW / el_w, 1)
-            elif ref is not None:
-                s2.k = 0
+            if mode.startswith("pool"):
+                e["note"] = f"{pairs} resident clip pairs in rotation (inside the Infinity Cache)"
+            if mode != "cold" and not mode.startswith("pool") and ref is not None:
+                s2.k, s2.issued = 0, -1
                 s2()
                 torch.cuda.synchronize()
                 e["max_abs_dlogit"] = float(np.abs(s2.logits.cpu().numpy() - ref).max())
