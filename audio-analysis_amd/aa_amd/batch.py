@@ -483,6 +483,11 @@ class BatchAnalyser:
 
             def worker(lane):
                 torch.cuda.set_device(self.dev)
+                prof = None
+                if os.environ.get("AA_BATCH_CPROFILE"):  # host-side profile of this lane (tools)
+                    import cProfile
+                    prof = cProfile.Profile()
+                    prof.enable()
                 try:
                     while True:
                         with lock:
@@ -500,6 +505,10 @@ class BatchAnalyser:
                             results.update(docs)
                 except BaseException as e:  # surfaces in the caller
                     errors.append(e)
+                finally:
+                    if prof is not None:
+                        prof.disable()
+                        prof.dump_stats(f"{os.environ['AA_BATCH_CPROFILE']}.{time.monotonic_ns()}")
 
             with lock:
                 submit_upto(len(lanes) + 1)

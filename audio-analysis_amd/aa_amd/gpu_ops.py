@@ -1,6 +1,8 @@
 """Small device helpers around libaa.so used by the classify() host code."""
 from __future__ import annotations
 
+from functools import lru_cache
+
 import numpy as np
 import torch
 
@@ -15,7 +17,14 @@ def get_end_spans(n_samples: int, sr: int):
     """Chunks of the reference's get_end scan (src/identify_tracks.py:387-413)
     as sample spans: chunk c covers frames [170 c, 170 c + 170) of a centred
     STFT with n_fft = sr // 10, hop 281, i.e. samples
-    [f0 * 281 - n_fft/2, f1 * 281 + n_fft/2) clipped to the recording."""
+    [f0 * 281 - n_fft/2, f1 * 281 + n_fft/2) clipped to the recording.
+    Memoised per (length, rate): a corpus repeats a few recording lengths
+    (callers offset a copy of the span array; the cached one is read-only)."""
+    return _get_end_spans(int(n_samples), int(sr))
+
+
+@lru_cache(maxsize=256)
+def _get_end_spans(n_samples: int, sr: int):
     hop = 281
     n_fft = sr // 10
     chunk = sr // hop
@@ -28,7 +37,9 @@ def get_end_spans(n_samples: int, sr: int):
         spans.append((a, max(a, b)))
         starts.append(start)
         start, end = end, end + chunk
-    return np.asarray(spans, dtype=np.int64).reshape(-1, 2), starts, hop
+    arr = np.asarray(spans, dtype=np.int64).reshape(-1, 2)
+    arr.flags.writeable = False
+    return arr, tuple(starts), hop
 
 
 def get_end(frames, sr, device=None, pcm_dev=None):
@@ -38,7 +49,7 @@ def get_end(frames, sr, device=None, pcm_dev=None):
         return n / sr
     dev = _dev(device)
     pcm = pcm_dev if pcm_dev is not None else torch.from_numpy(np.ascontiguousarray(frames, np.float32)).to(dev)
-    sp = torch.from_numpy(spans).to(dev)
+    sp = torch.from_numpy(np.array(spans)).to(dev)
     flags = torch.empty(len(starts), dtype=torch.int32, device=dev)
     _lib.check(_lib.lib().aa_span_nonzero(_lib.dptr(pcm), n, _lib.dptr(sp), len(starts), _lib.dptr(flags),
                                           _lib.stream_ptr()), "aa_span_nonzero")

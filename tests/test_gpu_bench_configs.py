@@ -39,3 +39,15 @@ def test_bench_configs4_fp16_logmel_fp8(gpu):
                   "--cpu-seconds", "0")
     assert line["dtype"] == "fp8 (fp16 log-mel)"
     assert "roofline" in line and line["roofline"]["achieved"] > 0
+
+
+@pytest.mark.parametrize("pipeline", ["0", "1", "2"])
+def test_bench_step_modes_hold_the_gate(gpu, pipeline):
+    """The headline step back to back (0), with the next batch's front end
+    overlapped (1) and with two batches in flight on two streams (2, the
+    default): each asserts the 1e-3 logit gate on its own 64 windows (a step
+    on clip pair 0 after the timed loop, against the CPU oracle)."""
+    line = _bench("--pipeline", pipeline, "--steps", "6", "--warmup", "2", "--secondary=", "--cpu-seconds", "0")
+    assert line["parity_gate"]["pass"]
+    assert line["max_abs_dlogit"]["bf16x3"] <= 1e-3
+    assert line["steps"] == 6
