@@ -84,9 +84,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="CPU-baseline processes for the numpy front end (the GPU box's CPU share is 16)")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=2, choices=[0, 1, 2],
+    ap.add_argument("--pipeline", type=int, default=2, choices=[0, 1, 2, 3, 4],
                     help="2 (default): two batches in flight on two HIP streams, steps alternating between "
-                         "them (each step: front end -> CNN -> track mean of its own batch); 1: only the "
+                         "them (each step: front end -> CNN -> track mean of its own batch; 3, 4: as many "
+                         "streams); 1: only the "
                          "front end of batch k+1 on a second stream beside the CNN of batch k; 0: one stream, "
                          "back to back (reported as the 'serial' secondary)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4],
@@ -228,12 +229,12 @@ class Step:
         self.m_ws = torch.empty(max(self.model.workspace_bytes(self.n_win), 256), dtype=torch.uint8, device=dev)
         self.k = 0
         self.lanes = None
-        if pipeline == 2:
+        if pipeline >= 2:
             # two batches in flight, each on its own stream (front end -> CNN ->
             # track mean), alternating steps: the kernels of one fill the other's
             # tails and phases
             self.lanes = []
-            for j in range(2):
+            for j in range(int(pipeline)):
                 self.lanes.append(dict(
                     s=torch.cuda.Stream(device=dev), logmel=self.logmel if j == 0 else torch.empty_like(self.logmel),
                     fe_ws=self.fe_ws if j == 0 else torch.empty_like(self.fe_ws),
@@ -269,7 +270,7 @@ class Step:
         if self.lanes is not None:
             k = self.k
             self.k += 1
-            L = self.lanes[k % 2]
+            L = self.lanes[k % len(self.lanes)]
             i = k % len(self.pcm)
             with torch.cuda.stream(L["s"]):
                 self.fe.run(self.pcm[i], self.rows[i], out=L["logmel"], workspace=L["fe_ws"])
@@ -434,7 +435,8 @@ def main_step(args, world, rank, dev):
         "data": "synthetic (48 kHz int16-quantised noise+chirps, seeded), seeded random-init model1",
         "config": {"workload": WORKLOAD, "model": "model1", "global_batch": n_win * world,
                    "seq_len": step.fe_s.win_len, "parallelism": f"dp{world}",
-                   "pipeline": "two batches in flight on two streams" if step.lanes is not None else
+                   "pipeline": f"{len(step.lanes)} batches in flight on {len(step.lanes)} streams"
+                               if step.lanes is not None else
                                "front end of batch k+1 on a second stream beside the CNN of batch k"
                                if step.pipeline else "serial",
                    "clip_pairs": f"{HEAD_PAIRS} resident clip pairs in rotation, one per step"},
@@ -480,7 +482,7 @@ def main_step(args, world, rank, dev):
                 el = timed(s2, n2, 5, 1)
             e = {"value": round(n2 * s2.n_win * SECONDS_PER_WINDOW / el, 1), "ms_per_step": round(1e3 * el / n2, 4),
                  "steps": n2, "dtype": prec + (" (fp16 log-mel)" if s2.logmel.dtype == torch.float16 else "")}
-            e["pipeline"] = 2 if s2.lanes is not None else int(s2.pipeline)
+            e["pipeline"] = len(s2.lanes) if s2.lanes is not None else int(s2.pipeline)
             if mode == "serial":
                 e["note"] = "front end and CNN back to back on one stream (no overlap across steps)"
             if mode == "cold":
