@@ -272,9 +272,17 @@ class BatchAnalyser:
         cur.wait_stream(lane.copy)
         L = _lib.lib()
         from .resample import resample_device
+        # every recording mono PCM16: the int16 and f32 offsets coincide, so one
+        # widening launch covers the batch
+        mono16 = all(r.dec.s16 is not None and r.dec.channels == 1 for r in recs)
+        if mono16 and total:
+            _lib.check(L.aa_pcm_s16_to_f32(_lib.dptr(s16), total, 1, _lib.dptr(pcm), _lib.stream_ptr(cur)),
+                       "aa_pcm_s16_to_f32")
         for r in recs:
             d = r.dec
             d.dev = pcm[r.off:r.off + d.n]
+            if mono16:
+                continue
             if d.s16 is not None and d.n:
                 _lib.check(L.aa_pcm_s16_to_f32(_lib.dptr(s16) + 2 * d.o16, d.n, d.channels,
                                                _lib.dptr(pcm) + 4 * r.off, _lib.stream_ptr(cur)),
