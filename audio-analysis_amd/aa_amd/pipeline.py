@@ -115,6 +115,7 @@ class Classifier:
         errs = [None] * R
         views = None  # per recording: per track window views (global sample offsets)
         logmel = rows = fe = None
+        status_host = status_views = None
         bird_labels = set()
         for group in groups:
             if len(group) > 1:
@@ -165,14 +166,11 @@ class Classifier:
                     rows = torch.from_numpy(pack_windows(flat, int(pcm.numel()), win_len=s.win_len)).to(dev)
                     status = torch.empty(len(flat), dtype=torch.int32, device=dev)
                     logmel = fe.run(pcm, rows, status=status, workspace=_grow(ws, "fe", fe.workspace_bytes(len(flat)), dev))
-                    st = status.cpu().numpy()
-                    if st.any():  # librosa valid_audio, per recording
-                        k = 0
-                        for i, rv in enumerate(views):
-                            nw = sum(len(tv) for tv in rv)
-                            if st[k:k + nw].any():
-                                errs[i] = ValueError("Audio buffer is not finite everywhere")
-                            k += nw
+                    # per-window status, read back with the first group's scores
+                    # (one host sync per batch, not two)
+                    status_host = torch.empty(len(flat), dtype=torch.int32, pin_memory=True)
+                    status_host.copy_(status, non_blocking=True)
+                    status_views = views
             else:
                 logging.info("Re using track data this will cuase problems if the STFT settings are "
                              "not the same for multiple models")
@@ -200,6 +198,16 @@ class Classifier:
             wb = torch.from_numpy(begin[sel]).to(dev)
             wc = torch.from_numpy(flat_counts[sel].astype(np.int32)).to(dev)
             means = track_mean(probs, wb, wc).cpu().numpy()
+            if status_host is not None:  # ready: the copy preceded the means on the stream
+                st = status_host.numpy()
+                status_host = None
+                if st.any():  # librosa valid_audio, per recording
+                    k = 0
+                    for i, rv in enumerate(status_views):
+                        nw = sum(len(tv) for tv in rv)
+                        if st[k:k + nw].any():
+                            errs[i] = ValueError("Audio buffer is not finite everywhere")
+                        k += nw
             row, t0 = 0, 0
             for i, (r, rc) in enumerate(zip(recs, counts)):
                 nt = len(rc)

@@ -8,7 +8,9 @@ windows (:547-551).  The MI355X shape of the same work: recordings are packed a
 few at a time into one batch -- one aa_fe_run over every window of every
 track of the batch, one aa_model_forward per ensemble model, one
 aa_track_mean -- and PCM reaches the device from pinned host buffers on a copy
-stream, double-buffered, so batch i+1's upload overlaps batch i's kernels.
+stream, double-buffered, so batch i+1's upload overlaps batch i's kernels,
+and the two buffer slots compute on their own streams, so batch i+1's
+kernels run beside batch i's.
 Per-track scores come back in one device->host copy per batch.  Every kernel
 works per window / per track, so each recording's scores are bit-identical to
 classifying it on its own.
@@ -60,7 +62,9 @@ class StreamRunner:
         self.max_windows, self.max_samples = int(max_windows), int(max_samples)
         self.stride, self.pad_short = segment_stride, pad_short_tracks
         self.copy_stream = torch.cuda.Stream(device=self.device)
-        self.compute_stream = torch.cuda.Stream(device=self.device)
+        # each slot computes on its own stream: batch i+1's kernels run beside
+        # batch i's (the slots own all their buffers), as the bench's
+        # two-stream step does
         self.slots = [self._slot() for _ in range(2)]
         self._next = 0
         # host staging copies, one recording per thread (numpy copies run
@@ -85,6 +89,7 @@ class StreamRunner:
             "fe_ws": torch.empty(max(self.fe.workspace_bytes(W), 256), dtype=torch.uint8, device=dev),
             "m_ws": torch.empty(max(max(m.workspace_bytes(W) for m in self.models), 256), dtype=torch.uint8,
                                 device=dev),
+            "ks": torch.cuda.Stream(device=dev),
             "uploaded": torch.cuda.Event(),
             "done": torch.cuda.Event(),
             "pending": None,
@@ -141,7 +146,7 @@ class StreamRunner:
             slot["h_win"].numpy()[:nw] = np.asarray(rows, dtype=np.int64)
             slot["h_tr"].numpy()[0, :nt] = begins
             slot["h_tr"].numpy()[1, :nt] = counts
-        cs, ks = self.copy_stream, self.compute_stream
+        cs, ks = self.copy_stream, slot["ks"]
         # (the slot's previous batch has finished: _drain above synchronised it)
         with torch.cuda.stream(cs):
             slot["d_pcm"][:off].copy_(slot["h_pcm"][:off], non_blocking=True)
