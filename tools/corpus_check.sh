@@ -1,6 +1,6 @@
 #!/bin/bash
-# corpus path check (through gpurun): the pipeline / batch / CLI GPU tests,
-# then configs[3] lines
+# corpus-path check (through gpurun): the pipeline / batch / CLI / corpus /
+# signal / stream GPU tests, configs[3] lines (3 runs) and the configs[2] stream line
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
