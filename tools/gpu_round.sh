@@ -26,3 +26,5 @@ done
 timeout -k 10 400 python bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err || { cat gpurun_out/bench.err; exit 7; }
 cat gpurun_out/kernel_stats_serial_bf16x3.txt
 tail -1 gpurun_out/bench.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 8; }
+tail -2 gpurun_out/smoke.log
