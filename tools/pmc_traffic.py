@@ -40,10 +40,20 @@ def last_step(ds):
     starts = [k for k, d in enumerate(ds) if "fe_stats" in d[1]]
     if len(starts) < 2:
         raise SystemExit("need at least two steps in the profile")
-    a = starts[-2]
-    b = starts[-1]
-    # the last step may be followed by copies; the step before it is complete
-    return ds[a:b]
+    # the last fe_stats whose step runs through to track_mean; runtime copies
+    # (__amd_rocclr_copyBuffer: parity read-backs, clip-pair rotation) that
+    # land inside the window are not launches of the step and are dropped
+    for a in reversed(starts):
+        step = []
+        for d in ds[a:]:
+            if "aa::" not in d[1]:
+                continue
+            if "fe_stats" in d[1] and step:
+                break
+            step.append(d)
+            if "track_mean" in d[1]:
+                return step
+    raise SystemExit("no complete step (fe_stats ... track_mean) in the profile")
 
 
 def main():
