@@ -424,14 +424,19 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
 //      melF[w][t][:] (frame-major: one contiguous row per frame) and the frame
 //      maximum -> pmax[w][t]
 // Block = 8 waves sharing one CSR image, 2 blocks per CU (16 waves: VGPRs
-// capped at 128).  Wave g of G takes frames g, g + G, ...; blocks are
-// renumbered so each XCD (block b runs on XCD b % 8) owns a contiguous range of
-// frames: neighbouring frames overlap by 4096 - hop samples and one L2 then
-// serves the overlap.
+// capped at 128).  Each XCD (block b runs on XCD b % 8) owns a contiguous
+// eighth of the frames -- neighbouring frames overlap by 4096 - hop samples
+// and one L2 then serves the overlap -- and its waves take them round-robin,
+// wave-major over its blocks, so the last partial round lands on every SIMD
+// (block-major over the whole grid left that round to the first XCDs: 16 frames
+// on their SIMDs against 12 elsewhere; 69.6 -> 64.0 us alone).
 // ---------------------------------------------------------------------------
 // band slots of the wave-per-frame kernel's CSR image: whole rounds of 64 lanes
 __host__ __device__ constexpr int fe_mel_slots(int n_mels) { return (n_mels + 63) / 64 * 64; }
 
+#ifndef AA_FE_ORDER
+#define AA_FE_ORDER 1  // frame -> wave order: 0 block-major (round 2), 1 per-XCD wave-major
+#endif
 #ifndef AA_FE_WPB
 #define AA_FE_WPB 8
 #endif
@@ -466,10 +471,22 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
     const float2 hwe = make_float2(te.x, -te.y), hwo = make_float2(to.x, -to.y);
     __syncthreads();                     // vmcnt(0): the CSR image has landed
 
+#if AA_FE_ORDER == 0
     const int nb = gridDim.x;  // a multiple of 8 (host)
     const int blk = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
     const int G = nb * kWpb;
     for (int fi = blk * kWpb + wave; fi < n_frames; fi += G) {
+#else
+    // XCD x (block b runs on XCD b % 8) owns frames [x n / 8, (x + 1) n / 8);
+    // its waves take them round-robin, wave-major over its blocks, so the last,
+    // partial round is spread over every XCD, CU and SIMD (a block's waves w
+    // and w + 4 share a SIMD) instead of filling the first XCDs only
+    const int nbx = gridDim.x >> 3;  // blocks per XCD (grid a multiple of 8)
+    const int xcd = blockIdx.x & 7;
+    const int f_end = (int)((long long)(xcd + 1) * n_frames / 8);
+    const int G = nbx * kWpb;
+    for (int fi = (int)((long long)xcd * n_frames / 8) + wave * nbx + (blockIdx.x >> 3); fi < f_end; fi += G) {
+#endif
         const int w = fi / T;
         const int t = fi - w * T;
         const aa_window d = wins[w];

@@ -204,11 +204,15 @@ __global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(3, 
     // (a negative offset wraps past num_records)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)pcm, 0, n_samples * 4, 0x00020000);
 
-    const int nb = gridDim.x;  // a multiple of 8 (host)
-    const int blk = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
-    const int G = nb * kSnWpb;
+    // XCD x (block b runs on XCD b % 8) owns frames [x n / 8, (x + 1) n / 8),
+    // taken round-robin by its waves, wave-major over its blocks: the last
+    // partial round is spread over every SIMD (as fe_stft_mel_4096)
+    const int nbx = gridDim.x >> 3;  // blocks per XCD (grid a multiple of 8)
+    const int xcd = blockIdx.x & 7;
+    const int f_end = (int)((long long)(xcd + 1) * n_frames / 8);
+    const int G = nbx * kSnWpb;
     unsigned wmax = 0;
-    for (int fi = blk * kSnWpb + wave; fi < n_frames; fi += G) {
+    for (int fi = (int)((long long)xcd * n_frames / 8) + wave * nbx + (blockIdx.x >> 3); fi < f_end; fi += G) {
         int l2 = 2 * lane;  // opaque: keeps the 64 load offsets from being hoisted
         __asm__ volatile("" : "+v"(l2));
         float2 wk = wk1;

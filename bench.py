@@ -27,6 +27,7 @@ only collective is the final RCCL all-gather of per-track results (§8e).
 from __future__ import annotations
 
 import argparse
+import csv
 import json
 import os
 import socket
@@ -199,6 +200,38 @@ def load_traffic(n_dispatch, precision):
                 and len(d.get("kernels", [])) == n_dispatch):
             return d, path.relative_to(ROOT).as_posix()
     return None, None
+
+
+def load_profiled_stages(traffic, precision):
+    """Average duration (us) of each launch of one step from the committed
+    rocprofv3 --kernel-trace --stats summary of the serial step
+    (bench_kernel_stats_serial_<precision>.csv beside the PMC summary),
+    launches named by the PMC summary's per-dispatch kernel list; a launch that
+    dispatches a second kernel (the network tail's head_final) is charged both.
+    None when either summary is missing."""
+    if traffic is None:
+        return None
+    for path in sorted((ROOT / "profiles").glob(f"*/bench_kernel_stats_serial_{precision}.csv"), reverse=True):
+        try:
+            rows = list(csv.DictReader(path.open()))
+        except OSError:
+            continue
+        avg = {r["Name"]: float(r["AverageNs"]) / 1e3 for r in rows}
+
+        def find(name):
+            hit = [v for k, v in avg.items() if k.startswith(name[:100])]
+            return hit[0] if len(hit) == 1 else None
+
+        durs = [find(k["name"]) for k in traffic["kernels"][:-1]]  # the last is track_mean
+        if any(d is None for d in durs):
+            continue
+        head = find("aa::head_final")
+        if head is not None:
+            for i, k in enumerate(traffic["kernels"][:-1]):
+                if "conv_tail" in k["name"]:
+                    durs[i] += head
+        return path.relative_to(ROOT).as_posix(), durs
+    return None
 
 
 class Step:
@@ -434,6 +467,20 @@ def main_step(args, world, rank, dev):
             b, pk, a = "mfma", PEAK[args.precision], c["flops"] / (c["avg_ms"] * 1e-3) / 1e12
         per[c["name"]] = {"bound": b, "achieved": round(a, 1), "frac": round(a / pk, 4)}
     roofline["stages"] = per
+    # the same stages from a profile pass: rocprofv3's kernel trace of the
+    # serial step (committed summary), kernels matched to launches in dispatch
+    # order through the PMC summary's kernel names
+    prof = load_profiled_stages(tr, args.precision)
+    if prof is not None:
+        stats_path, durs = prof
+        ps = {}
+        for c, us in zip(calib, durs):
+            b = per[c["name"]]["bound"]
+            pk = {"valu": VALU_F32_PEAK, "hbm": HBM_PEAK_GBS}.get(b, PEAK[args.precision])
+            a = c["bytes"] / (us * 1e-6) / 1e9 if b == "hbm" else c["flops"] / (us * 1e-6) / 1e12
+            ps[c["name"]] = {"bound": b, "avg_us": round(us, 2), "achieved": round(a, 1), "frac": round(a / pk, 4)}
+        roofline["stages_profiled"] = ps
+        roofline["stages_profiled_source"] = stats_path
     # whole step against the CNN's matrix roofline + the front end's VALU one
     step_flops = sum(c["flops"] for c in calib)
     roofline["step_tflops"] = round(step_flops / (elapsed / args.steps) / 1e12, 2)
