@@ -665,8 +665,11 @@ def main_corpus(args, world, rank, dev):
     ppg = max(1, args.procs_per_gpu)
     cdev = dev if (world > 1 and dist.get_backend() == "nccl") else torch.device("cpu")  # collectives
     n_gpus = max(1, world // ppg)
-    # warm-up (untimed): plans, kernels, model upload, the pinned staging slots
-    corpus.run([files[0]] * (4 * max(args.batch, 1)), models, rank=0, world=1, batch=args.batch)
+    # warm-up (untimed): plans, kernels, model upload, and every pinned staging
+    # slot the timed run holds (aa_amd.batch: (lanes + 2) batches; a slot pool
+    # grown inside the timed run allocated ~6 MB of pinned memory per slot there)
+    lanes = int(os.environ.get("AA_BATCH_LANES", "3"))
+    corpus.run([files[0]] * (max(4, lanes + 2) * max(args.batch, 1)), models, rank=0, world=1, batch=args.batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
