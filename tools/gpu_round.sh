@@ -23,6 +23,14 @@ for P in $PRECS; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats_serial_$P -o run -- python3 bench.py --precision $P --steps 25 --warmup 5 --cpu-seconds 0 --secondary= --pipeline 0 > gpurun_out/stats_serial_$P.log 2>&1 || exit 6
   python tools/prof_summary.py gpurun_out/stats_serial_$P > gpurun_out/kernel_stats_serial_$P.txt
 done
+# the bench line reads the traffic and serial-trace summaries from profiles/:
+# on the box, give it this pass's (PROFILE_DIR, e.g. profiles/r03; the local
+# copy is made from gpurun_out/ afterwards)
+if [ -n "$PROFILE_DIR" ]; then
+  for P in $PRECS; do
+    cp gpurun_out/pmc_traffic_$P.json "$PROFILE_DIR/" && cp gpurun_out/stats_serial_$P/run_kernel_stats.csv "$PROFILE_DIR/bench_kernel_stats_serial_$P.csv" || exit 9
+  done
+fi
 timeout -k 10 400 python bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err || { cat gpurun_out/bench.err; exit 7; }
 cat gpurun_out/kernel_stats_serial_bf16x3.txt
 tail -1 gpurun_out/bench.log
