@@ -232,8 +232,63 @@ def _fp8(x):
     return x.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).to(torch.float32)
 
 
+# fp8 MFMA accumulation (gfx950, measured by tools/mfma_fp8_precision.hip,
+# profiles/r03/fp8_mfma_precision.txt): v_mfma_f32_16x16x32_fp8_fp8 and the
+# K = 128 f8f6f4 form sum each group of 8 products (one lane's 8 bytes of a
+# 32-deep chunk: 8 consecutive input channels of one tap) after truncating
+# every product toward zero to a multiple of 2^(E - 13), E the largest sum of
+# operand exponents (ea + eb) in the group; one instruction adds its groups to
+# the f32 accumulator and rounds.
+MFMA_FP8_WIN = 13
+
+
+def _fp8_mfma_conv(x: torch.Tensor, wq: torch.Tensor, k128: bool, lchunk: int = 256) -> torch.Tensor:
+    """Valid conv of e4m3 activations x [N, C, H, W] with e4m3 weights wq
+    [O, C, kh, kw] (scaled), summed the way conv_mfma / conv_head do on the
+    fp8 MFMAs: chunk k = tap * C/32 + channel chunk, one instruction per chunk
+    (C = 32) or per four chunks (C >= 64, K = 128; the last padded), groups of
+    8 channels truncated as above, f32 rounding after every instruction.
+    Returns the f32 accumulator [N, O, Ho, Wo]."""
+    N, C, H, W = x.shape
+    O, _, kh, kw = wq.shape
+    assert C % 32 == 0
+    taps, cpc = kh * kw, C // 32
+    nch = taps * cpc
+    per = 4 if k128 else 1
+    nst = -(-nch // per)
+    Ho, Wo = H - kh + 1, W - kw + 1
+    L = Ho * Wo
+    # e4m3 x e4m3 products, their truncation to a power-of-two grid and a
+    # group's sum of 8 are exact in f32; chunks and steps are summed in f64
+    cols = F.unfold(x.float(), (kh, kw)).view(N, C, taps, L).permute(0, 3, 2, 1)  # [N, L, taps, C]
+    xc = cols.reshape(N, L, nch, 4, 8)  # chunk k = t * cpc + cc, group g = channels 8g..8g+7
+    wc = wq.float().view(O, C, taps).permute(0, 2, 1).reshape(O, nch, 4, 8).contiguous()
+    def e4m3_exp(v):  # unbiased exponent field of e4m3 values (subnormal / zero: -6)
+        return torch.clamp(torch.frexp(v).exponent - 1, min=-6).to(torch.int32)
+
+    ex, ew = e4m3_exp(xc), e4m3_exp(wc)
+    out = torch.empty(N, L, O, dtype=torch.float32)
+    for n in range(N):
+        for l0 in range(0, L, lchunk):
+            p = xc[n, l0:l0 + lchunk, None] * wc[None]  # [l, O, nch, 4, 8]
+            # grid 2^(max over the group of (ea + eb) - WIN): the operands' e4m3
+            # exponents (subnormals and zero at the minimum, -6), not the
+            # product's own (1.5 x 1.5 = 2.25 keeps the finer grid)
+            es = (ex[n, l0:l0 + lchunk, None] + ew[None]).amax(-1, keepdim=True)
+            inv = torch.ldexp(torch.ones_like(p[..., :1]), MFMA_FP8_WIN - es)
+            p.mul_(inv).trunc_().div_(inv)
+            cs = p.sum(-1).double().sum(-1)  # [l, O, nch]: one chunk's groups
+            if per > 1:
+                cs = F.pad(cs, (0, nst * per - nch)).view(cs.shape[0], O, nst, per).sum(-1)
+            acc = torch.zeros(cs.shape[:2], dtype=torch.float32)
+            for st in range(nst):
+                acc = (acc.double() + cs[..., st]).float()
+            out[n, l0:l0 + lchunk] = acc
+    return out.permute(0, 2, 1).reshape(N, O, Ho, Wo)
+
+
 @torch.no_grad()
-def forward_fp8_emulated(path, x_nhwc: np.ndarray, first_bf16=True):
+def forward_fp8_emulated(path, x_nhwc: np.ndarray, first_bf16=True, mfma=True):
     """CPU emulation of libaa's AA_PREC_FP8 numerics (the checker of that mode,
     not a reference result): BN folded into the conv (per output channel), a
     C_in = 1 first conv with bf16 weights on the f32 input (first_bf16: the
@@ -241,7 +296,10 @@ def forward_fp8_emulated(path, x_nhwc: np.ndarray, first_bf16=True):
     later conv's folded weights quantised per output channel to e4m3fn with
     the largest |w| at 240 and dequantised after the f32 accumulation,
     pre-pool values rounded to bf16 (the epilogue tile), every stored
-    activation rounded to e4m3fn.  A 1x1 conv followed by GlobalMaxPool2D is
+    activation rounded to e4m3fn.  mfma: the convs summed as the fp8 MFMAs
+    sum (_fp8_mfma_conv: per 8-product group truncation, f32 rounding per
+    instruction) with the epilogue's single-rounding fmaf; False: torch's f32
+    conv.  A 1x1 conv followed by GlobalMaxPool2D is
     the head kernel (max of the f32 values); any other conv followed by it
     stores e4m3fn activations that the global max then reads.  Returns
     (logits, probs)."""
@@ -279,7 +337,11 @@ def forward_fp8_emulated(path, x_nhwc: np.ndarray, first_bf16=True):
             amax = w.abs().amax(dim=(1, 2, 3))
             s = torch.where(amax > 0, 240.0 / amax, torch.ones_like(amax))
             wq = _fp8(w * s[:, None, None, None])
-            y = F.conv2d(x, wq) * (1.0 / s)[None, :, None, None] + b[None, :, None, None]
+            if mfma:  # the fp8 MFMAs' own summation, then the epilogue's fmaf(acc, 1/s, bias)
+                acc = _fp8_mfma_conv(x, wq, k128=w.shape[1] >= 64)
+                y = (acc.double() * (1.0 / s).double()[None, :, None, None] + b.double()[None, :, None, None]).float()
+            else:
+                y = F.conv2d(x, wq) * (1.0 / s)[None, :, None, None] + b[None, :, None, None]
         act, pool, head = None, None, False
         while i < len(arch) and arch[i]["type"] in ("leakyrelu", "maxpool2d", "globalmaxpool2d", "activation"):
             k = arch[i]["type"]

@@ -18,8 +18,10 @@ def test_e4m3fn_known_values():
 
 def test_fp8_emulation_close_to_f32(model_root):
     path = model_root / "model1" / "audioModel.safetensors"
-    x = calibration_input(4, 160, 226, True, np.random.default_rng(3))
+    x = calibration_input(2, 160, 226, True, np.random.default_rng(3))
     el, ep = cnn_oracle.forward_fp8_emulated(path, x)
+    fl, _ = cnn_oracle.forward_fp8_emulated(path, x, mfma=False)
+    assert np.abs(el - fl).max() < 0.5  # the MFMA sums vs torch's f32 conv: truncation-sized
     rl, rp = cnn_oracle.forward(path, x)
     assert np.isfinite(el).all()
     # e4m3 activations: a 3-bit mantissa through six layers

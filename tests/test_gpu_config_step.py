@@ -96,19 +96,24 @@ def test_config4_step(step, gpu):
     test_gpu_cnn.py), and the delta to the fp32 oracle reported."""
     from aa_amd.model import Model
     from oracle import cnn_oracle
-    from tests.test_gpu_cnn import FP8_EMU_MAX, FP8_EMU_MEAN
+    from tests.test_gpu_cnn import FP8_EMU_MAX, FP8_EMU_MEAN, FP8_F32EMU_MAX, FP8_F32EMU_MEAN
     lm16 = step["logmel"].half()
     m = Model(step["path"], lm16.shape[1:], precision="fp8", device=gpu)
     lg, _ = m.forward(lm16)
     torch.cuda.synchronize()
     lg = lg.cpu().numpy()
-    elg, _ = cnn_oracle.forward_fp8_emulated(step["path"], lm16.float().cpu().numpy())
-    d_emu = np.abs(lg - elg)
+    x16 = lm16.float().cpu().numpy()
+    # all 64 windows against the f32-conv emulation, 3 against the MFMA-sum one
+    elg, _ = cnn_oracle.forward_fp8_emulated(step["path"], x16, mfma=False)
+    mlg, _ = cnn_oracle.forward_fp8_emulated(step["path"], x16[:3])
+    d_emu, d_mfma = np.abs(lg - elg), np.abs(lg[:3] - mlg)
     d_ref = np.abs(lg - step["ref_logits"])
-    print(f"configs[4] fp16 log-mel + fp8: max|dlogit| vs emulation {d_emu.max():.3e} (mean {d_emu.mean():.3e}), "
+    print(f"configs[4] fp16 log-mel + fp8: max|dlogit| vs the MFMA emulation {d_mfma.max():.3e} (mean {d_mfma.mean():.3e}), "
+          f"vs the f32-conv emulation {d_emu.max():.3e} (mean {d_emu.mean():.3e}), "
           f"vs fp32 oracle {d_ref.max():.3e} (mean {d_ref.mean():.3e})")
     assert np.isfinite(lg).all()
-    assert d_emu.max() <= FP8_EMU_MAX and d_emu.mean() <= FP8_EMU_MEAN
+    assert d_mfma.max() <= FP8_EMU_MAX and d_mfma.mean() <= FP8_EMU_MEAN
+    assert d_emu.max() <= FP8_F32EMU_MAX and d_emu.mean() <= FP8_F32EMU_MEAN
     assert d_ref.max() <= LOOSE["fp8"]
 
 
