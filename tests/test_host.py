@@ -109,3 +109,15 @@ def test_layer_table_from_model_file(model_root):
     assert (conv.op, conv.kh, conv.kw, conv.filters) == (1, 3, 3, 32)
     k = tensors["conv1.kernel"].reshape(-1)
     assert np.array_equal(blob[conv.off[0]:conv.off[0] + k.size], k)
+
+
+def test_fe_db_row_by_float_reciprocal():
+    """fe_db (csrc/aa_frontend.hip) finds an element's tile row as
+    int((idx + 0.5f) * (1.0f / n_mels)) in f32 instead of idx / n_mels: exact
+    for every tile the host can launch (at most 64 KiB of [tile_t][n_mels + 1]
+    floats, so idx < 2^14)."""
+    for n in range(1, 4097):
+        inv = np.float32(1) / np.float32(n)
+        idx = np.arange(16384, dtype=np.int64)
+        q = ((idx.astype(np.float32) + np.float32(0.5)) * inv).astype(np.int32)
+        assert (q == idx // n).all(), n
