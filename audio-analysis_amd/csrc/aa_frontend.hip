@@ -79,11 +79,20 @@ __global__ __launch_bounds__(256) void fe_stats(const float* __restrict__ pcm,
         }
         const int nb = (n - head) / 4;
         const float4* q = reinterpret_cast<const float4*>(p + head);
-        for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-            float4 x = q[i];
-            bad |= !isfinite(x.x) | !isfinite(x.y) | !isfinite(x.z) | !isfinite(x.w);
-            mn = fminf(fminf(mn, x.x), fminf(x.y, fminf(x.z, x.w)));
-            mx = fmaxf(fmaxf(mx, x.x), fmaxf(x.y, fmaxf(x.z, x.w)));
+        // four independent loads in flight per thread before any is consumed
+        // (past the end a lane re-reads the last float4: min / max / the
+        // non-finite flag do not change under duplicates)
+        constexpr int U = 4;
+        for (int i = threadIdx.x; i < nb; i += U * blockDim.x) {
+            float4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = q[min(i + u * (int)blockDim.x, nb - 1)];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                bad |= !isfinite(x[u].x) | !isfinite(x[u].y) | !isfinite(x[u].z) | !isfinite(x[u].w);
+                mn = fminf(fminf(mn, x[u].x), fminf(x[u].y, fminf(x[u].z, x[u].w)));
+                mx = fmaxf(fmaxf(mx, x[u].x), fmaxf(x[u].y, fmaxf(x[u].z, x[u].w)));
+            }
         }
         for (int i = head + nb * 4 + threadIdx.x; i < n; i += blockDim.x) {
             float x = p[i];
@@ -370,8 +379,9 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
         __syncthreads();  // P / buffers reused by the next frame
     }
     // staged [n_mels][nf] tile -> melS[w][m][f0 .. f0 + nf)
+    const float inv_nm = 1.0f / (float)n_mels;  // exact row below 2^21 (as in fe_db)
     for (int idx = tid; idx < nf * n_mels; idx += NT) {  // frame-major rows
-        const int f = idx / n_mels, m = idx - f * n_mels;
+        const int f = (int)(((float)idx + 0.5f) * inv_nm), m = idx - f * n_mels;
         melS[((size_t)w * T + f0 + f) * n_mels + m] = melT[m * kFpb + f];
     }
     // item max -> blkmax[w][fb]
