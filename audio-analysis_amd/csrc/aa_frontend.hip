@@ -788,7 +788,10 @@ __global__ __launch_bounds__(256) void fe_db(const float* __restrict__ melF, con
     // holds at most 2^14 elements), ~35 VALU cheaper than an integer divide
     const float inv_nm = 1.0f / (float)n_mels;
     const int tsh = __builtin_ctz(tile_t);  // tile_t is a power of two (host)
-    constexpr int U = 8;  // loads in flight per thread before any is consumed
+#ifndef AA_FE_DB_U
+#define AA_FE_DB_U 8
+#endif
+    constexpr int U = AA_FE_DB_U;  // loads in flight per thread before any is consumed
     // the first batch of rows is issued before the window's reference max
     // (independent loads: their latencies overlap instead of adding up)
     float v[U];
