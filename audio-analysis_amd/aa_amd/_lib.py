@@ -154,6 +154,7 @@ _SIGS = {
                                   C.c_void_p]),
     "aa_sn_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.c_void_p,
                             C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "aa_sn_spectrogram": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p]),
     "aa_sn_components_from_mask": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t,
                                              C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "aa_flac_info": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(FlacInfo)]),
@@ -174,9 +175,9 @@ def lib():
             try:
                 f = getattr(h, name)
             except AttributeError:
-                if os.environ.get("AA_LIB"):
+                if os.environ.get("AA_LIB_AB"):
                     continue  # an older A/B build (tools/ab_head.py) lacks newer entry points
-                raise
+                raise AAError(f"{LIB_PATH} lacks {name}: a stale libaa.so (rebuild with __graft_entry__.build())")
             f.restype = res
             f.argtypes = args
         v = h.aa_abi_version()

@@ -214,6 +214,7 @@ class _Lane:
 
 
 SN_CAP = 4096   # components per recording kept in the batch slots
+PREFETCH = 2    # batches decoded ahead of the newest batch a lane has taken
 _SN_LOCK = __import__("threading").Lock()
 SN_HEAD = 64    # component rows read back with the counts (more: a second copy)
 
@@ -464,8 +465,11 @@ class BatchAnalyser:
         K = self.K
         lanes = [_Lane(self.dev) for _ in range(min(self.n_lanes, -(-len(jobs) // K)))]
         slot_bytes = max(os.path.getsize(p) for _, p in jobs) + 4096
-        # slots: every lane's batch plus two batches of prefetch
-        pool = slot_pool(min(len(jobs), (len(lanes) + 2) * K), slot_bytes)
+        # slots: every lane's batch plus PREFETCH batches decoded ahead of the
+        # newest batch a lane has taken -- exactly the batches that can hold
+        # slots at once, so a decode never waits for a slot (a waiting decode
+        # of a later batch could otherwise hold the slots the oldest batch needs)
+        pool = slot_pool(min(len(jobs), (len(lanes) + PREFETCH) * K), slot_bytes)
 
         def load(job):
             idx, path = job
@@ -481,7 +485,7 @@ class BatchAnalyser:
         lock = threading.Lock()
         batches = [jobs[b:b + K] for b in range(0, len(jobs), K)]
         with ThreadPoolExecutor(max_workers=self.workers) as io:
-            futs = {}  # batch index -> its decode futures, submitted two batches ahead
+            futs = {}  # batch index -> its decode futures, submitted PREFETCH batches ahead
             state = {"next": 0, "submitted": 0}
 
             def submit_upto(b):
@@ -503,7 +507,7 @@ class BatchAnalyser:
                             if b >= len(batches):
                                 return
                             state["next"] += 1
-                            submit_upto(b + 1 + len(lanes))
+                            submit_upto(b + 1 + PREFETCH)
                             fb = futs.pop(b)
                         t = time.perf_counter()
                         items = [f.result() for f in fb]
@@ -519,7 +523,7 @@ class BatchAnalyser:
                         prof.dump_stats(f"{os.environ['AA_BATCH_CPROFILE']}.{time.monotonic_ns()}")
 
             with lock:
-                submit_upto(len(lanes) + 1)
+                submit_upto(len(lanes) + PREFETCH)
             threads = [threading.Thread(target=worker, args=(ln,), daemon=True) for ln in lanes]
             for th in threads:
                 th.start()

@@ -90,6 +90,19 @@ class SignalDetector:
         _lib.check(rc, "aa_sn_run")
         return self._collect()
 
+    def spectrogram(self, pcm, stream=None):
+        """np.abs(librosa.stft(frames, n_fft=4096, hop_length=hop)) (:654) of a
+        device float32 recording, in the reference's precision (f64 transform,
+        complex64 rounding, numpy's magnitude): a device float32 [2049, F]
+        view of a frame-major [F, 2049] tensor."""
+        n = int(pcm.numel())
+        F = self.n_frames(n)
+        out = torch.empty((F, N_BINS), dtype=torch.float32, device=self.device)
+        rc = _lib.lib().aa_sn_spectrogram(self._h, _lib.dptr(pcm) if n else 0, n, _lib.dptr(out), N_BINS,
+                                          _lib.stream_ptr(stream))
+        _lib.check(rc, "aa_sn_spectrogram")
+        return out.t()
+
     def components_from_mask(self, mask, n_frames, stream=None) -> np.ndarray:
         """The same from a device int64 [2049, words] mask (aa_sn_run's
         mask_out layout): morphology, components, size filter."""

@@ -1,6 +1,8 @@
 // libaa.so: ABI version and the thread-local error string.
 #include <cstdarg>
 #include <cstdio>
+#include <mutex>
+#include <unordered_map>
 
 #include "aa_common.h"
 
@@ -11,6 +13,21 @@ void set_error(const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof(g_err), fmt, ap);
     va_end(ap);
+}
+
+// Per-kernel dynamic-LDS opt-in, raised to the largest size asked for.  Lane
+// threads launch the same kernels concurrently, so the high-water marks sit
+// behind one mutex (a plain static per call site would be a data race).
+int ensure_dyn_lds(const void* kernel, size_t bytes) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, size_t> granted;
+    std::lock_guard<std::mutex> g(mu);
+    size_t& have = granted[kernel];
+    if (bytes > have) {
+        AA_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        have = bytes;
+    }
+    return AA_OK;
 }
 }  // namespace aa
 

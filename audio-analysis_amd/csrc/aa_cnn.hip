@@ -1152,11 +1152,7 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
                        first->mag_exp, first->Hin, first->Win, s.lm_f16};
     }
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
-    static size_t attr = 0;
-    if (lds > attr) {
-        AA_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = lds;
-    }
+    AA_DYN_LDS(k, lds);
     const int tiles_h = (s.Hout * POOL + TH - 1) / TH;
     const int tiles_w = (s.Wout * POOL + TW - 1) / TW;
     dim3 grid(tiles_h * tiles_w, s.cout_pad / BN, n);
@@ -1267,11 +1263,7 @@ static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream
                        first->mag_exp, first->Hin, first->Win, s.lm_f16};
     }
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
-    static size_t attr = 0;
-    if (lds > attr) {
-        AA_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = lds;
-    }
+    AA_DYN_LDS(k, lds);
     const int tiles_h = (s.Hout * POOL + TH - 1) / TH;
     const int tiles_w = (s.Wout * POOL + TW - 1) / TW;
     dim3 grid(tiles_h * tiles_w, s.cout_pad / BN, n);
@@ -1290,11 +1282,7 @@ static int launch_wg(const Stage& s, const void* in, void* out, int n, hipStream
              "conv %s: one window's activations exceed 2 GiB", s.name.c_str());
     const size_t lds = wg_lds_bytes<KH, BN, TH, TW>();
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
-    static size_t attr = 0;
-    if (lds > attr) {
-        AA_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = lds;
-    }
+    AA_DYN_LDS(k, lds);
     const int tiles_h = (s.Hout * POOL + TH - 1) / TH;
     const int tiles_w = (s.Wout * POOL + TW - 1) / TW;
     dim3 grid(tiles_h * tiles_w, s.cout_pad / BN, n);
@@ -1373,11 +1361,7 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
             const int tiles_h = (c.Hc + TH - 1) / TH, tiles_w = (c.Wc + TW - 1) / TW;
             auto k = conv_tail_x3<1, 3, 128, 5, TH, TW>;
             constexpr size_t lds = tail_lds_bytes<1, 3, 128, TH, TW>();
-            static bool attr = false;
-            if (!attr) {
-                AA_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                attr = true;
-            }
+            AA_DYN_LDS(k, lds);
             float* part = static_cast<float*>(out);
             hipLaunchKernelGGL(k, dim3(tiles_h * tiles_w, 1, n), dim3(TAIL_NW * 64), lds, st, (const float*)in, c.Hin,
                                c.Win, (const bf16*)c.d_w, c.d_b, c.Hc, c.Wc, tiles_w, c.act, c.alpha,

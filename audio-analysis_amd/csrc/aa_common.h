@@ -46,6 +46,14 @@ void set_error(const char* fmt, ...);
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Raise `kernel`'s dynamic-LDS limit to at least `bytes` (thread-safe, aa_api.cpp).
+int ensure_dyn_lds(const void* kernel, size_t bytes);
+#define AA_DYN_LDS(kernel, bytes)                                                    \
+    do {                                                                             \
+        const int rc_ = ::aa::ensure_dyn_lds((const void*)(kernel), (bytes));        \
+        if (rc_ != AA_OK) return rc_;                                                \
+    } while (0)
+
 // HIP-event timing of selected launches (bench.py's roofline): a pair of
 // events on the launch stream around each timed launch, recycled through a
 // pool.  Only the stages named in `mask` are timed, so an untimed launch

@@ -867,12 +867,7 @@ static int launch_stft(const FePlan& p, const float* pcm, const aa_window* wins,
                        const float4* stats, float* melS, float* blkmax, hipStream_t st) {
     const size_t lds = fe_lds_bytes(p);
     AA_CHECK(lds <= 150 * 1024, AA_ERR_UNSUPPORTED, "fe: hop %d needs %zu B of LDS", p.cfg.hop, lds);
-    static size_t attr_set = 0;  // dynamic LDS opt-in already granted (static LDS comes on top)
-    if (lds > attr_set) {
-        AA_HIP(hipFuncSetAttribute((const void*)fe_stft_mel<NFFT, PM>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr_set = lds;
-    }
+    AA_DYN_LDS((fe_stft_mel<NFFT, PM>), lds);  // dynamic LDS opt-in (static LDS comes on top)
     const int n_items = p.nfblk * n_win;
     // persistent grid: as many blocks as fit (LDS-limited) on 256 CUs
     const int per_cu = std::max(1, (int)((160 * 1024) / (lds + 256)));
@@ -904,12 +899,7 @@ static int launch_stft4096(const FePlan& p, const float* pcm, const aa_window* w
                            const float4* stats, float* melS, float* pmax, hipStream_t st) {
     const size_t lds = fe_lds_bytes4096(p);
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "fe4096: %zu B of LDS", lds);
-    static size_t attr_set = 0;
-    if (lds > attr_set) {
-        AA_HIP(hipFuncSetAttribute((const void*)fe_stft_mel_4096<PM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds));
-        attr_set = lds;
-    }
+    AA_DYN_LDS(fe_stft_mel_4096<PM>, lds);
     const int n_frames = p.T * n_win;
     // persistent grid: blocks resident together (LDS-limited, 2 per CU at the
     // CFG filterbank), a multiple of 8 for the XCD renumbering

@@ -337,9 +337,12 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
     std::vector<std::pair<size_t, size_t>> live;  // [begin, end) of buffers in use
     size_t peak = 0;
     std::vector<std::vector<int>> frees(n_nodes + 1);
+    // per-window sizes rounded up to 16 floats: every buffer starts 64-B
+    // aligned, so the float4 loads / stores of the kernels never straddle
+    auto node_sz = [&](int k) { return align_up((size_t)G->nodes[k].H * G->nodes[k].W * G->nodes[k].C, 16); };
     for (int i = 0; i < n_nodes; ++i) {
         GNode& N = G->nodes[i];
-        const size_t sz = (size_t)N.H * N.W * N.C;
+        const size_t sz = node_sz(i);
         std::sort(live.begin(), live.end());
         size_t at = 0;
         for (auto& iv : live) {
@@ -352,8 +355,7 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
         // release the inputs whose last use is this node
         for (int k : {N.d.in0, N.d.in1}) {
             if (k < 0 || G->nodes[k].last_use != i) continue;
-            auto it = std::find(live.begin(), live.end(),
-                                std::make_pair(G->nodes[k].off, G->nodes[k].off + (size_t)G->nodes[k].H * G->nodes[k].W * G->nodes[k].C));
+            auto it = std::find(live.begin(), live.end(), std::make_pair(G->nodes[k].off, G->nodes[k].off + node_sz(k)));
             if (it != live.end()) live.erase(it);
         }
         // a node nobody reads (a dangling branch) frees itself

@@ -3,15 +3,14 @@
 //
 // Launches (one stream, no host synchronisation inside aa_sn_run):
 //   sn_zero       the per-run counters (global max, run count, status) = 0
-//   sn_stft       |STFT| of the recording (n_fft 4096, centre zero padding,
-//                 periodic Hann), one wave per frame through the front end's
-//                 wave FFT (aa_wavefft.h).  The real split yields every bin:
-//                 the lane holding Z[k] and its mirror Z[2048 - k] forms
-//                 X[k] = E + W^k O and X[2048 - k] = conj(E - W^k O).  Writes
-//                 the frame-major magnitude S[f][0..2048] and the maximum,
-//                 and the frame's median over bins: radix select on the f32
-//                 bit patterns of the row still in registers, digits below the
-//                 row's common min/max prefix, 4 LDS histograms per wave
+//   sn_stft64     |STFT| of the recording (n_fft 4096, centre zero padding,
+//                 scipy's periodic Hann) in librosa's own precision: f64
+//                 window x f32 frame, an f64 FFT (128 threads per frame,
+//                 radix 16 x 16 x 8 through LDS, real split in registers),
+//                 rounded to complex64 and np.abs'd with numpy's f32 formula,
+//                 so S is the reference's S.  Writes the frame-major S[f][0..2048],
+//                 the maximum, and the frame's median over bins (block radix
+//                 select on the bit patterns)
 //   sn_transpose  S -> ST[bin][frame] (64 x 64 tiles through LDS), and the
 //                 frame thresholds c3 = 3 (colmed / a) (numpy's f32 steps)
 //   sn_select     per-bin median over frames: radix select over the ST row
@@ -39,7 +38,6 @@
 
 namespace aa {
 
-constexpr int kSnWpb = 4;      // waves per sn_stft block (3 blocks per CU: 3 waves per SIMD)
 constexpr int kSnBins = 2049;  // n_fft / 2 + 1
 constexpr int kSnLd = 2080;    // S row stride in floats (128-B aligned rows)
 constexpr int kSnHist = 256;   // radix-select buckets (8 bits per pass)
@@ -65,11 +63,8 @@ struct SnPlan {
     int kh_d = 0, kw_d = 0;  // cv2.dilate(ones((height, width))) (:683)
     int kh_e = 0, kw_e = 0;  // cv2.erode(ones((height // 10, width))) (:684)
     int wmin = 0, hmin = 0;  // kept: width >= wmin, height >= hmin (:689-691)
-    float2* d_tw = nullptr;      // exp(-2 pi i m / 2048), m < 2048
-    float2* d_tw4096 = nullptr;  // exp(-2 pi i k / 4096), k <= 2048
+    double2* d_tab = nullptr;  // sn_stft64's tables: window pairs [2048], tw1 [15][128], tw2 [16][128], tw3 [128]
 };
-
-__device__ __forceinline__ float mag(float re, float im) { return __builtin_amdgcn_sqrtf(fmaf(re, re, im * im)); }
 
 __device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
 #pragma unroll
@@ -80,12 +75,116 @@ __device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
     return v;
 }
 
+// sn_zero: the counters a run accumulates into (atomicMax / atomicAdd), one
+// launch for every recording of the batch instead of a memset per buffer
+__global__ void sn_zero(unsigned* __restrict__ gmax, int* __restrict__ counters, size_t pf, int32_t* __restrict__ n_out,
+                        int n_out_stride) {
+    const int i = threadIdx.x, k = blockIdx.x;
+    if (gmax && i < 16) sn_at(gmax, pf, k)[i] = 0u;
+    if (i < 16) sn_at(counters, pf, k)[i] = 0;
+    if (i < 2) n_out[(size_t)k * n_out_stride + i] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// signal_noise's |STFT| in the reference's own precision.  librosa 0.11 forms
+// each frame as the f64 Hann window times the f32 samples, transforms it with
+// numpy's f64 rfft and stores the result as complex64; np.abs of that array
+// (numpy's SIMD complex absolute value, loops_unary_complex) is
+// L * sqrtf(fmaf(r, r, 1)) with L = max(|re|, |im|), r = min / L, every step
+// a correctly rounded f32 operation.  sn_stft64 does the same: the transform
+// in f64 (its result agrees with pocketfft's to ~1e-16 relative, so the
+// complex64 rounding of the two agree except on values within that distance
+// of a rounding midpoint), then the f64 -> f32 rounding and numpy's
+// magnitude formula bit for bit.  That makes S -- and the medians, the mask
+// and the components built on it -- the reference's values, not an f32
+// approximation of them.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double2 dadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 dsub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 dmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 dnegi(double2 a) { return make_double2(a.y, -a.x); }  // a * (-i)
+
+constexpr double kCos8 = 0.92387953251128675613;  // cos(pi / 8)
+constexpr double kSin8 = 0.38268343236508977173;  // sin(pi / 8)
+constexpr double kRt2 = 0.70710678118654752440;   // sqrt(1 / 2)
+
+// a * W16^E, W16 = exp(-2 pi i / 16), for the exponents a DFT-16 and the
+// real split need (E in 0..9)
+template <int E>
+__device__ __forceinline__ double2 w16(double2 a) {
+    static_assert(E >= 0 && E <= 9, "w16");
+    if constexpr (E == 0) return a;
+    else if constexpr (E == 1) return make_double2(a.x * kCos8 + a.y * kSin8, a.y * kCos8 - a.x * kSin8);
+    else if constexpr (E == 2) return make_double2(kRt2 * (a.x + a.y), kRt2 * (a.y - a.x));
+    else if constexpr (E == 3) return make_double2(a.x * kSin8 + a.y * kCos8, a.y * kSin8 - a.x * kCos8);
+    else if constexpr (E == 4) return dnegi(a);
+    else if constexpr (E == 5) return make_double2(a.y * kCos8 - a.x * kSin8, -(a.x * kCos8 + a.y * kSin8));
+    else if constexpr (E == 6) return make_double2(kRt2 * (a.y - a.x), -kRt2 * (a.x + a.y));
+    else if constexpr (E == 7) return make_double2(a.y * kSin8 - a.x * kCos8, -(a.x * kSin8 + a.y * kCos8));
+    else if constexpr (E == 8) return make_double2(-a.x, -a.y);
+    else return make_double2(-(a.x * kCos8 + a.y * kSin8), a.x * kSin8 - a.y * kCos8);  // E == 9
+}
+
+__device__ __forceinline__ void ddft4(double2& a, double2& b, double2& c, double2& d) {  // natural order out
+    const double2 t0 = dadd(a, c), t1 = dsub(a, c), t2 = dadd(b, d), t3 = dnegi(dsub(b, d));
+    a = dadd(t0, t2);
+    c = dsub(t0, t2);
+    b = dadd(t1, t3);
+    d = dsub(t1, t3);
+}
+__device__ __forceinline__ void ddft8(double2 (&v)[8]) {  // natural order out
+    double2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    double2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    ddft4(e0, e1, e2, e3);
+    ddft4(o0, o1, o2, o3);
+    o1 = w16<2>(o1);
+    o2 = w16<4>(o2);
+    o3 = w16<6>(o3);
+    v[0] = dadd(e0, o0);
+    v[4] = dsub(e0, o0);
+    v[1] = dadd(e1, o1);
+    v[5] = dsub(e1, o1);
+    v[2] = dadd(e2, o2);
+    v[6] = dsub(e2, o2);
+    v[3] = dadd(e3, o3);
+    v[7] = dsub(e3, o3);
+}
+// 16-point DFT in place (radix 4 x 4): X[k] is left in v[dp16(k)]
+__device__ __forceinline__ constexpr int dp16(int k) { return 4 * (k & 3) + (k >> 2); }
+__device__ __forceinline__ void ddft16(double2 (&v)[16]) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) ddft4(v[b], v[4 + b], v[8 + b], v[12 + b]);  // v[4c + b] = Y_b[c]
+    v[5] = w16<1>(v[5]);
+    v[9] = w16<2>(v[9]);
+    v[13] = w16<3>(v[13]);
+    v[6] = w16<2>(v[6]);
+    v[10] = w16<4>(v[10]);
+    v[14] = w16<6>(v[14]);
+    v[7] = w16<3>(v[7]);
+    v[11] = w16<6>(v[11]);
+    v[15] = w16<9>(v[15]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ddft4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);  // v[4c + d] = X[c + 4d]
+}
+
+// np.abs of one complex64 value, numpy's SIMD formula (non-finite parts give
+// a NaN / inf magnitude, which the host reports as non-finite input)
+__device__ __forceinline__ float np_cabsf(double re64, double im64) {
+    const float re = (float)re64, im = (float)im64;  // complex128 -> complex64 (round to nearest)
+    const float x = fabsf(re), y = fabsf(im);
+    const float L = fmaxf(x, y), s = fminf(x, y);
+    const float r = (L == 0.f || s == __builtin_huge_valf()) ? 0.f : s / L;  // correctly rounded
+    float m = sqrtf(fmaf(r, r, 1.f)) * L;                                     // correctly rounded sqrt
+    if (re != re || im != im) m = __builtin_nanf("");
+    return m;
+}
+
 // The bucket of a 256-bucket histogram that holds `rank` (0-based), found by
-// one wave (lane owns buckets 4 lane .. 4 lane + 3).  *below: elements in
+// one wave; c: the lane's buckets 4 lane .. 4 lane + 3.  *below: elements in
 // lower buckets; *cnt: elements in the bucket.
-__device__ __forceinline__ unsigned hist_pick(const unsigned* hist, unsigned rank, int lane, unsigned* below,
-                                              unsigned* cnt) {
-    const uint4 c = reinterpret_cast<const uint4*>(hist)[lane];
+__device__ __forceinline__ unsigned hist_pick4(uint4 c, unsigned rank, int lane, unsigned* below, unsigned* cnt) {
     const unsigned s = c.x + c.y + c.z + c.w;
     const unsigned incl = wave_incl_scan(s, lane);
     const unsigned excl = incl - s;
@@ -105,194 +204,237 @@ __device__ __forceinline__ unsigned hist_pick(const unsigned* hist, unsigned ran
     *cnt = __shfl(cn, src, 64);
     return __shfl(dig, src, 64);
 }
-
-// sn_zero: the counters a run accumulates into (atomicMax / atomicAdd), one
-// launch for every recording of the batch instead of a memset per buffer
-__global__ void sn_zero(unsigned* __restrict__ gmax, int* __restrict__ counters, size_t pf, int32_t* __restrict__ n_out,
-                        int n_out_stride) {
-    const int i = threadIdx.x, k = blockIdx.x;
-    if (gmax && i < 16) sn_at(gmax, pf, k)[i] = 0u;
-    if (i < 16) sn_at(counters, pf, k)[i] = 0;
-    if (i < 2) n_out[(size_t)k * n_out_stride + i] = 0;
+__device__ __forceinline__ unsigned hist_pick(const unsigned* hist, unsigned rank, int lane, unsigned* below,
+                                              unsigned* cnt) {
+    return hist_pick4(reinterpret_cast<const uint4*>(hist)[lane], rank, lane, below, cnt);
 }
 
-// ---------------------------------------------------------------------------
+// sn_stft64 geometry: 128 threads per frame; the 2048 complex points z[n] =
+// x[2n] + i x[2n + 1] of the 4096-sample real frame, n = 128 n1 + 8 n2 + n3,
+// bins k = k1 + 16 k2 + 256 k3:
+//   1. thread (n2, n3): DFT-16 over n1, twiddle W256^(n2 k1)
+//   2. thread (k1, n3): DFT-16 over n2, twiddle W2048^(n3 (k1 + 16 k2))
+//   3. thread j owns columns m = k1 + 16 k2 = j and 256 - j (thread 0: 0 and
+//      128): DFT-8 over n3 gives Z[m + 256 k3], and Z[2048 - k] of every k it
+//      holds sits in its other column, so the real split needs no exchange:
+//      X[k] = E + W4096^k O, X[2048 - k] = conj(E - W4096^k O),
+//      E = (Z[k] + conj Z[2048 - k]) / 2, O = -i (Z[k] - conj Z[2048 - k]) / 2.
+// LDS: one 36,864-B buffer holds each exchange in turn (step-1 rows of 136
+// double2 per k1, step-2 columns of 9 double2: both read conflict-free by
+// ds_read_b128), then the frame's 2049 magnitudes and the median histograms.
+constexpr int kS64T = 128;
+constexpr int kS64R1 = 136;
+constexpr int kS64C2 = 9;
+constexpr int kS64Buf = 256 * kS64C2;  // double2
+constexpr int kS64Hist = 2176;         // unsigned offset of the histograms (after the magnitudes)
+constexpr int kS64TabTw1 = 2048, kS64TabTw2 = kS64TabTw1 + 15 * kS64T, kS64TabTw3 = kS64TabTw2 + 16 * kS64T,
+              kS64TabN = kS64TabTw3 + kS64T;  // double2 entries of SnPlan::d_tab
+static_assert(16 * kS64R1 <= kS64Buf && (kS64Hist + 1024) * 4 <= kS64Buf * 16, "sn_stft64 LDS");
+
 // The median over bins of one frame (numpy, odd count 2049: the middle
-// element) by radix select on the bit patterns, by the wave that holds the
-// frame: v[i] = bin lane + 64 i (i < 32), v[32] = bin 2048 (lane 0 only).
-// 8-bit digits start below the bits the frame's min and max share (a
-// spectrum spans a few binades: the first histogram then spreads over the
-// exponents present instead of piling onto a handful of counters), counted
-// in 4 LDS histogram copies (lane & 3 picks one: a frame's values crowd a
-// few buckets, and same-address LDS atomics serialise).  hists: the wave's
-// 4 x 256 unsigned.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ unsigned wave_median_2049(const unsigned (&v)[33], unsigned* hists, int lane) {
-    unsigned* myh = hists + (lane & 3) * kSnHist;
+// element) by radix select on the bit patterns of the block's 2049 values
+// (v[i] = bin t + 128 i, v[16] = bin 2048 on thread 0).  8-bit digits start
+// below the bits the frame's min and max share; one histogram copy per wave,
+// two sets used alternately so a pass needs two barriers.
+__device__ __forceinline__ unsigned block_median_2049(const unsigned (&v)[17], int t, unsigned* hist,
+                                                      unsigned* red) {
+    const int lane = t & 63, wv = t >> 6;
     unsigned mn = v[0], mx = v[0];
 #pragma unroll
-    for (int i = 1; i < 32; ++i) {
+    for (int i = 1; i < 16; ++i) {
         mn = min(mn, v[i]);
         mx = max(mx, v[i]);
     }
-    if (lane == 0) {
-        mn = min(mn, v[32]);
-        mx = max(mx, v[32]);
+    if (t == 0) {
+        mn = min(mn, v[16]);
+        mx = max(mx, v[16]);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
         mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
     }
-    if (mn == mx) return mn;
+    if (lane == 0) {
+        red[wv] = mn;
+        red[2 + wv] = mx;
+    }
+    uint4* h4 = reinterpret_cast<uint4*>(hist);
+    h4[t] = make_uint4(0u, 0u, 0u, 0u);
+    h4[t + kS64T] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    mn = min(red[0], red[1]);
+    mx = max(red[2], red[3]);
+    if (mn == mx) return mn;  // block-uniform
     const int hb = 31 - __clz(mn ^ mx);
     unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
     unsigned prefix = mn & pmask, rank = kSnBins / 2;
+    int set = 0;
 #pragma unroll 1
     for (int sh = hb - 7;; sh -= 8) {
-        const int shift = max(sh, 0);
+        const int shift = max(sh, 0);  // a last digit may repeat known prefix bits: harmless
+        unsigned* H = hist + set * 512 + wv * 256;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(hists + q * kSnHist)[lane] = make_uint4(0u, 0u, 0u, 0u);
-        wave_sync();
-#pragma unroll
-        for (int i = 0; i < 33; ++i)
-            if ((i < 32 || lane == 0) && (v[i] & pmask) == prefix) atomicAdd(&myh[(v[i] >> shift) & 255u], 1u);
-        wave_sync();
-        {  // fold the copies into copy 0 (lane owns buckets 4 lane .. 4 lane + 3)
-            uint4 t = reinterpret_cast<uint4*>(hists)[lane];
-#pragma unroll
-            for (int q = 1; q < 4; ++q) {
-                const uint4 u = reinterpret_cast<uint4*>(hists + q * kSnHist)[lane];
-                t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
-            }
-            reinterpret_cast<uint4*>(hists)[lane] = t;
-        }
-        wave_sync();
+        for (int i = 0; i < 16; ++i)
+            if ((v[i] & pmask) == prefix) atomicAdd(&H[(v[i] >> shift) & 255u], 1u);
+        if (t == 0 && (v[16] & pmask) == prefix) atomicAdd(&H[(v[16] >> shift) & 255u], 1u);
+        __syncthreads();
+        uint4 c = h4[set * 128 + lane];
+        const uint4 c2 = h4[set * 128 + 64 + lane];
+        c.x += c2.x;
+        c.y += c2.y;
+        c.z += c2.z;
+        c.w += c2.w;
+        h4[(set ^ 1) * 128 + t] = make_uint4(0u, 0u, 0u, 0u);  // the next pass's set
         unsigned below, cnt;
-        const unsigned dig = hist_pick(hists, rank, lane, &below, &cnt);
+        const unsigned dig = hist_pick4(c, rank, lane, &below, &cnt);
         prefix = (prefix & ~(255u << shift)) | (dig << shift);
         pmask |= 255u << shift;
         rank -= below;
-        wave_sync();
         if (shift == 0) break;
+        __syncthreads();
+        set ^= 1;
     }
     return prefix;
 }
 
-// ---------------------------------------------------------------------------
-// sn_stft: one wave per frame, persistent over frames (XCD-contiguous ranges
-// of frames like fe_stft_mel_4096: neighbouring frames share 4096 - hop
-// samples through one L2).  Register budget 168 (3 waves per SIMD): the wave
-// FFT and the 2-bin split need ~170 VGPRs; at the 128-VGPR budget of 4 waves
-// per SIMD they spill heavily.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64 * kSnWpb) __attribute__((amdgpu_waves_per_eu(3, 3))) void sn_stft(
-    const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const float2* __restrict__ tw,
-    const float2* __restrict__ tw4096, float* __restrict__ S, unsigned* __restrict__ gmax,
-    unsigned* __restrict__ colmed) {
-    extern __shared__ float lds[];
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    float2* wb = reinterpret_cast<float2*>(lds) + wave * kHalf;
-    const int k1 = lane >> 1, h = lane & 1;
-    float2 t1 = tw[lane];                 // W2048^c
-    float2 t8 = tw[(8 * lane) & 2047];    // W2048^(8c)
-    const float2 wk1 = tw4096[k1];        // W4096^k1
-    const float2 te = tw4096[2 * lane], to = tw4096[2 * lane + 1];
-    const float2 hwe = make_float2(te.x, -te.y), hwo = make_float2(to.x, -to.y);
+// sn_stft64: persistent blocks, XCD x (block b on XCD b % 8) owning frames
+// [x F / 8, (x + 1) F / 8) (neighbouring frames share 4096 - hop samples
+// through one L2).  Per frame: S row (stride ld; may be null), the running
+// maximum (gmax: atomicMax on the bit patterns, may be null) and the median
+// over bins (colmed, may be null).  win2: the f64 Hann window as pairs
+// (w[2n], w[2n + 1]); tw1 / tw2: the step-1 / step-2 twiddles per thread;
+// tw3: W4096^t (thread 0: W4096^128), the split's per-thread base.
+__global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) void sn_stft64(
+    const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const double2* __restrict__ win2,
+    const double2* __restrict__ tw1, const double2* __restrict__ tw2, const double2* __restrict__ tw3,
+    float* __restrict__ S, int ld, unsigned* __restrict__ gmax, unsigned* __restrict__ colmed) {
+    __shared__ double2 buf[kS64Buf];
+    __shared__ unsigned red[4];
+    const int t = threadIdx.x;
+    const bool z = t == 0;
     // the recording as a buffer view: centre padding and the ends read as 0
     // (a negative offset wraps past num_records)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)pcm, 0, n_samples * 4, 0x00020000);
-
-    // XCD x (block b runs on XCD b % 8) owns frames [x n / 8, (x + 1) n / 8),
-    // taken round-robin by its waves, wave-major over its blocks: the last
-    // partial round is spread over every SIMD (as fe_stft_mel_4096)
+    double2 wv[16];  // the thread's window pairs, the same in every frame
+#pragma unroll
+    for (int n1 = 0; n1 < 16; ++n1) wv[n1] = win2[128 * n1 + t];
+    const double2 tb = tw3[t];
+    const int k1b = t >> 3, n3b = t & 7;         // step 2
+    const int m1 = t, m2 = z ? 128 : 256 - t;    // step 3 columns
+    const int mA = z ? 128 : t;                  // split: first bin of slots 0..3
+    float* mag = reinterpret_cast<float*>(buf);
+    unsigned* hist = reinterpret_cast<unsigned*>(buf) + kS64Hist;
+    unsigned wmax = 0;
     const int nbx = gridDim.x >> 3;  // blocks per XCD (grid a multiple of 8)
     const int xcd = blockIdx.x & 7;
     const int f_end = (int)((long long)(xcd + 1) * n_frames / 8);
-    const int G = nbx * kSnWpb;
-    unsigned wmax = 0;
-    for (int fi = (int)((long long)xcd * n_frames / 8) + wave * nbx + (blockIdx.x >> 3); fi < f_end; fi += G) {
-        int l2 = 2 * lane;  // opaque: keeps the 64 load offsets from being hoisted
-        __asm__ volatile("" : "+v"(l2));
-        float2 wk = wk1;
-        __asm__ volatile("" : "+v"(wk.x), "+v"(wk.y));
-        float2 u[32];
+#pragma unroll 1
+    for (int fi = (int)((long long)xcd * n_frames / 8) + (blockIdx.x >> 3); fi < f_end; fi += nbx) {
+        // the twiddle tables are loop-invariant: an opaque index per frame keeps
+        // the compiler from hoisting their 31 loads into live registers
+        int ti = t;
+        __asm__ volatile("" : "+v"(ti));
+        double2 v[16];
         {
-            float2 y[32];
-            const int offe = fi * hop - 2048 + l2;
-            int offo = offe + 1;  // separate register: no merged 8-byte loads
-            __asm__ volatile("" : "+v"(offo));
+            const int off = fi * hop - 2048 + 2 * t;
 #pragma unroll
-            for (int r = 0; r < 32; ++r) y[r] = make_float2(load_view(rs, offe + 128 * r), load_view(rs, offo + 128 * r));
-            wave_hann(y, hwe, hwo, lane);
-            wave_fft_core(y, u, wb, lane, t1, t8);
-        }
-        // ---- real split, every bin: lane (k1, 0) holds Z[k], k = k1 + 32 j <
-        // 1024, reads the mirror Z[2048 - k] the h = 1 lanes stored, and forms
-        // |X[k]| and |X[2048 - k]|.  The magnitudes stream into the same buffer
-        // from the top down as the mirrors below are consumed: step j writes
-        // |X[k]| at float 2111 - 64 j - k1 and |X[2048 - k]| at 2079 - 64 j - k1,
-        // above every mirror a later step reads (float2 <= 1024 - 32 (j + 1)).
-        // |X[1024]| = |Z[1024]| (lane 1) goes to float 31. ----
-        const float mid = mag(u[dperm(0)].x, u[dperm(0)].y);
-        if (h) {
-#pragma unroll
-            for (int j = 0; j < 32; ++j) wb[k1 + 32 * j] = u[dperm(j)];  // Z[1024 + k1 + 32 j]
-        }
-        wave_sync();
-        float* P = reinterpret_cast<float*>(wb);
-        if (!h) {
-            const float2* mb = wb + (32 - k1);  // Z[2048 - k] at mb[32 (31 - j)]
-            float* pb = P + (95 - k1);          // |X[2048 - k]| at pb[64 (31 - j)], |X[k]| 32 above
-#pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                const float2 a = u[dperm(j)];
-                const float2 zb = mb[32 * (31 - j)];
-                const float2 b = (j == 0 && k1 == 0) ? a : zb;  // Z[0] is its own mirror
-                const float2 E = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
-                const float2 O = make_float2(0.5f * (a.y + b.y), -0.5f * (a.x - b.x));
-                float2 wj = cmul(wk, wconst128(j));  // W4096^k
-                __asm__ volatile("" : "+v"(wj.x), "+v"(wj.y));
-                const float2 q = cmul(wj, O);
-                pb[64 * (31 - j) + 32] = mag(E.x + q.x, E.y + q.y);
-                pb[64 * (31 - j)] = mag(E.x - q.x, E.y - q.y);
+            for (int n1 = 0; n1 < 16; ++n1) {
+                const float xe = load_view(rs, off + 256 * n1), xo = load_view(rs, off + 256 * n1 + 1);
+                v[n1] = make_double2((double)xe * wv[n1].x, (double)xo * wv[n1].y);
             }
         }
-        wave_sync();
-        if (lane == 1) P[31] = mid;
-        wave_sync();
-        // ---- the frame's row of S and its maximum ----
-        // bin lane + 64 i sits at float lb - 128 i (i < 16) / hb + 128 i (i >= 16)
-        unsigned v[33];  // v[32] = bin 2048 (counted by lane 0)
-        {
-            const int lb = 2111 - 64 * (lane >> 5) - (lane & 31);
-            const int hb = -1889 - 64 * ((64 - lane) >> 5) - ((64 - lane) & 31);
+        // ---- 1. DFT-16 over n1, twiddle, rows k1 ----
+        ddft16(v);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = __float_as_uint(P[lb - 128 * i]);
+        for (int k1 = 1; k1 < 16; ++k1) v[dp16(k1)] = dmul(v[dp16(k1)], tw1[(k1 - 1) * kS64T + ti]);
 #pragma unroll
-            for (int i = 16; i < 32; ++i) v[i] = __float_as_uint(P[hb + 128 * i]);
-            v[32] = __float_as_uint(P[2079]);
+        for (int k1 = 0; k1 < 16; ++k1) buf[k1 * kS64R1 + t] = v[dp16(k1)];
+        __syncthreads();
+        // ---- 2. DFT-16 over n2, twiddle, columns m = k1 + 16 k2 ----
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) v[n2] = buf[k1b * kS64R1 + 8 * n2 + n3b];
+        ddft16(v);
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) v[dp16(k2)] = dmul(v[dp16(k2)], tw2[k2 * kS64T + ti]);
+        __syncthreads();
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) buf[(k1b + 16 * k2) * kS64C2 + n3b] = v[dp16(k2)];
+        __syncthreads();
+        // ---- 3. DFT-8 over n3 of the thread's two columns ----
+        double2 c1[8], c2[8];
+#pragma unroll
+        for (int n3 = 0; n3 < 8; ++n3) {
+            c1[n3] = buf[m1 * kS64C2 + n3];
+            c2[n3] = buf[m2 * kS64C2 + n3];
         }
-        float* srow = S + (size_t)fi * kSnLd;
+        ddft8(c1);
+        ddft8(c2);
+        __syncthreads();
+        // ---- real split and magnitudes into the buffer.  Slot s of thread j
+        // pairs Z[j + 256 s] with Z[2048 - j - 256 s] (column 256 - j, entry
+        // 7 - s).  Thread 0: slots 0-3 pair column 128 with itself (bins 128 +
+        // 256 s), slots 4-7 column 0 (bins 256 (s - 3)), and Z[0] gives bins 0
+        // and 2048. ----
 #pragma unroll
-        for (int i = 0; i < 32; ++i) srow[lane + 64 * i] = __uint_as_float(v[i]);
-        if (lane == 0) srow[2048] = __uint_as_float(v[32]);
+        for (int s = 0; s < 8; ++s) {
+            double2 a, b, w;
+            int ka;
+            if (s < 4) {
+                a = z ? c2[s] : c1[s];
+                b = c2[7 - s];
+                ka = mA + 256 * s;
+            } else {
+                a = z ? c1[s - 3] : c1[s];
+                b = z ? c1[11 - s] : c2[7 - s];
+                ka = z ? 256 * (s - 3) : t + 256 * s;
+            }
+            switch (s) {  // W4096^ka: the thread's base times W16^s (thread 0, s >= 4: W16^(s - 3))
+                case 0: w = tb; break;
+                case 1: w = w16<1>(tb); break;
+                case 2: w = w16<2>(tb); break;
+                case 3: w = w16<3>(tb); break;
+                case 4: w = z ? make_double2(kCos8, -kSin8) : w16<4>(tb); break;
+                case 5: w = z ? make_double2(kRt2, -kRt2) : w16<5>(tb); break;
+                case 6: w = z ? make_double2(kSin8, -kCos8) : w16<6>(tb); break;
+                default: w = z ? make_double2(0.0, -1.0) : w16<7>(tb); break;
+            }
+            const double2 E = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+            const double2 O = make_double2(0.5 * (a.y + b.y), -0.5 * (a.x - b.x));
+            const double2 q = dmul(w, O);
+            mag[ka] = np_cabsf(E.x + q.x, E.y + q.y);
+            mag[2048 - ka] = np_cabsf(E.x - q.x, q.y - E.y);
+        }
+        if (z) {  // rfft's DC and Nyquist bins: real
+            mag[0] = fabsf((float)(c1[0].x + c1[0].y));
+            mag[2048] = fabsf((float)(c1[0].x - c1[0].y));
+        }
+        __syncthreads();
+        // ---- the frame's row of S, its maximum and its median over bins ----
+        unsigned vv[17];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) vv[i] = __float_as_uint(mag[t + 128 * i]);
+        vv[16] = z ? __float_as_uint(mag[2048]) : 0u;
+        if (S) {
+            float* srow = S + (size_t)fi * ld;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) srow[t + 128 * i] = __uint_as_float(vv[i]);
+            if (z) srow[2048] = __uint_as_float(vv[16]);
+        }
         // bit patterns of non-negative floats order like the values (NaN and
         // inf above every finite value: the host reads that as non-finite input)
 #pragma unroll
-        for (int i = 0; i < 32; ++i) wmax = max(wmax, v[i]);
-        wmax = max(wmax, v[32]);
-        // ---- the frame's median over bins, from the registers the row
-        // came from (the wave's buffer, read above, holds the histograms) ----
-        wave_sync();
-        const unsigned med = wave_median_2049(v, reinterpret_cast<unsigned*>(wb), lane);
-        if (lane == 0) colmed[fi] = med;
-        wave_sync();  // the buffer is rewritten by the next frame
+        for (int i = 0; i < 17; ++i) wmax = max(wmax, vv[i]);
+        if (colmed) {
+            const unsigned med = block_median_2049(vv, t, hist, red);
+            if (z) colmed[fi] = med;
+        }
+        __syncthreads();  // the buffer is rewritten by the next frame
     }
+    if (gmax) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (unsigned)__shfl_xor((int)wmax, o, 64));
-    if (lane == 0 && wmax) atomicMax(gmax, wmax);
+        for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (unsigned)__shfl_xor((int)wmax, o, 64));
+        if ((t & 63) == 0 && wmax) atomicMax(gmax, wmax);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -787,6 +929,19 @@ static int sn_components(const SnPlan& p, const SnWs& ws, const SnBatch& nb, boo
     return AA_OK;
 }
 
+// sn_stft64 over one recording: persistent blocks (4 per CU, the LDS limit),
+// a multiple of 8 so every XCD owns an equal share of the blocks
+static int sn_launch_stft(const SnPlan& p, const float* pcm, int64_t n, int F, float* S, int ld, unsigned* gmax,
+                          unsigned* colmed, hipStream_t st) {
+    int grid = std::min(F, 256 * 4);
+    grid = (grid + 7) & ~7;
+    const double2* tab = p.d_tab;
+    hipLaunchKernelGGL(sn_stft64, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
+                       tab + kS64TabTw1, tab + kS64TabTw2, tab + kS64TabTw3, S, ld, gmax, colmed);
+    AA_LAUNCH_CHECK();
+    return AA_OK;
+}
+
 // The whole detector over K recordings of one PCM buffer (recording k:
 // offs[k], lens[k] samples, host arrays): per recording the STFT (+ column
 // medians), transpose and row select (+ mask) into its own mask slot, then
@@ -810,23 +965,14 @@ static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const i
              workspace_bytes, ws.bytes);
     hipLaunchKernelGGL(sn_zero, dim3(K), dim3(64), 0, st, ws.gmax, ws.counters, ws.pf, n_out, n_out_stride);
     AA_LAUNCH_CHECK();
-    const size_t lds = sizeof(float2) * kSnWpb * kHalf;
-    static bool attr_set = false;
-    if (!attr_set) {
-        AA_HIP(hipFuncSetAttribute((const void*)sn_stft, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr_set = true;
-    }
     for (int k = 0; k < K; ++k) {
         const int F = nb.nf[k];
         unsigned* gmax = sn_at(ws.gmax, ws.pf, k);
         unsigned* colmed = sn_at(ws.colmed, ws.pf, k);
         float* c3 = sn_at(ws.c3, ws.pf, k);
         unsigned long long* M0 = sn_at(ws.M0, ws.pf, k);
-        int grid = std::min((F + kSnWpb - 1) / kSnWpb, 256 * 3);  // persistent: 3 blocks per CU
-        grid = (grid + 7) & ~7;
-        hipLaunchKernelGGL(sn_stft, dim3(grid), dim3(64 * kSnWpb), lds, st, lens[k] ? pcm + offs[k] : pcm,
-                           (int)lens[k], p->cfg.hop_length, F, p->d_tw, p->d_tw4096, ws.S, gmax, colmed);
-        AA_LAUNCH_CHECK();
+        int rc = sn_launch_stft(*p, lens[k] ? pcm + offs[k] : pcm, lens[k], F, ws.S, kSnLd, gmax, colmed, st);
+        if (rc != AA_OK) return rc;
         const int words = (F + 63) / 64, ldt = words * 64;
         hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST, gmax,
                            colmed, c3);
@@ -886,19 +1032,30 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
         delete p;
         return rc;
     }
-    std::vector<float2> tw(2048), tw2(2049);
-    for (int m = 0; m < 2048; ++m) {
-        const double a = -2.0 * M_PI * m / 2048;
-        tw[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+    // sn_stft64's tables, rounded from long double
+    auto wexp = [](long long e, long long m) {  // exp(-2 pi i e / m)
+        const long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)(e % m) / (long double)m;
+        return make_double2((double)cosl(a), (double)sinl(a));
+    };
+    std::vector<double2> tab(kS64TabN);
+    {  // scipy.signal.get_window('hann', 4096, fftbins=True) (librosa 0.11's window, :654): general_cosine
+       // over np.linspace(-pi, pi, 4097)[:4096], w = 0.5 + 0.5 cos(fac) in float64
+        const double start = -M_PI, step = (M_PI - start) / 4096.0;
+        std::vector<double> w(4096);
+        for (int i = 0; i < 4096; ++i) {
+            const double fac = (double)i * step + start;
+            w[i] = 0.5 + 0.5 * std::cos(fac);
+        }
+        for (int n = 0; n < 2048; ++n) tab[n] = make_double2(w[2 * n], w[2 * n + 1]);
     }
-    for (int k = 0; k <= 2048; ++k) {
-        const double a = -2.0 * M_PI * k / 4096;
-        tw2[k] = make_float2((float)std::cos(a), (float)std::sin(a));
-    }
-    hipError_t e = hipMalloc((void**)&p->d_tw, sizeof(float2) * tw.size());
-    if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(float2) * tw.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc((void**)&p->d_tw4096, sizeof(float2) * tw2.size());
-    if (e == hipSuccess) e = hipMemcpy(p->d_tw4096, tw2.data(), sizeof(float2) * tw2.size(), hipMemcpyHostToDevice);
+    for (int k1 = 1; k1 < 16; ++k1)
+        for (int t = 0; t < kS64T; ++t) tab[kS64TabTw1 + (k1 - 1) * kS64T + t] = wexp((long long)(t >> 3) * k1, 256);
+    for (int k2 = 0; k2 < 16; ++k2)
+        for (int t = 0; t < kS64T; ++t)
+            tab[kS64TabTw2 + k2 * kS64T + t] = wexp((long long)(t & 7) * ((t >> 3) + 16 * k2), 2048);
+    for (int t = 0; t < kS64T; ++t) tab[kS64TabTw3 + t] = wexp(t ? t : 128, 4096);
+    hipError_t e = hipMalloc((void**)&p->d_tab, sizeof(double2) * tab.size());
+    if (e == hipSuccess) e = hipMemcpy(p->d_tab, tab.data(), sizeof(double2) * tab.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         set_error("aa_sn_create: %s", hipGetErrorString(e));
         aa_sn_destroy(p);
@@ -911,8 +1068,7 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
 extern "C" int aa_sn_destroy(void* plan) {
     SnPlan* p = static_cast<SnPlan*>(plan);
     if (!p) return AA_OK;
-    (void)hipFree(p->d_tw);
-    (void)hipFree(p->d_tw4096);
+    (void)hipFree(p->d_tab);
     delete p;
     return AA_OK;
 }
@@ -990,4 +1146,15 @@ extern "C" int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int6
     nb.n = 1;
     nb.nf[0] = F;
     return sn_components(*p, ws, nb, false, out, max_out, max_out, n_out, 2, st);
+}
+
+extern "C" int aa_sn_spectrogram(void* plan, const float* pcm, int64_t n_samples, float* out, int64_t ld,
+                                 void* stream) {
+    SnPlan* p = static_cast<SnPlan*>(plan);
+    AA_CHECK(p && out && (pcm || n_samples == 0), AA_ERR_INVALID, "aa_sn_spectrogram: null argument");
+    AA_CHECK(n_samples >= 0 && n_samples < (int64_t(1) << 29), AA_ERR_UNSUPPORTED,
+             "aa_sn_spectrogram: %lld samples (below 2^29)", (long long)n_samples);
+    AA_CHECK(ld >= kSnBins && ld <= (int64_t(1) << 20), AA_ERR_INVALID, "aa_sn_spectrogram: ld %lld", (long long)ld);
+    const int F = sn_frames(*p, n_samples);
+    return sn_launch_stft(*p, pcm, n_samples, F, out, (int)ld, nullptr, nullptr, static_cast<hipStream_t>(stream));
 }

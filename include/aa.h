@@ -317,6 +317,11 @@ size_t aa_sn_batch_workspace_bytes(const void* plan, int64_t max_samples, int32_
 int aa_sn_run_batch(void* plan, const float* pcm, const int64_t* offsets, const int64_t* lengths, int32_t n_rec,
                     void* workspace, size_t workspace_bytes, aa_sn_component* out, int32_t max_out,
                     int64_t out_stride, int32_t* n_out, int32_t n_out_stride, void* stream);
+/* np.abs(librosa.stft(pcm, n_fft=4096, hop_length=hop)) (:654) alone, in the
+ * reference's precision (f64 transform, complex64 rounding, numpy's f32
+ * magnitude): out = device f32 [F][ld] (F = aa_sn_n_frames, ld >= 2049), row f
+ * = frame f's 2049 bins.  No workspace. */
+int aa_sn_spectrogram(void* plan, const float* pcm, int64_t n_samples, float* out, int64_t ld, void* stream);
 /* Morphology, components and filter of a given mask (mask_out's layout). */
 int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int64_t n_frames, void* workspace,
                                size_t workspace_bytes, aa_sn_component* out, int32_t max_out,

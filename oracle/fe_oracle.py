@@ -50,9 +50,11 @@ def normalize_data(x: np.ndarray) -> np.ndarray:
 # A4  librosa 0.11 stft, as called at src/identify_tracks.py:243
 # --------------------------------------------------------------------------
 def hann_periodic(n: int) -> np.ndarray:
-    """scipy.signal.get_window('hann', n, fftbins=True) in float64."""
-    k = np.arange(n, dtype=np.float64)
-    return 0.5 - 0.5 * np.cos(2.0 * np.pi * k / n)
+    """scipy.signal.get_window('hann', n, fftbins=True) in float64 -- the call
+    librosa 0.11's stft makes (filters.get_window); scipy is the reference's own
+    pinned dependency (requirements.txt) and is present here."""
+    from scipy.signal import get_window
+    return get_window("hann", n, fftbins=True)
 
 
 def n_frames(n_samples: int, hop: int) -> int:

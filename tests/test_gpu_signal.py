@@ -1,13 +1,16 @@
 """signal_noise on the GPU (aa_sn_run, csrc/aa_signal.hip) against the CPU
 oracle (oracle/signal_oracle.py, src/identify_tracks.py:650-706).
 
+* |STFT| (aa_sn_spectrogram): the f64 transform rounded to complex64 and
+  numpy's f32 magnitude give the oracle's S (numpy's own rfft + np.abs) bit for
+  bit, on full 60 s recordings, ragged lengths and recordings shorter than one
+  hop.
+* The mask, the components and the Signal tuples: identical to the oracle's
+  on full 60 s recordings (zero pixels differ), and so are the tracks built from
+  those signals and their window start indices (the CLI default path,
+  analyse_tracks=False, :435-437).
 * Morphology + components + filter: bit-exact on identical masks
   (aa_sn_components_from_mask vs the oracle's cv2 restatement).
-* The mask: the GPU f32 FFT vs the oracle's f64 FFT (librosa 0.11) can flip
-  pixels sitting on the 3x-median thresholds; the test bounds the disagreement
-  (<= 1e-4 of the pixels) and requires the GPU components to equal the oracle's
-  morphology of the GPU's own mask exactly, and the oracle's end result up to
-  those flips (same count, boxes within 2 frames / 2 bins).
 * Edge cases: silent input (max 0: no signals), non-finite input raises,
   recordings shorter than one frame hop, frame counts not a multiple of 64.
 """
@@ -69,23 +72,66 @@ def test_components_from_mask_bit_exact(gpu, F, seed):
     assert got.tolist() == ref.tolist()
 
 
-@pytest.mark.parametrize("seconds,seed", [(3.0, 10), (10.0, 11), (7.3, 12)])
+@pytest.mark.parametrize("n,seed", [(60 * SR, 30), (60 * SR, 31), (7 * SR + 12345, 32), (3000, 33), (0, 34)])
+def test_spectrogram_bit_exact(gpu, n, seed):
+    x = _clip(n / SR, seed) if n else np.zeros(0, np.float32)
+    det = _det(gpu)
+    got = det.spectrogram(torch.from_numpy(x).to(gpu)).cpu().numpy()
+    from oracle.fe_oracle import stft_mag
+    want = stft_mag(x, 4096, HOP)
+    assert got.shape == want.shape
+    diff = int((got.view(np.uint32) != want.view(np.uint32)).sum())
+    assert diff == 0, f"{diff} of {want.size} magnitudes differ"
+
+
+def test_spectrogram_tone_bit_exact(gpu):
+    """a pure 1 kHz tone (most bins far below the peak: the small magnitudes
+    are where an f32 transform loses the reference's low bits)"""
+    t = np.arange(20 * SR) / SR
+    x = (np.round(0.5 * np.sin(2 * np.pi * 1000.0 * t) * 32768) / 32768).astype(np.float32)
+    got = _det(gpu).spectrogram(torch.from_numpy(x).to(gpu)).cpu().numpy()
+    from oracle.fe_oracle import stft_mag
+    want = stft_mag(x, 4096, HOP)
+    assert int((got.view(np.uint32) != want.view(np.uint32)).sum()) == 0
+
+
+@pytest.mark.parametrize("seconds,seed", [(60.0, 10), (60.0, 11), (60.0, 12), (7.3, 13), (10.0, 14)])
 def test_signal_noise_vs_oracle(gpu, seconds, seed):
     x = _clip(seconds, seed)
+    x = x[:len(x) - seed]  # ragged lengths: frame counts off the 64-frame words
     det = _det(gpu)
     F = det.n_frames(len(x))
     mask_dev = torch.empty((2049, det.words(F)), dtype=torch.int64, device=gpu)
     stats = det.components(torch.from_numpy(x).to(gpu), mask_out=mask_dev)
     gmask = _unpack(mask_dev.cpu().numpy(), F)
     ref_sig, ref_mask, ref_stats = so.signal_noise(x, SR, HOP)
-    diff = int((gmask != ref_mask).sum())
-    assert diff <= max(2, 1e-4 * ref_mask.size), diff
-    assert stats.tolist() == so.signal_mask_to_stats(gmask, SR, HOP).tolist()
-    assert len(stats) == len(ref_stats) and len(stats) > 0
-    assert np.abs(stats[:, :4] - ref_stats[:, :4]).max() <= 2
-    got_sig = det.to_tuples(stats)
-    if diff == 0:
-        assert got_sig == ref_sig
+    assert int((gmask != ref_mask).sum()) == 0
+    assert stats.tolist() == ref_stats.tolist() and len(stats) > 0
+    assert det.to_tuples(stats) == ref_sig
+
+
+def test_tracks_from_signals_window_indices(gpu):
+    """The CLI default path (analyse_tracks=False, :435-437): the tracks built
+    from the GPU's signals and their windows' start indices equal those built
+    from the oracle's signals (same seeded np.random draws)."""
+    from aa_amd.identify_tracks import Signal, get_tracks_from_signals
+    from aa_amd import windows
+    x = _clip(60.0, 15, n_chirps=10)
+    det = _det(gpu)
+    got_sig = det.signal_noise(pcm=torch.from_numpy(x).to(gpu))
+    ref_sig, _, _ = so.signal_noise(x, SR, HOP)
+    assert got_sig == ref_sig and len(got_sig) > 0
+
+    def views(sig):
+        tracks = get_tracks_from_signals([Signal(*s) for s in sig], 60.0)
+        np.random.seed(1234)
+        return [(t.start, t.end, t.freq_start, t.freq_end) for t in tracks], windows.schedule(
+            len(x), SR, tracks, 3.0, 1.5, 50.0, 11000.0)
+
+    got_tracks, got_views = views(got_sig)
+    ref_tracks, ref_views = views(ref_sig)
+    assert len(got_tracks) > 0 and sum(len(v) for v in got_views) > 0
+    assert got_tracks == ref_tracks and got_views == ref_views
 
 
 def test_signal_noise_edge_cases(gpu):

@@ -6,7 +6,7 @@ R=$1; shift
 mkdir -p gpurun_out
 for r in $(seq 1 $R); do
   for L in "$@"; do
-    if [ "$L" = main ]; then unset AA_LIB; else export AA_LIB=$PWD/$L; fi
+    if [ "$L" = main ]; then unset AA_LIB; else export AA_LIB=$PWD/$L AA_LIB_AB=1; fi
     timeout -k 10 120 python bench.py --steps 100 --warmup 20 --cpu-seconds 0 --secondary= --no-parity > gpurun_out/ab.log 2>&1 || { tail -5 gpurun_out/ab.log; exit 1; }
     python - "$L" <<'PY'
 import json, sys
