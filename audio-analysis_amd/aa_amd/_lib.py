@@ -155,6 +155,11 @@ _SIGS = {
     "aa_sn_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.c_void_p,
                             C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "aa_sn_spectrogram": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p]),
+    "aa_sn_n_stages": (C.c_int, [C.c_void_p]),
+    "aa_sn_stage_info": (C.c_int, [C.c_void_p, C.c_int32, C.c_char_p, C.c_int32, C.POINTER(C.c_double),
+                                   C.POINTER(C.c_double)]),
+    "aa_sn_set_timing": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "aa_sn_stage_time": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "aa_sn_components_from_mask": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t,
                                              C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "aa_flac_info": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(FlacInfo)]),

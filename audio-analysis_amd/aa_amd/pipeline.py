@@ -67,6 +67,7 @@ class Classifier:
         self._models = {}
         self._fes = {}
         self._lock = threading.RLock()
+        self.windows_done = 0  # windows through the front end (bench.py's configs[3] roofline)
 
     def frontend(self, s: FeSettings) -> FrontEnd:
         with self._lock:
@@ -178,6 +179,9 @@ class Classifier:
             total = sum(sum(c) for c in counts)
             if total == 0:
                 continue
+            if group is groups[0]:
+                with self._lock:
+                    self.windows_done += total
             group_mel = logmel
             if "efficientnet" in model_name.lower():
                 # np.repeat(d, 3, -1) of the shared windows (:539-540): every

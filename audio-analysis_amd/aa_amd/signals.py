@@ -37,9 +37,11 @@ def geometry(sr, hop_length=281):
     return tuple(g)
 
 
-class SignalDetector:
+class SignalDetector(_lib.StageTiming):
     """One device plan per (sample rate, hop); the workspace grows with the
-    longest recording seen."""
+    longest recording seen.  Stage timing (aa_sn_stage_*): per-launch HIP
+    events, an item being one STFT frame."""
+    _timing_prefix = "aa_sn"
 
     def __init__(self, sr=48000, hop_length=281, device=None, max_components=65536):
         self.sr, self.hop = int(sr), int(hop_length)

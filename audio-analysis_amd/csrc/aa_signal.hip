@@ -32,6 +32,8 @@
 #include "aa_wavefft.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <climits>
 #include <cmath>
 #include <type_traits>
@@ -48,6 +50,9 @@ enum { R_X0 = 0, R_X1, R_Y, R_P, R_LEFT, R_RIGHT, R_TOP, R_BOT, R_AREA, R_KEY };
 // counters, morphology and components): their frame counts, passed by value;
 // recording k's buffers sit k * pf bytes after recording 0's (blockIdx.z or
 // .y = k).
+// launch stages (aa_sn_stage_*): per recording stft / transpose / select,
+// per batch the four morphology launches and the component launches
+enum { SN_STAGE_STFT = 0, SN_STAGE_TRANSPOSE, SN_STAGE_SELECT, SN_STAGE_MORPH, SN_STAGE_COMPONENTS, SN_N_STAGES };
 constexpr int kSnMaxBatch = 64;
 struct SnBatch {
     int n;
@@ -64,6 +69,8 @@ struct SnPlan {
     int kh_e = 0, kw_e = 0;  // cv2.erode(ones((height // 10, width))) (:684)
     int wmin = 0, hmin = 0;  // kept: width >= wmin, height >= hmin (:689-691)
     double2* d_tab = nullptr;  // sn_stft64's tables: window pairs [2048], tw1 [15][128], tw2 [16][128], tw3 [128]
+    StageTimer timer;          // HIP events around the launches of the stages in timer.mask
+    bool select_reg = false;   // row medians by sn_select_reg (AA_SN_SELECT=reg; A/B knob) or sn_select
 };
 
 __device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
@@ -169,6 +176,19 @@ __device__ __forceinline__ void ddft16(double2 (&v)[16]) {
     for (int c = 0; c < 4; ++c) ddft4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);  // v[4c + d] = X[c + 4d]
 }
 
+// sqrtf correctly rounded for x in [1, 2]: v_sqrt_f32 (within 1 ulp), then
+// the neighbour whose residual brackets x -- the IEEE sqrt sequence the
+// compiler emits, without its denormal scaling and special-value checks
+// (fmaf(r, r, 1) of a ratio r in [0, 1] is always in range)
+__device__ __forceinline__ float sqrt_rn_1_2(float x) {
+    float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rd = fmaf(-sd, s, x), ru = fmaf(-su, s, x);
+    s = rd <= 0.f ? sd : s;
+    s = ru > 0.f ? su : s;
+    return s;
+}
+
 // np.abs of one complex64 value, numpy's SIMD formula (non-finite parts give
 // a NaN / inf magnitude, which the host reports as non-finite input)
 __device__ __forceinline__ float np_cabsf(double re64, double im64) {
@@ -176,7 +196,7 @@ __device__ __forceinline__ float np_cabsf(double re64, double im64) {
     const float x = fabsf(re), y = fabsf(im);
     const float L = fmaxf(x, y), s = fminf(x, y);
     const float r = (L == 0.f || s == __builtin_huge_valf()) ? 0.f : s / L;  // correctly rounded
-    float m = sqrtf(fmaf(r, r, 1.f)) * L;                                     // correctly rounded sqrt
+    float m = sqrt_rn_1_2(fmaf(r, r, 1.f)) * L;
     if (re != re || im != im) m = __builtin_nanf("");
     return m;
 }
@@ -226,7 +246,8 @@ constexpr int kS64T = 128;
 constexpr int kS64R1 = 136;
 constexpr int kS64C2 = 9;
 constexpr int kS64Buf = 256 * kS64C2;  // double2
-constexpr int kS64Hist = 2176;         // unsigned offset of the histograms (after the magnitudes)
+constexpr int kS64Mag = 64;            // float offset of the magnitudes (after column 0's 8 double2)
+constexpr int kS64Hist = 2240;         // unsigned offset of the histograms (after the magnitudes)
 constexpr int kS64TabTw1 = 2048, kS64TabTw2 = kS64TabTw1 + 15 * kS64T, kS64TabTw3 = kS64TabTw2 + 16 * kS64T,
               kS64TabN = kS64TabTw3 + kS64T;  // double2 entries of SnPlan::d_tab
 static_assert(16 * kS64R1 <= kS64Buf && (kS64Hist + 1024) * 4 <= kS64Buf * 16, "sn_stft64 LDS");
@@ -320,9 +341,9 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
     for (int n1 = 0; n1 < 16; ++n1) wv[n1] = win2[128 * n1 + t];
     const double2 tb = tw3[t];
     const int k1b = t >> 3, n3b = t & 7;         // step 2
-    const int m1 = t, m2 = z ? 128 : 256 - t;    // step 3 columns
-    const int mA = z ? 128 : t;                  // split: first bin of slots 0..3
-    float* mag = reinterpret_cast<float*>(buf);
+    // step 3 columns: j and 256 - j; thread 0: 0 and 128
+    const int m1 = t, m2 = z ? 128 : 256 - t;
+    float* mag = reinterpret_cast<float*>(buf) + kS64Mag;
     unsigned* hist = reinterpret_cast<unsigned*>(buf) + kS64Hist;
     unsigned wmax = 0;
     const int nbx = gridDim.x >> 3;  // blocks per XCD (grid a multiple of 8)
@@ -337,9 +358,14 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
         double2 v[16];
         {
             const int off = fi * hop - 2048 + 2 * t;
+            // the odd sample's offset in a register of its own: two adjacent
+            // dword loads merged into one dwordx2 would be range-checked as a
+            // unit, so the view's first / last sample would read as 0 / garbage
+            int offo = off + 1;
+            __asm__ volatile("" : "+v"(offo));
 #pragma unroll
             for (int n1 = 0; n1 < 16; ++n1) {
-                const float xe = load_view(rs, off + 256 * n1), xo = load_view(rs, off + 256 * n1 + 1);
+                const float xe = load_view(rs, off + 256 * n1), xo = load_view(rs, offo + 256 * n1);
                 v[n1] = make_double2((double)xe * wv[n1].x, (double)xo * wv[n1].y);
             }
         }
@@ -370,43 +396,50 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
         ddft8(c1);
         ddft8(c2);
         __syncthreads();
-        // ---- real split and magnitudes into the buffer.  Slot s of thread j
-        // pairs Z[j + 256 s] with Z[2048 - j - 256 s] (column 256 - j, entry
-        // 7 - s).  Thread 0: slots 0-3 pair column 128 with itself (bins 128 +
-        // 256 s), slots 4-7 column 0 (bins 256 (s - 3)), and Z[0] gives bins 0
-        // and 2048. ----
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            double2 a, b, w;
-            int ka;
-            if (s < 4) {
-                a = z ? c2[s] : c1[s];
-                b = c2[7 - s];
-                ka = mA + 256 * s;
-            } else {
-                a = z ? c1[s - 3] : c1[s];
-                b = z ? c1[11 - s] : c2[7 - s];
-                ka = z ? 256 * (s - 3) : t + 256 * s;
-            }
-            switch (s) {  // W4096^ka: the thread's base times W16^s (thread 0, s >= 4: W16^(s - 3))
-                case 0: w = tb; break;
-                case 1: w = w16<1>(tb); break;
-                case 2: w = w16<2>(tb); break;
-                case 3: w = w16<3>(tb); break;
-                case 4: w = z ? make_double2(kCos8, -kSin8) : w16<4>(tb); break;
-                case 5: w = z ? make_double2(kRt2, -kRt2) : w16<5>(tb); break;
-                case 6: w = z ? make_double2(kSin8, -kCos8) : w16<6>(tb); break;
-                default: w = z ? make_double2(0.0, -1.0) : w16<7>(tb); break;
-            }
-            const double2 E = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
-            const double2 O = make_double2(0.5 * (a.y + b.y), -0.5 * (a.x - b.x));
+        // ---- real split and magnitudes into the buffer (the window carries
+        // the split's factor 1/2: Z here is half the transform of z).  Slot s
+        // of thread j pairs a = Z[j + 256 s] with b = Z[2048 - j - 256 s]
+        // (column 256 - j, entry 7 - s): X[k] = E + W4096^k O, X[2048 - k] =
+        // conj(E - W4096^k O), E = a + conj b, O = -i (a - conj b).  Thread 0
+        // re-seats its registers so the same slots pair column 128 with itself
+        // (slots 0-3: bins 128 + 256 s) and column 0 with itself (slots 4-7:
+        // bins 256 (s - 3)); Z[0] gives the DC and Nyquist bins. ----
+        const double2 z0 = c1[0];
+        if (z) {  // per-lane selects (no branch: one lane of one wave)
+            const double2 a4 = c1[1], a5 = c1[2], a6 = c1[3], a7 = c1[4];
+            const double2 b0 = c1[4], b1 = c1[5], b2 = c1[6], b3 = c1[7];
+            c1[0] = c2[0];
+            c1[1] = c2[1];
+            c1[2] = c2[2];
+            c1[3] = c2[3];
+            c1[4] = a4;
+            c1[5] = a5;
+            c1[6] = a6;
+            c1[7] = a7;
+            c2[0] = b0;
+            c2[1] = b1;
+            c2[2] = b2;
+            c2[3] = b3;
+        }
+        auto split = [&](double2 a, double2 b, double2 w, int ka) {
+            const double2 E = make_double2(a.x + b.x, a.y - b.y);
+            const double2 O = make_double2(a.y + b.y, b.x - a.x);
             const double2 q = dmul(w, O);
             mag[ka] = np_cabsf(E.x + q.x, E.y + q.y);
             mag[2048 - ka] = np_cabsf(E.x - q.x, q.y - E.y);
-        }
+        };
+        const int mA = z ? 128 : t;
+        split(c1[0], c2[7], tb, mA);
+        split(c1[1], c2[6], w16<1>(tb), mA + 256);
+        split(c1[2], c2[5], w16<2>(tb), mA + 512);
+        split(c1[3], c2[4], w16<3>(tb), mA + 768);
+        split(c1[4], c2[3], z ? make_double2(kCos8, -kSin8) : w16<4>(tb), z ? 256 : t + 1024);
+        split(c1[5], c2[2], z ? make_double2(kRt2, -kRt2) : w16<5>(tb), z ? 512 : t + 1280);
+        split(c1[6], c2[1], z ? make_double2(kSin8, -kCos8) : w16<6>(tb), z ? 768 : t + 1536);
+        split(c1[7], c2[0], z ? make_double2(0.0, -1.0) : w16<7>(tb), z ? 1024 : t + 1792);
         if (z) {  // rfft's DC and Nyquist bins: real
-            mag[0] = fabsf((float)(c1[0].x + c1[0].y));
-            mag[2048] = fabsf((float)(c1[0].x - c1[0].y));
+            mag[0] = fabsf((float)(2.0 * (z0.x + z0.y)));
+            mag[2048] = fabsf((float)(2.0 * (z0.x - z0.y)));
         }
         __syncthreads();
         // ---- the frame's row of S, its maximum and its median over bins ----
@@ -564,6 +597,193 @@ __global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, in
         bool bit = false;
         if (f < n) {
             const float d = __fdiv_rn(__uint_as_float(row[f]), a);
+            bit = d > c3[f] && d > rb;
+        }
+        const unsigned long long m = __ballot(bit);
+        if (lane == 0) M[(size_t)blockIdx.x * words + w] = m;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// sn_select_reg: the row median and mask of sn_select with the row held in
+// registers (512 threads x 24 values: rows of up to 12,288 frames; longer
+// rows take sn_select<false>).  One block-wide 8-bit radix pass (per-wave
+// histograms, folded, every wave picking the same bucket) usually leaves a
+// few hundred candidates in the median's bucket; they are compacted into LDS
+// and wave 0 finishes the select over them in registers with wave-local
+// histograms -- no further block barriers, no re-read of the row.  Buckets
+// larger than kSelCand (long runs of equal values, e.g. digital silence) take
+// more block-wide passes first.  Then the mask bits from the same registers.
+// ---------------------------------------------------------------------------
+constexpr int kSelT = 512, kSelPer = 24, kSelCand = 1024;
+constexpr int kSelNW = kSelT / 64;
+
+__global__ __launch_bounds__(kSelT) __attribute__((amdgpu_waves_per_eu(4))) void sn_select_reg(const float* __restrict__ X, int ld, int n,
+                                                      const unsigned* __restrict__ gmax,
+                                                      const float* __restrict__ c3, int words,
+                                                      unsigned long long* __restrict__ M) {
+    __shared__ unsigned hist[kSelNW][256];
+    __shared__ unsigned cand[kSelCand];
+    __shared__ unsigned red[64];
+    const unsigned* grow = reinterpret_cast<const unsigned*>(X) + (size_t)blockIdx.x * ld;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    unsigned v[kSelPer];
+    unsigned mn = 0xFFFFFFFFu, mx = 0;
+#pragma unroll
+    for (int i = 0; i < kSelPer; ++i) {
+        const int f = tid + kSelT * i;
+        v[i] = f < n ? grow[f] : 0u;
+        if (f < n) {
+            mn = min(mn, v[i]);
+            mx = max(mx, v[i]);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if (lane == 0) {
+        red[wv] = mn;
+        red[kSelNW + wv] = mx;
+    }
+    reinterpret_cast<uint4*>(&hist[0][0])[tid] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    mn = red[0];
+    mx = red[kSelNW];
+#pragma unroll
+    for (int w = 1; w < kSelNW; ++w) {
+        mn = min(mn, red[w]);
+        mx = max(mx, red[kSelNW + w]);
+    }
+    unsigned rlo = mn, rhi = mn;  // a constant row (block-uniform): its value
+    if (mn != mx) {
+        const int hb = 31 - __clz(mn ^ mx);
+        unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
+        unsigned prefix = mn & pmask, rank = (unsigned)(n - 1) / 2, cnt = 0;
+        int shift = max(hb - 7, 0);
+        bool done = false;
+        // ---- block-wide passes until the median's bucket fits kSelCand ----
+#pragma unroll 1
+        for (;;) {
+#pragma unroll
+            for (int i = 0; i < kSelPer; ++i)
+                if (tid + kSelT * i < n && (v[i] & pmask) == prefix) atomicAdd(&hist[wv][(v[i] >> shift) & 255u], 1u);
+            __syncthreads();
+            if (tid < 256) {
+                unsigned s = hist[0][tid];
+#pragma unroll
+                for (int w = 1; w < kSelNW; ++w) s += hist[w][tid];
+                hist[0][tid] = s;
+            }
+            __syncthreads();
+            unsigned below, c;  // every wave picks the same bucket
+            const unsigned dig = hist_pick(&hist[0][0], rank, lane, &below, &c);
+            prefix = (prefix & ~(255u << shift)) | (dig << shift);
+            pmask |= 255u << shift;
+            rank -= below;
+            cnt = c;
+            if (shift == 0) {
+                done = true;
+                break;
+            }
+            if (cnt <= (unsigned)kSelCand) break;  // block-uniform
+            __syncthreads();  // every wave has read the folded copy
+            reinterpret_cast<uint4*>(&hist[0][0])[tid] = make_uint4(0u, 0u, 0u, 0u);
+            __syncthreads();
+            shift = max(shift - 8, 0);
+        }
+        if (!done) {
+            // ---- compact the bucket's cnt values (block exclusive scan of the
+            // per-thread counts), then wave 0 selects among them ----
+            unsigned mine = 0;
+#pragma unroll
+            for (int i = 0; i < kSelPer; ++i) mine += (tid + kSelT * i < n && (v[i] & pmask) == prefix) ? 1u : 0u;
+            const unsigned incl = wave_incl_scan(mine, lane);
+            if (lane == 63) red[16 + wv] = incl;
+            __syncthreads();
+            unsigned pos = incl - mine;
+            for (int w = 0; w < wv; ++w) pos += red[16 + w];
+#pragma unroll
+            for (int i = 0; i < kSelPer; ++i)
+                if (tid + kSelT * i < n && (v[i] & pmask) == prefix) cand[pos++] = v[i];
+            __syncthreads();
+            if (wv == 0) {
+                unsigned cv[kSelCand / 64];
+#pragma unroll
+                for (int j = 0; j < kSelCand / 64; ++j) {
+                    const int idx = lane + 64 * j;
+                    cv[j] = idx < (int)cnt ? cand[idx] : 0u;
+                }
+#pragma unroll 1
+                do {
+                    shift = max(shift - 8, 0);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(&hist[q][0])[lane] = make_uint4(0u, 0u, 0u, 0u);
+                    wave_sync();
+#pragma unroll
+                    for (int j = 0; j < kSelCand / 64; ++j)
+                        if (lane + 64 * j < (int)cnt && (cv[j] & pmask) == prefix)
+                            atomicAdd(&hist[lane & 3][(cv[j] >> shift) & 255u], 1u);
+                    wave_sync();
+                    uint4 c4 = reinterpret_cast<const uint4*>(&hist[0][0])[lane];
+#pragma unroll
+                    for (int q = 1; q < 4; ++q) {
+                        const uint4 u = reinterpret_cast<const uint4*>(&hist[q][0])[lane];
+                        c4.x += u.x;
+                        c4.y += u.y;
+                        c4.z += u.z;
+                        c4.w += u.w;
+                    }
+                    unsigned below, c;
+                    const unsigned dig = hist_pick4(c4, rank, lane, &below, &c);
+                    prefix = (prefix & ~(255u << shift)) | (dig << shift);
+                    pmask |= 255u << shift;
+                    rank -= below;
+                    cnt = c;
+                    wave_sync();
+                } while (shift > 0);
+                if (lane == 0) {
+                    red[32] = prefix;
+                    red[33] = rank;
+                    red[34] = cnt;
+                }
+            }
+            __syncthreads();
+            prefix = red[32];
+            rank = red[33];
+            cnt = red[34];
+        }
+        // prefix: the rank-(n-1)/2 element, `rank` its place among the cnt equal ones
+        rlo = rhi = prefix;
+        if ((n & 1) == 0 && rank + 1 >= cnt) {  // block-uniform: rank n/2 is the next larger value
+            unsigned m2 = 0xFFFFFFFFu;
+#pragma unroll
+            for (int i = 0; i < kSelPer; ++i)
+                if (tid + kSelT * i < n && v[i] > prefix) m2 = min(m2, v[i]);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m2 = min(m2, (unsigned)__shfl_xor((int)m2, o, 64));
+            if (lane == 0) red[40 + wv] = m2;
+            __syncthreads();
+            rhi = red[40];
+#pragma unroll
+            for (int w = 1; w < kSelNW; ++w) rhi = min(rhi, red[40 + w]);
+        }
+    }
+    // ---- the row's mask (sn_select's numpy f32 steps): bit f % 64 of word
+    // f / 64; lane l of wave w holds frame 512 i + 64 w + l at iteration i ----
+    const float a = __uint_as_float(*gmax);
+    float dr = __fdiv_rn(__uint_as_float(rlo), a);
+    if ((n & 1) == 0) dr = __fmul_rn(__fadd_rn(dr, __fdiv_rn(__uint_as_float(rhi), a)), 0.5f);
+    const float rb = __fmul_rn(3.f, dr);
+#pragma unroll
+    for (int i = 0; i < kSelPer; ++i) {
+        const int w = kSelNW * i + wv;
+        if (w >= words) break;  // wave-uniform
+        const int f = tid + kSelT * i;
+        bool bit = false;
+        if (f < n) {
+            const float d = __fdiv_rn(__uint_as_float(v[i]), a);
             bit = d > c3[f] && d > rb;
         }
         const unsigned long long m = __ballot(bit);
@@ -892,7 +1112,7 @@ static SnWs sn_ws_layout(const SnPlan& p, int F, int K, char* base) {
 // morphology (:670-684), components (:686) and the size filter (:689-691)
 // of every recording of the batch from its mask in M0, one launch per step
 // for the whole batch
-static int sn_components(const SnPlan& p, const SnWs& ws, const SnBatch& nb, bool with_gmax, aa_sn_component* out,
+static int sn_components(SnPlan& p, const SnWs& ws, const SnBatch& nb, bool with_gmax, aa_sn_component* out,
                          int max_out, long long out_stride, int32_t* n_out, int n_out_stride, hipStream_t st) {
     int maxw = 1;
     for (int k = 0; k < nb.n; ++k) maxw = std::max(maxw, (nb.nf[k] + 63) / 64);
@@ -902,17 +1122,22 @@ static int sn_components(const SnPlan& p, const SnWs& ws, const SnBatch& nb, boo
     // one launch per structuring element: rectangle kh x kw, anchor (kw / 2, kh / 2)
     auto morph = [&](int kh, int kw, int erode) -> int {
         const int ax = kw / 2, ay = kh / 2;
+        hipEvent_t e0;
+        int rc = p.timer.begin(SN_STAGE_MORPH, st, &e0);
+        if (rc != AA_OK) return rc;
         hipLaunchKernelGGL(sn_morph, gm, dim3(256), 0, st, a, b, kSnBins, nb, ws.pf, -ay, kh - 1 - ay, -ax,
                            kw - 1 - ax, erode);
         AA_LAUNCH_CHECK();
         std::swap(a, b);
-        return AA_OK;
+        return p.timer.end(SN_STAGE_MORPH, st, e0);
     };
     int rc = AA_OK;
     // MORPH_OPEN with ones(4, 4): erode, then dilate; dilate; erode
     if ((rc = morph(4, 4, 1)) || (rc = morph(4, 4, 0))) return rc;
     if ((rc = morph(p.kh_d, p.kw_d, 0)) || (rc = morph(p.kh_e, p.kw_e, 1))) return rc;
     // (counters were zeroed by sn_zero; sn_runs marks the slots of a dropped row)
+    hipEvent_t e0;
+    if ((rc = p.timer.begin(SN_STAGE_COMPONENTS, st, &e0)) != AA_OK) return rc;
     hipLaunchKernelGGL(sn_runs, dim3((kSnBins + 3) / 4, nb.n), dim3(256), 0, st, a, kSnBins, nb, ws.pf, ws.R,
                        ws.max_runs, ws.row_off, ws.row_cnt, ws.counters);
     AA_LAUNCH_CHECK();
@@ -926,20 +1151,23 @@ static int sn_components(const SnPlan& p, const SnWs& ws, const SnBatch& nb, boo
     hipLaunchKernelGGL(sn_emit, gr, dim3(256), 0, st, ws.R, ws.max_runs, p.wmin, p.hmin, ws.counters,
                        with_gmax ? ws.gmax : nullptr, ws.pf, out, max_out, out_stride, n_out, n_out_stride);
     AA_LAUNCH_CHECK();
-    return AA_OK;
+    return p.timer.end(SN_STAGE_COMPONENTS, st, e0);
 }
 
 // sn_stft64 over one recording: persistent blocks (4 per CU, the LDS limit),
 // a multiple of 8 so every XCD owns an equal share of the blocks
-static int sn_launch_stft(const SnPlan& p, const float* pcm, int64_t n, int F, float* S, int ld, unsigned* gmax,
+static int sn_launch_stft(SnPlan& p, const float* pcm, int64_t n, int F, float* S, int ld, unsigned* gmax,
                           unsigned* colmed, hipStream_t st) {
     int grid = std::min(F, 256 * 4);
     grid = (grid + 7) & ~7;
     const double2* tab = p.d_tab;
+    hipEvent_t e0;
+    int rc = p.timer.begin(SN_STAGE_STFT, st, &e0);
+    if (rc != AA_OK) return rc;
     hipLaunchKernelGGL(sn_stft64, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
                        tab + kS64TabTw1, tab + kS64TabTw2, tab + kS64TabTw3, S, ld, gmax, colmed);
     AA_LAUNCH_CHECK();
-    return AA_OK;
+    return p.timer.end(SN_STAGE_STFT, st, e0);
 }
 
 // The whole detector over K recordings of one PCM buffer (recording k:
@@ -974,15 +1202,22 @@ static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const i
         int rc = sn_launch_stft(*p, lens[k] ? pcm + offs[k] : pcm, lens[k], F, ws.S, kSnLd, gmax, colmed, st);
         if (rc != AA_OK) return rc;
         const int words = (F + 63) / 64, ldt = words * 64;
+        hipEvent_t e0;
+        if ((rc = p->timer.begin(SN_STAGE_TRANSPOSE, st, &e0)) != AA_OK) return rc;
         hipLaunchKernelGGL(sn_transpose, dim3((kSnBins + 63) / 64, words), dim3(256), 0, st, ws.S, F, ldt, ws.ST, gmax,
                            colmed, c3);
         AA_LAUNCH_CHECK();
-        if (F <= kSnStageMax)
+        if ((rc = p->timer.end(SN_STAGE_TRANSPOSE, st, e0)) != AA_OK) return rc;
+        if ((rc = p->timer.begin(SN_STAGE_SELECT, st, &e0)) != AA_OK) return rc;
+        if (p->select_reg && F <= kSelT * kSelPer)
+            hipLaunchKernelGGL(sn_select_reg, dim3(kSnBins), dim3(kSelT), 0, st, ws.ST, ldt, F, gmax, c3, words, M0);
+        else if (F <= kSnStageMax)
             hipLaunchKernelGGL(sn_select<true>, dim3(kSnBins), dim3(256), sizeof(unsigned) * F, st, ws.ST, ldt, F, gmax,
                                c3, words, M0);
         else
             hipLaunchKernelGGL(sn_select<false>, dim3(kSnBins), dim3(256), 0, st, ws.ST, ldt, F, gmax, c3, words, M0);
         AA_LAUNCH_CHECK();
+        if ((rc = p->timer.end(SN_STAGE_SELECT, st, e0)) != AA_OK) return rc;
     }
     if (mask_out)
         AA_HIP(hipMemcpyAsync(mask_out, ws.M0, 8 * (size_t)kSnBins * ((nb.nf[0] + 63) / 64), hipMemcpyDeviceToDevice,
@@ -1032,6 +1267,7 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
         delete p;
         return rc;
     }
+    if (const char* e = std::getenv("AA_SN_SELECT")) p->select_reg = std::strcmp(e, "reg") == 0;
     // sn_stft64's tables, rounded from long double
     auto wexp = [](long long e, long long m) {  // exp(-2 pi i e / m)
         const long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)(e % m) / (long double)m;
@@ -1046,7 +1282,8 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
             const double fac = (double)i * step + start;
             w[i] = 0.5 + 0.5 * std::cos(fac);
         }
-        for (int n = 0; n < 2048; ++n) tab[n] = make_double2(w[2 * n], w[2 * n + 1]);
+        // halved (exact): the real split's factor 1/2 rides on the window
+        for (int n = 0; n < 2048; ++n) tab[n] = make_double2(0.5 * w[2 * n], 0.5 * w[2 * n + 1]);
     }
     for (int k1 = 1; k1 < 16; ++k1)
         for (int t = 0; t < kS64T; ++t) tab[kS64TabTw1 + (k1 - 1) * kS64T + t] = wexp((long long)(t >> 3) * k1, 256);
@@ -1069,6 +1306,7 @@ extern "C" int aa_sn_destroy(void* plan) {
     SnPlan* p = static_cast<SnPlan*>(plan);
     if (!p) return AA_OK;
     (void)hipFree(p->d_tab);
+    p->timer.release();
     delete p;
     return AA_OK;
 }
@@ -1157,4 +1395,45 @@ extern "C" int aa_sn_spectrogram(void* plan, const float* pcm, int64_t n_samples
     AA_CHECK(ld >= kSnBins && ld <= (int64_t(1) << 20), AA_ERR_INVALID, "aa_sn_spectrogram: ld %lld", (long long)ld);
     const int F = sn_frames(*p, n_samples);
     return sn_launch_stft(*p, pcm, n_samples, F, out, (int)ld, nullptr, nullptr, static_cast<hipStream_t>(stream));
+}
+
+// Launch stages of aa_sn_run / aa_sn_run_batch and their timing (the
+// aa_fe_stage_* contract); an item is one STFT frame of one recording.
+//   stft: the f64 transform (2.5 N log2 N + the window's N), PCM read once
+//         (hop samples per frame) + the S row written;
+//   transpose: S read + ST written; select: ST read + the mask bits written;
+//   morph: per launch the mask read and written (bits); components: the mask read.
+extern "C" int aa_sn_n_stages(const void* plan) { return plan ? SN_N_STAGES : -1; }
+
+extern "C" int aa_sn_stage_info(const void* plan, int32_t stage, char* name, int32_t name_len,
+                                double* flops_per_item, double* bytes_per_item) {
+    const SnPlan* p = static_cast<const SnPlan*>(plan);
+    AA_CHECK(p && stage >= 0 && stage < SN_N_STAGES, AA_ERR_INVALID, "aa_sn_stage_info: bad stage");
+    const double N = p->cfg.n_fft, B = kSnBins, hop = p->cfg.hop_length;
+    double fl = 0, by = 0;
+    const char* nm = "";
+    switch (stage) {
+        case SN_STAGE_STFT: nm = "sn_stft64"; fl = 2.5 * N * std::log2(N) + N; by = 4 * hop + 4 * B; break;
+        case SN_STAGE_TRANSPOSE: nm = "sn_transpose"; by = 8 * B; break;
+        case SN_STAGE_SELECT: nm = "sn_select"; by = 4 * B + B / 8; break;
+        case SN_STAGE_MORPH: nm = "sn_morph"; by = B / 4; break;
+        default: nm = "sn_components"; by = B / 8; break;
+    }
+    if (name && name_len > 0) snprintf(name, name_len, "%s", nm);
+    if (flops_per_item) *flops_per_item = fl;
+    if (bytes_per_item) *bytes_per_item = by;
+    return AA_OK;
+}
+
+extern "C" int aa_sn_set_timing(void* plan, uint32_t stage_mask) {
+    SnPlan* p = static_cast<SnPlan*>(plan);
+    AA_CHECK(p, AA_ERR_INVALID, "aa_sn_set_timing: null plan");
+    p->timer.mask = stage_mask;
+    return AA_OK;
+}
+
+extern "C" int aa_sn_stage_time(void* plan, int32_t stage, double* total_ms, int64_t* count) {
+    SnPlan* p = static_cast<SnPlan*>(plan);
+    AA_CHECK(p && stage >= 0 && stage < SN_N_STAGES, AA_ERR_INVALID, "aa_sn_stage_time: bad stage");
+    return p->timer.collect(stage, total_ms, count);
 }

@@ -58,6 +58,7 @@ GATED = ("bf16x3", "f32")
 # bf16 rate.
 PEAK = {"bf16": 2500.0, "bf16x3": 2500.0 / 3, "f32": 157.3, "fp8": 5000.0}
 VALU_F32_PEAK = 157.3                   # FP32 VALU TFLOP/s (fma counted as 2)
+VALU_F64_PEAK = 78.6                    # FP64 VALU TFLOP/s (AMD MI355X spec; half the FP32 vector rate)
 HBM_PEAK_GBS = 8000.0
 WORKLOAD = ("config2: 64 windows/step (39 of clip A + 25 of clip B, 60 s 48 kHz mono), "
             "htk log-mel n_fft 4096 hop 640 160 mel + model1 CNN")
@@ -78,7 +79,7 @@ def parse(argv=None):
                     help="bf16x3: split-bf16 (gated, default); fp8: OCP e4m3fn CNN (BASELINE configs[4])")
     ap.add_argument("--logmel", default="f32", choices=["f32", "f16"],
                     help="log-mel dtype between the front end and the CNN (f16: BASELINE configs[4])")
-    ap.add_argument("--secondary", default="serial,f32,bf16,fp8,fp8_f16mel,cold",
+    ap.add_argument("--secondary", default="serial,f32,bf16,fp8,fp8_f16mel,cold,config3,config4",
                     help="N=1 only: extra modes measured into the same line ('' disables)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bound on the CPU-baseline sample (0 disables)")
@@ -360,6 +361,39 @@ def collect(owner_stages, n_win):
     return out
 
 
+def stage_bound(name, precision):
+    """(bound, peak, unit) of a launch stage by kernel name."""
+    if name.startswith("fe_stft"):
+        return "valu", VALU_F32_PEAK, "TFLOP/s"
+    if name.startswith("sn_stft64"):
+        return "valu_f64", VALU_F64_PEAK, "TFLOP/s"
+    if name.startswith(("fe_", "sn_", "head", "pool", "track")):
+        return "hbm", HBM_PEAK_GBS, "GB/s"
+    return "mfma", PEAK[precision], "TFLOP/s"
+
+
+def stage_table(owners, precision):
+    """Per-stage time and roofline from HIP-event stage timing: owners =
+    [(StageTiming object, items processed while timed, per_what)]; returns
+    (rows, dominant row).  achieved = algorithmic flops (bytes) per item x
+    items / total event time of the stage's launches."""
+    rows = []
+    for obj, items, per in owners:
+        for i in range(obj.n_stages()):
+            ms, cnt = obj.stage_time(i)
+            if cnt == 0:
+                continue
+            name, fl, by = obj.stage_info(i)
+            b, pk, unit = stage_bound(name, precision)
+            work = (by * items / 1e9) if unit == "GB/s" else (fl * items / 1e12)
+            a = work / (ms * 1e-3)
+            rows.append({"kernel": name, "bound": b, "total_ms": round(ms, 4), "launches": cnt,
+                         "ms_per_" + per: round(ms / max(items, 1) * (WINDOWS_PER_CLIP if per == "clip" else 1), 5),
+                         "achieved": round(a, 2), "peak": pk, "unit": unit, "frac": round(a / pk, 4)})
+    dom = max(rows, key=lambda r: r["total_ms"]) if rows else None
+    return rows, dom
+
+
 def main_step(args, world, rank, dev):
     from tools.make_models import make_model
     tmp = tempfile.mkdtemp(prefix="aa_bench_")
@@ -518,7 +552,15 @@ def main_step(args, world, rank, dev):
                 if d > LOGIT_GATE:
                     gate_fail = f"{args.precision}: max|dlogit| {d:.3e} > {LOGIT_GATE}"
         sec = {}
-        for mode in [m for m in args.secondary.split(",") if m]:
+        modes = [m for m in args.secondary.split(",") if m]
+        for mode in [m for m in modes if m.startswith("config")]:
+            # BASELINE configs[2] / configs[3] as bounded runs on this GPU, each
+            # with the roofline of its own dominant kernel
+            if mode == "config3":
+                sec[mode] = run_stream(args, 1, rank, dev, clips=96, roofline=True)
+            elif mode == "config4":
+                sec[mode] = run_corpus(args, 1, rank, dev, files=96, roofline=True)
+        for mode in [m for m in modes if not m.startswith("config")]:
             # "fp8_f16mel": BASELINE configs[4] (fp16 log-mel + fp8 CNN)
             prec = args.precision if mode in ("cold", "serial") else mode.split("_")[0]
             if mode == args.precision:
@@ -575,6 +617,12 @@ def main_step(args, world, rank, dev):
 
 
 def main_stream(args, world, rank, dev):
+    out = run_stream(args, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def run_stream(args, world, rank, dev, clips=None, roofline=False):
     """configs[2]: clips streamed through aa_amd.stream.StreamRunner (host PCM
     -> pinned staging -> copy stream, double-buffered against the kernels),
     model1+model2+model3 sharing one front end; one 0-60 s track per clip
@@ -597,21 +645,22 @@ def main_stream(args, world, rank, dev):
     runner = StreamRunner(paths, fe_s, precision=args.precision, device=dev, max_windows=8 * WINDOWS_PER_CLIP,
                           max_samples=8 * len(pool[0]))
 
-    def clips(n, first=0):
+    def clip_iter(n, first=0):
         return (Recording(key=first + i, pcm=pool[i % len(pool)], tracks=[Track()]) for i in range(n))
 
-    for _ in runner.run(clips(32)):
+    n_clips = int(clips or args.clips)
+    for _ in runner.run(clip_iter(32)):
         pass
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    results = list(runner.run(clips(args.clips, first=rank * args.clips)))
+    results = list(runner.run(clip_iter(n_clips, first=rank * n_clips)))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    assert len(results) == args.clips
+    assert len(results) == n_clips
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     n_gathered = len(results)
     if world > 1:
@@ -619,20 +668,32 @@ def main_stream(args, world, rank, dev):
         rec = shard.pack_records([k for k, _, _ in results], [ti for _, ti, _ in results],
                                  np.stack([s for _, _, s in results]), width=runner.L)
         n_gathered = int(shard.gather_records(torch.from_numpy(rec).to(dev)).shape[0])
-        assert n_gathered == world * args.clips
+        assert n_gathered == world * n_clips
     elapsed = float(t.item())
-    out = {"metric": METRIC, "value": round(world * args.clips * 60.0 / elapsed, 1), "unit": "audio-s/s",
-           "n_gpus": world, "steps": args.clips, "warmup": 32,
-           "ms_per_step": round(1e3 * elapsed / args.clips, 4), "higher_is_better": True, "scaling": "weak",
+    out = {"metric": METRIC, "value": round(world * n_clips * 60.0 / elapsed, 1), "unit": "audio-s/s",
+           "n_gpus": world, "steps": n_clips, "warmup": 32,
+           "ms_per_step": round(1e3 * elapsed / n_clips, 4), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": args.precision,
            "data": "synthetic (48 kHz int16-quantised noise+chirps, seeded), seeded random-init model1/2/3",
            "config": {"workload": "config3: 60 s clips streamed from host memory, 39 windows each, "
                                   "model1+model2+model3 ensemble, 8 clips per batch",
                       "model": "model1+model2+model3", "global_batch": 8 * WINDOWS_PER_CLIP * world,
-                      "seq_len": fe_s.win_len, "parallelism": f"dp{world}", "clips_per_rank": args.clips,
+                      "seq_len": fe_s.win_len, "parallelism": f"dp{world}", "clips_per_rank": n_clips,
                       "records_gathered": n_gathered}}
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    if roofline:
+        # the stream's kernels, HIP events around every launch over 16 more
+        # clips (untimed for the value above)
+        objs = [runner.fe] + list(runner.models)
+        for o in objs:
+            o.set_timing(True)
+        list(runner.run(clip_iter(16)))
+        torch.cuda.synchronize()
+        for o in objs:
+            o.set_timing(False)
+        rows, dom = stage_table([(o, 16 * WINDOWS_PER_CLIP, "clip") for o in objs], args.precision)
+        out["roofline"] = dict(dom, timed_on="HIP events around every launch of 16 streamed clips",
+                               stages=rows)
+    return out
 
 
 def _write_clip(path, seed):
@@ -641,6 +702,12 @@ def _write_clip(path, seed):
 
 
 def main_corpus(args, world, rank, dev):
+    out = run_corpus(args, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def run_corpus(args, world, rank, dev, files=None, roofline=False):
     """configs[3]: a corpus of 60 s WAV files through the whole analyse path
     (aa_amd.corpus: decode, signal_noise, tracks, classify() with model1,
     post-processing to the reference's per-file JSON), files sharded one per
@@ -652,7 +719,7 @@ def main_corpus(args, world, rank, dev):
     from tools.make_models import make_model
     root = Path(tempfile.mkdtemp(prefix="aa_bench4_"))
     model = make_model(root / "model1", "model1", seed=1)
-    n = args.files
+    n = int(files or args.files)
     files = [root / f"clip{i:05d}.wav" for i in range(n * world)]
     # every rank writes its own share (plus file 0 for the warm-up) into its own
     # temp dir, on a pool of host processes
@@ -696,8 +763,39 @@ def main_corpus(args, world, rank, dev):
                       "seq_len": 48000 * 60, "parallelism": f"dp{n_gpus}", "host_procs_per_gpu": ppg,
                       "files_per_rank": n,
                       "documents_gathered": len(res), "tracks_classified": n_pred}}
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    if roofline:
+        # the corpus path's kernels (signal_noise, get_end, front end, CNN),
+        # HIP events around every launch over 32 more files (untimed above)
+        from aa_amd.pipeline import Classifier
+        from aa_amd.signals import detector
+        clf = Classifier.shared(device=dev)
+        det = detector(48000, 281, dev)
+        fes, mods = list(clf._fes.values()), list(clf._models.values())
+        objs = [det] + fes + mods
+        for o in objs:
+            o.set_timing(True)
+        w0 = clf.windows_done
+        sub = files[:32]
+        lanes_env = os.environ.get("AA_BATCH_LANES")
+        os.environ["AA_BATCH_LANES"] = "1"  # one host thread: the stage timers are not shared across lanes
+        try:
+            corpus.run(sub, models, rank=0, world=1, batch=args.batch)
+            torch.cuda.synchronize()
+        finally:
+            if lanes_env is None:
+                os.environ.pop("AA_BATCH_LANES")
+            else:
+                os.environ["AA_BATCH_LANES"] = lanes_env
+        for o in objs:
+            o.set_timing(False)
+        wins = clf.windows_done - w0
+        frames = len(sub) * det.n_frames(48000 * 60)
+        rows, dom = stage_table([(det, frames, "frame")] + [(o, wins, "window") for o in fes + mods], "bf16x3")
+        per_file = {r["kernel"]: round(r["total_ms"] / len(sub), 4) for r in rows}
+        out["roofline"] = dict(dom, timed_on=f"HIP events around every launch of {len(sub)} corpus files "
+                                             f"({frames} signal_noise frames, {wins} windows)",
+                               ms_per_file=per_file, stages=rows)
+    return out
 
 
 def worker(local, world, args, port=None):

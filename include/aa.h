@@ -322,6 +322,14 @@ int aa_sn_run_batch(void* plan, const float* pcm, const int64_t* offsets, const 
  * magnitude): out = device f32 [F][ld] (F = aa_sn_n_frames, ld >= 2049), row f
  * = frame f's 2049 bins.  No workspace. */
 int aa_sn_spectrogram(void* plan, const float* pcm, int64_t n_samples, float* out, int64_t ld, void* stream);
+/* Launch stages of aa_sn_run / aa_sn_run_batch (0 sn_stft64, 1 sn_transpose,
+ * 2 sn_select, 3 sn_morph, 4 the component launches) and their timing, the
+ * aa_fe_stage_* contract; an item is one STFT frame of one recording. */
+int aa_sn_n_stages(const void* plan);
+int aa_sn_stage_info(const void* plan, int32_t stage, char* name, int32_t name_len, double* flops_per_item,
+                     double* bytes_per_item);
+int aa_sn_set_timing(void* plan, uint32_t stage_mask);
+int aa_sn_stage_time(void* plan, int32_t stage, double* total_ms, int64_t* count);
 /* Morphology, components and filter of a given mask (mask_out's layout). */
 int aa_sn_components_from_mask(void* plan, const uint64_t* mask, int64_t n_frames, void* workspace,
                                size_t workspace_bytes, aa_sn_component* out, int32_t max_out,

@@ -103,7 +103,7 @@ def test_mean_group_plus_pre_model(gpu, model_root, tmp_path, monkeypatch):
     assert len(seen["views"]) == 1 and len(seen["scores"]) == 2
     pcm, views = seen["pcm"][0], seen["views"][0]
     s = pipeline.fe_settings_from_meta(groups[0][0][1], 48000)
-    assert s.hop == 640  # not the pre-model's 281
+    assert s.hop_length == 640  # not the pre-model's 281
     cfg = bench.fe_config(s)
     oracle_means = []
     worst = 0.0
