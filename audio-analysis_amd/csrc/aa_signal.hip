@@ -52,7 +52,8 @@ enum { R_X0 = 0, R_X1, R_Y, R_P, R_LEFT, R_RIGHT, R_TOP, R_BOT, R_AREA, R_KEY };
 // .y = k).
 // launch stages (aa_sn_stage_*): per recording stft / transpose / select,
 // per batch the four morphology launches and the component launches
-enum { SN_STAGE_STFT = 0, SN_STAGE_TRANSPOSE, SN_STAGE_SELECT, SN_STAGE_MORPH, SN_STAGE_COMPONENTS, SN_N_STAGES };
+enum { SN_STAGE_STFT = 0, SN_STAGE_TRANSPOSE, SN_STAGE_SELECT, SN_STAGE_MORPH, SN_STAGE_COMPONENTS, SN_STAGE_COLMED,
+       SN_N_STAGES };
 constexpr int kSnMaxBatch = 64;
 struct SnBatch {
     int n;
@@ -68,9 +69,10 @@ struct SnPlan {
     int kh_d = 0, kw_d = 0;  // cv2.dilate(ones((height, width))) (:683)
     int kh_e = 0, kw_e = 0;  // cv2.erode(ones((height // 10, width))) (:684)
     int wmin = 0, hmin = 0;  // kept: width >= wmin, height >= hmin (:689-691)
-    double2* d_tab = nullptr;  // sn_stft64's tables: window pairs [2048], tw1 [15][128], tw2 [16][128], tw3 [128]
+    double2* d_tab = nullptr;  // sn_stft64's tables (kS64Tab*)
     StageTimer timer;          // HIP events around the launches of the stages in timer.mask
     bool select_reg = false;   // row medians by sn_select_reg (AA_SN_SELECT=reg; A/B knob) or sn_select
+    int diag = 0;              // AA_SN_DIAG: ablation bits of sn_select_reg (tools only; results then invalid)
 };
 
 __device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
@@ -80,6 +82,22 @@ __device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
         if (lane >= o) v += t;
     }
     return v;
+}
+
+// One histogram increment per active lane, wave-aggregated: the lanes that
+// share the first active lane's bucket add their count with ONE atomic, the
+// rest add one each.  A row of near-equal magnitudes (a quiet band: every
+// value in one or two buckets, pass after pass) otherwise serialises 64 LDS
+// atomics on one address per wave-instruction.
+__device__ __forceinline__ void hist_add(unsigned* H, unsigned b, bool act) {
+    const unsigned long long m = __ballot(act);
+    if (m == 0) return;  // wave-uniform
+    const int leader = __builtin_ctzll(m);
+    const unsigned bl = __builtin_amdgcn_readlane(b, leader);
+    const bool same = act && b == bl;
+    const unsigned long long ms = __ballot(same);
+    if ((threadIdx.x & 63) == leader) atomicAdd(&H[bl], (unsigned)__popcll(ms));
+    if (act && !same) atomicAdd(&H[b], 1u);
 }
 
 // sn_zero: the counters a run accumulates into (atomicMax / atomicAdd), one
@@ -231,130 +249,81 @@ __device__ __forceinline__ unsigned hist_pick(const unsigned* hist, unsigned ran
 
 // sn_stft64 geometry: 128 threads per frame; the 2048 complex points z[n] =
 // x[2n] + i x[2n + 1] of the 4096-sample real frame, n = 128 n1 + 8 n2 + n3,
-// bins k = k1 + 16 k2 + 256 k3:
+// bins k = k1 + 16 k2 + 256 k3, m = k1 + 16 k2:
 //   1. thread (n2, n3): DFT-16 over n1, twiddle W256^(n2 k1)
-//   2. thread (k1, n3): DFT-16 over n2, twiddle W2048^(n3 (k1 + 16 k2))
-//   3. thread j owns columns m = k1 + 16 k2 = j and 256 - j (thread 0: 0 and
-//      128): DFT-8 over n3 gives Z[m + 256 k3], and Z[2048 - k] of every k it
-//      holds sits in its other column, so the real split needs no exchange:
+//   2. thread (k1, n3): DFT-16 over n2 (the remaining twiddle W2048^(n3 m)
+//      moves to step 3, where it is per-column)
+//   3. thread j owns columns m = j and 256 - j (thread 0: 0 and 128):
+//      twiddle W2048^(n3 m), DFT-8 over n3 gives Z[m + 256 k3].  The second
+//      column's twiddle is W8^n3 conj(W2048^(n3 j)), and a W8^n3 factor on a
+//      DFT-8's input shifts its output by one bin, so both columns use the same
+//      7 twiddles.  Z[2048 - k] of every k the thread holds sits in its other
+//      column, so the real split needs no exchange:
 //      X[k] = E + W4096^k O, X[2048 - k] = conj(E - W4096^k O),
 //      E = (Z[k] + conj Z[2048 - k]) / 2, O = -i (Z[k] - conj Z[2048 - k]) / 2.
+// The step-1 twiddles depend on n2 only (a wave-instruction reads 8 distinct
+// table entries), the step-3 ones on the thread: 7 x 16 B per thread and
+// frame from L2, the window stays in registers.
 // LDS: one 36,864-B buffer holds each exchange in turn (step-1 rows of 136
 // double2 per k1, step-2 columns of 9 double2: both read conflict-free by
-// ds_read_b128), then the frame's 2049 magnitudes and the median histograms.
+// ds_read_b128), then the frame's 2049 magnitudes.
+// AA_SN_WIN_REG: the window in 64 VGPRs across frames (1) or read from L2
+// per frame (0)
+#ifndef AA_SN_WIN_REG
+#define AA_SN_WIN_REG 0
+#endif
 constexpr int kS64T = 128;
 constexpr int kS64R1 = 136;
 constexpr int kS64C2 = 9;
 constexpr int kS64Buf = 256 * kS64C2;  // double2
 constexpr int kS64Mag = 64;            // float offset of the magnitudes (after column 0's 8 double2)
-constexpr int kS64Hist = 2240;         // unsigned offset of the histograms (after the magnitudes)
-constexpr int kS64TabTw1 = 2048, kS64TabTw2 = kS64TabTw1 + 15 * kS64T, kS64TabTw3 = kS64TabTw2 + 16 * kS64T,
-              kS64TabN = kS64TabTw3 + kS64T;  // double2 entries of SnPlan::d_tab
-static_assert(16 * kS64R1 <= kS64Buf && (kS64Hist + 1024) * 4 <= kS64Buf * 16, "sn_stft64 LDS");
-
-// The median over bins of one frame (numpy, odd count 2049: the middle
-// element) by radix select on the bit patterns of the block's 2049 values
-// (v[i] = bin t + 128 i, v[16] = bin 2048 on thread 0).  8-bit digits start
-// below the bits the frame's min and max share; one histogram copy per wave,
-// two sets used alternately so a pass needs two barriers.
-__device__ __forceinline__ unsigned block_median_2049(const unsigned (&v)[17], int t, unsigned* hist,
-                                                      unsigned* red) {
-    const int lane = t & 63, wv = t >> 6;
-    unsigned mn = v[0], mx = v[0];
-#pragma unroll
-    for (int i = 1; i < 16; ++i) {
-        mn = min(mn, v[i]);
-        mx = max(mx, v[i]);
-    }
-    if (t == 0) {
-        mn = min(mn, v[16]);
-        mx = max(mx, v[16]);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
-        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
-    }
-    if (lane == 0) {
-        red[wv] = mn;
-        red[2 + wv] = mx;
-    }
-    uint4* h4 = reinterpret_cast<uint4*>(hist);
-    h4[t] = make_uint4(0u, 0u, 0u, 0u);
-    h4[t + kS64T] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
-    mn = min(red[0], red[1]);
-    mx = max(red[2], red[3]);
-    if (mn == mx) return mn;  // block-uniform
-    const int hb = 31 - __clz(mn ^ mx);
-    unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
-    unsigned prefix = mn & pmask, rank = kSnBins / 2;
-    int set = 0;
-#pragma unroll 1
-    for (int sh = hb - 7;; sh -= 8) {
-        const int shift = max(sh, 0);  // a last digit may repeat known prefix bits: harmless
-        unsigned* H = hist + set * 512 + wv * 256;
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            if ((v[i] & pmask) == prefix) atomicAdd(&H[(v[i] >> shift) & 255u], 1u);
-        if (t == 0 && (v[16] & pmask) == prefix) atomicAdd(&H[(v[16] >> shift) & 255u], 1u);
-        __syncthreads();
-        uint4 c = h4[set * 128 + lane];
-        const uint4 c2 = h4[set * 128 + 64 + lane];
-        c.x += c2.x;
-        c.y += c2.y;
-        c.z += c2.z;
-        c.w += c2.w;
-        h4[(set ^ 1) * 128 + t] = make_uint4(0u, 0u, 0u, 0u);  // the next pass's set
-        unsigned below, cnt;
-        const unsigned dig = hist_pick4(c, rank, lane, &below, &cnt);
-        prefix = (prefix & ~(255u << shift)) | (dig << shift);
-        pmask |= 255u << shift;
-        rank -= below;
-        if (shift == 0) break;
-        __syncthreads();
-        set ^= 1;
-    }
-    return prefix;
-}
+// SnPlan::d_tab: window pairs [2048] | tw1 [15][16] | tw3 [7][128] | split bases [128]
+constexpr int kS64TabTw1 = 2048, kS64TabTw3 = kS64TabTw1 + 15 * 16, kS64TabTwS = kS64TabTw3 + 7 * kS64T,
+              kS64TabN = kS64TabTwS + kS64T;
+static_assert(16 * kS64R1 <= kS64Buf && (kS64Mag + 2049) * 4 <= kS64Buf * 16, "sn_stft64 LDS");
 
 // sn_stft64: persistent blocks, XCD x (block b on XCD b % 8) owning frames
 // [x F / 8, (x + 1) F / 8) (neighbouring frames share 4096 - hop samples
-// through one L2).  Per frame: S row (stride ld; may be null), the running
-// maximum (gmax: atomicMax on the bit patterns, may be null) and the median
-// over bins (colmed, may be null).  win2: the f64 Hann window as pairs
-// (w[2n], w[2n + 1]); tw1 / tw2: the step-1 / step-2 twiddles per thread;
-// tw3: W4096^t (thread 0: W4096^128), the split's per-thread base.
+// through one L2).  Per frame: its S row (stride ld) and the running maximum
+// (gmax: atomicMax on the bit patterns, may be null).  win2: the f64 Hann
+// window (halved) as pairs (w[2n], w[2n + 1]); tw1: W256^(n2 k1) [k1 - 1][n2];
+// tw3: W2048^(n3 j) [n3 - 1][j]; twS: W4096^t (thread 0: W4096^128), the
+// split's per-thread base.
 __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) void sn_stft64(
     const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const double2* __restrict__ win2,
-    const double2* __restrict__ tw1, const double2* __restrict__ tw2, const double2* __restrict__ tw3,
-    float* __restrict__ S, int ld, unsigned* __restrict__ gmax, unsigned* __restrict__ colmed) {
+    const double2* __restrict__ tw1, const double2* __restrict__ tw3, const double2* __restrict__ twS,
+    float* __restrict__ S, int ld, unsigned* __restrict__ gmax) {
     __shared__ double2 buf[kS64Buf];
-    __shared__ unsigned red[4];
     const int t = threadIdx.x;
     const bool z = t == 0;
     // the recording as a buffer view: centre padding and the ends read as 0
     // (a negative offset wraps past num_records)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)pcm, 0, n_samples * 4, 0x00020000);
+#if AA_SN_WIN_REG
     double2 wv[16];  // the thread's window pairs, the same in every frame
 #pragma unroll
     for (int n1 = 0; n1 < 16; ++n1) wv[n1] = win2[128 * n1 + t];
-    const double2 tb = tw3[t];
-    const int k1b = t >> 3, n3b = t & 7;         // step 2
+#endif
+    const double2 tb = twS[t];
+    const int n2a = t >> 3;                 // step 1
+    const int k1b = t >> 3, n3b = t & 7;    // step 2
     // step 3 columns: j and 256 - j; thread 0: 0 and 128
     const int m1 = t, m2 = z ? 128 : 256 - t;
     float* mag = reinterpret_cast<float*>(buf) + kS64Mag;
-    unsigned* hist = reinterpret_cast<unsigned*>(buf) + kS64Hist;
     unsigned wmax = 0;
     const int nbx = gridDim.x >> 3;  // blocks per XCD (grid a multiple of 8)
     const int xcd = blockIdx.x & 7;
     const int f_end = (int)((long long)(xcd + 1) * n_frames / 8);
 #pragma unroll 1
     for (int fi = (int)((long long)xcd * n_frames / 8) + (blockIdx.x >> 3); fi < f_end; fi += nbx) {
-        // the twiddle tables are loop-invariant: an opaque index per frame keeps
-        // the compiler from hoisting their 31 loads into live registers
-        int ti = t;
-        __asm__ volatile("" : "+v"(ti));
+        // the twiddle tables are loop-invariant: opaque indices per frame keep
+        // the compiler from hoisting their loads into live registers
+        int i1 = n2a, i3 = t;
+        __asm__ volatile("" : "+v"(i1), "+v"(i3));
+#if !AA_SN_WIN_REG
+        int iw = t;  // the window from L2 every frame (16 x 1 KiB per wave, coalesced)
+        __asm__ volatile("" : "+v"(iw));
+#endif
         double2 v[16];
         {
             const int off = fi * hop - 2048 + 2 * t;
@@ -366,36 +335,54 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
 #pragma unroll
             for (int n1 = 0; n1 < 16; ++n1) {
                 const float xe = load_view(rs, off + 256 * n1), xo = load_view(rs, offo + 256 * n1);
-                v[n1] = make_double2((double)xe * wv[n1].x, (double)xo * wv[n1].y);
+#if AA_SN_WIN_REG
+                const double2 w = wv[n1];
+#else
+                const double2 w = win2[128 * n1 + iw];
+#endif
+                v[n1] = make_double2((double)xe * w.x, (double)xo * w.y);
             }
         }
         // ---- 1. DFT-16 over n1, twiddle, rows k1 ----
         ddft16(v);
 #pragma unroll
-        for (int k1 = 1; k1 < 16; ++k1) v[dp16(k1)] = dmul(v[dp16(k1)], tw1[(k1 - 1) * kS64T + ti]);
+        for (int k1 = 1; k1 < 16; ++k1) v[dp16(k1)] = dmul(v[dp16(k1)], tw1[(k1 - 1) * 16 + i1]);
 #pragma unroll
         for (int k1 = 0; k1 < 16; ++k1) buf[k1 * kS64R1 + t] = v[dp16(k1)];
         __syncthreads();
-        // ---- 2. DFT-16 over n2, twiddle, columns m = k1 + 16 k2 ----
+        // ---- 2. DFT-16 over n2, columns m = k1 + 16 k2 ----
 #pragma unroll
         for (int n2 = 0; n2 < 16; ++n2) v[n2] = buf[k1b * kS64R1 + 8 * n2 + n3b];
         ddft16(v);
-#pragma unroll
-        for (int k2 = 0; k2 < 16; ++k2) v[dp16(k2)] = dmul(v[dp16(k2)], tw2[k2 * kS64T + ti]);
         __syncthreads();
 #pragma unroll
         for (int k2 = 0; k2 < 16; ++k2) buf[(k1b + 16 * k2) * kS64C2 + n3b] = v[dp16(k2)];
         __syncthreads();
-        // ---- 3. DFT-8 over n3 of the thread's two columns ----
-        double2 c1[8], c2[8];
+        // ---- 3. twiddle and DFT-8 over n3 of the thread's two columns ----
+        double2 c1[8], y2[8];
 #pragma unroll
         for (int n3 = 0; n3 < 8; ++n3) {
             c1[n3] = buf[m1 * kS64C2 + n3];
-            c2[n3] = buf[m2 * kS64C2 + n3];
+            y2[n3] = buf[m2 * kS64C2 + n3];
+        }
+        __syncthreads();  // the buffer takes the magnitudes next
+        // W16^n = (cos, -sin)(2 pi n / 16), n < 8
+        constexpr double kW16r[8] = {1.0, kCos8, kRt2, kSin8, 0.0, -kSin8, -kRt2, -kCos8};
+        constexpr double kW16i[8] = {0.0, -kSin8, -kRt2, -kCos8, -1.0, -kCos8, -kRt2, -kSin8};
+#pragma unroll
+        for (int n3 = 1; n3 < 8; ++n3) {
+            const double2 w = tw3[(n3 - 1) * kS64T + i3];  // W2048^(n3 j)
+            // thread 0's second column (128) takes W16^n3 = W8^n3 conj(W16^n3):
+            // the same shift by one bin, times conj(W16^n3)
+            const double2 b2 = z ? make_double2(kW16r[n3], kW16i[n3]) : w;
+            c1[n3] = dmul(c1[n3], w);
+            y2[n3] = dmul(y2[n3], make_double2(b2.x, -b2.y));
         }
         ddft8(c1);
-        ddft8(c2);
-        __syncthreads();
+        ddft8(y2);
+        double2 c2[8];  // the second column: Z[m2 + 256 k] = y2[(k + 1) % 8]
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c2[k] = y2[(k + 1) & 7];
         // ---- real split and magnitudes into the buffer (the window carries
         // the split's factor 1/2: Z here is half the transform of z).  Slot s
         // of thread j pairs a = Z[j + 256 s] with b = Z[2048 - j - 256 s]
@@ -442,24 +429,21 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
             mag[2048] = fabsf((float)(2.0 * (z0.x - z0.y)));
         }
         __syncthreads();
-        // ---- the frame's row of S, its maximum and its median over bins ----
-        unsigned vv[17];
+        // ---- the frame's row of S and its maximum ----
+        float* srow = S + (size_t)fi * ld;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) vv[i] = __float_as_uint(mag[t + 128 * i]);
-        vv[16] = z ? __float_as_uint(mag[2048]) : 0u;
-        if (S) {
-            float* srow = S + (size_t)fi * ld;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) srow[t + 128 * i] = __uint_as_float(vv[i]);
-            if (z) srow[2048] = __uint_as_float(vv[16]);
+        for (int i = 0; i < 16; ++i) {
+            const float m = mag[t + 128 * i];
+            srow[t + 128 * i] = m;
+            // bit patterns of non-negative floats order like the values (NaN
+            // and inf above every finite value: the host reads that as
+            // non-finite input)
+            wmax = max(wmax, __float_as_uint(m));
         }
-        // bit patterns of non-negative floats order like the values (NaN and
-        // inf above every finite value: the host reads that as non-finite input)
-#pragma unroll
-        for (int i = 0; i < 17; ++i) wmax = max(wmax, vv[i]);
-        if (colmed) {
-            const unsigned med = block_median_2049(vv, t, hist, red);
-            if (z) colmed[fi] = med;
+        if (z) {
+            const float m = mag[2048];
+            srow[2048] = m;
+            wmax = max(wmax, __float_as_uint(m));
         }
         __syncthreads();  // the buffer is rewritten by the next frame
     }
@@ -468,6 +452,88 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
         for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (unsigned)__shfl_xor((int)wmax, o, 64));
         if ((t & 63) == 0 && wmax) atomicMax(gmax, wmax);
     }
+}
+
+// ---------------------------------------------------------------------------
+// The median over bins of one frame (numpy, odd count 2049: the middle
+// element) by radix select on the bit patterns, by the wave that holds the
+// frame: v[i] = bin lane + 64 i (i < 32), v[32] = bin 2048 (lane 0 only).
+// 8-bit digits start below the bits the frame's min and max share (a
+// spectrum spans a few binades: the first histogram then spreads over the
+// exponents present instead of piling onto a handful of counters), counted
+// in 4 LDS histogram copies (lane & 3 picks one: a frame's values crowd a
+// few buckets, and same-address LDS atomics serialise).  hists: the wave's
+// 4 x 256 unsigned.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned wave_median_2049(const unsigned (&v)[33], unsigned* hists, int lane) {
+    unsigned* myh = hists + (lane & 3) * kSnHist;
+    unsigned mn = v[0], mx = v[0];
+#pragma unroll
+    for (int i = 1; i < 32; ++i) {
+        mn = min(mn, v[i]);
+        mx = max(mx, v[i]);
+    }
+    if (lane == 0) {
+        mn = min(mn, v[32]);
+        mx = max(mx, v[32]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if (mn == mx) return mn;
+    const int hb = 31 - __clz(mn ^ mx);
+    unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
+    unsigned prefix = mn & pmask, rank = kSnBins / 2;
+#pragma unroll 1
+    for (int sh = hb - 7;; sh -= 8) {
+        const int shift = max(sh, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(hists + q * kSnHist)[lane] = make_uint4(0u, 0u, 0u, 0u);
+        wave_sync();
+#pragma unroll
+        for (int i = 0; i < 33; ++i)
+            hist_add(myh, (v[i] >> shift) & 255u, (i < 32 || lane == 0) && (v[i] & pmask) == prefix);
+        wave_sync();
+        {  // fold the copies into copy 0 (lane owns buckets 4 lane .. 4 lane + 3)
+            uint4 t = reinterpret_cast<uint4*>(hists)[lane];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                const uint4 u = reinterpret_cast<uint4*>(hists + q * kSnHist)[lane];
+                t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+            }
+            reinterpret_cast<uint4*>(hists)[lane] = t;
+        }
+        wave_sync();
+        unsigned below, cnt;
+        const unsigned dig = hist_pick(hists, rank, lane, &below, &cnt);
+        prefix = (prefix & ~(255u << shift)) | (dig << shift);
+        pmask |= 255u << shift;
+        rank -= below;
+        wave_sync();
+        if (shift == 0) break;
+    }
+    return prefix;
+}
+
+// sn_colmed: one wave per frame, the frame's S row (2049 floats, just
+// written by sn_stft64: L2 / Infinity-Cache resident) into registers, its
+// median over bins into colmed[f].  Four frames per 256-thread block, 4 KiB
+// of histograms per wave.
+__global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, int ld, int n_frames,
+                                                 unsigned* __restrict__ colmed) {
+    __shared__ unsigned hists[4][4 * kSnHist];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.x * 4 + wave;
+    if (f >= n_frames) return;  // wave-uniform; no block barrier below
+    const unsigned* row = reinterpret_cast<const unsigned*>(S) + (size_t)f * ld;
+    unsigned v[33];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = row[lane + 64 * i];
+    v[32] = lane == 0 ? row[2048] : 0u;
+    const unsigned med = wave_median_2049(v, hists[wave], lane);
+    if (lane == 0) colmed[f] = med;
 }
 
 // ---------------------------------------------------------------------------
@@ -549,7 +615,7 @@ __global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, in
         __syncthreads();
         for (int i = tid; i < n; i += 256) {
             const unsigned v = row[i];
-            if ((v & pmask) == prefix) atomicAdd(&hist[wv][(v >> shift) & 255u], 1u);
+            hist_add(&hist[wv][0], (v >> shift) & 255u, i < n && (v & pmask) == prefix);
         }
         __syncthreads();
         hist[0][tid] += hist[1][tid] + hist[2][tid] + hist[3][tid];
@@ -621,7 +687,7 @@ constexpr int kSelNW = kSelT / 64;
 __global__ __launch_bounds__(kSelT) __attribute__((amdgpu_waves_per_eu(4))) void sn_select_reg(const float* __restrict__ X, int ld, int n,
                                                       const unsigned* __restrict__ gmax,
                                                       const float* __restrict__ c3, int words,
-                                                      unsigned long long* __restrict__ M) {
+                                                      unsigned long long* __restrict__ M, int diag) {
     __shared__ unsigned hist[kSelNW][256];
     __shared__ unsigned cand[kSelCand];
     __shared__ unsigned red[64];
@@ -657,7 +723,7 @@ __global__ __launch_bounds__(kSelT) __attribute__((amdgpu_waves_per_eu(4))) void
         mx = max(mx, red[kSelNW + w]);
     }
     unsigned rlo = mn, rhi = mn;  // a constant row (block-uniform): its value
-    if (mn != mx) {
+    if (mn != mx && !(diag & 1)) {
         const int hb = 31 - __clz(mn ^ mx);
         unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
         unsigned prefix = mn & pmask, rank = (unsigned)(n - 1) / 2, cnt = 0;
@@ -668,7 +734,7 @@ __global__ __launch_bounds__(kSelT) __attribute__((amdgpu_waves_per_eu(4))) void
         for (;;) {
 #pragma unroll
             for (int i = 0; i < kSelPer; ++i)
-                if (tid + kSelT * i < n && (v[i] & pmask) == prefix) atomicAdd(&hist[wv][(v[i] >> shift) & 255u], 1u);
+                hist_add(&hist[wv][0], (v[i] >> shift) & 255u, tid + kSelT * i < n && (v[i] & pmask) == prefix);
             __syncthreads();
             if (tid < 256) {
                 unsigned s = hist[0][tid];
@@ -723,8 +789,8 @@ __global__ __launch_bounds__(kSelT) __attribute__((amdgpu_waves_per_eu(4))) void
                     wave_sync();
 #pragma unroll
                     for (int j = 0; j < kSelCand / 64; ++j)
-                        if (lane + 64 * j < (int)cnt && (cv[j] & pmask) == prefix)
-                            atomicAdd(&hist[lane & 3][(cv[j] >> shift) & 255u], 1u);
+                        hist_add(&hist[lane & 3][0], (cv[j] >> shift) & 255u,
+                                 lane + 64 * j < (int)cnt && (cv[j] & pmask) == prefix);
                     wave_sync();
                     uint4 c4 = reinterpret_cast<const uint4*>(&hist[0][0])[lane];
 #pragma unroll
@@ -776,6 +842,10 @@ __global__ __launch_bounds__(kSelT) __attribute__((amdgpu_waves_per_eu(4))) void
     float dr = __fdiv_rn(__uint_as_float(rlo), a);
     if ((n & 1) == 0) dr = __fmul_rn(__fadd_rn(dr, __fdiv_rn(__uint_as_float(rhi), a)), 0.5f);
     const float rb = __fmul_rn(3.f, dr);
+    if (diag & 2) {  // ablation: no mask
+        if (tid == 0) M[(size_t)blockIdx.x * words] = rlo ^ rhi;
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < kSelPer; ++i) {
         const int w = kSelNW * i + wv;
@@ -788,6 +858,133 @@ __global__ __launch_bounds__(kSelT) __attribute__((amdgpu_waves_per_eu(4))) void
         }
         const unsigned long long m = __ballot(bit);
         if (lane == 0) M[(size_t)blockIdx.x * words + w] = m;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// sn_select_row: the row median and mask of sn_select with the row in
+// registers: 256 threads x 40 values (rows of up to 10,240 frames -- a 57 s
+// recording; sn_select_reg / sn_select above that) so that 6 blocks share a
+// CU: the row's passes are latency chains (histogram, barrier, pick), and
+// rows in flight are what hides them.  Per pass every wave counts its values
+// into its own 256-bucket histogram (wave-aggregated atomics), then every
+// wave folds the four copies and picks the same bucket (two barriers per
+// pass, no broadcast).
+// ---------------------------------------------------------------------------
+constexpr int kRowT = 256, kRowPer = 41;  // 10,496 values
+
+__global__ __launch_bounds__(kRowT) __attribute__((amdgpu_waves_per_eu(6))) void sn_select_row(
+    const float* __restrict__ X, int ld, int n, const unsigned* __restrict__ gmax, const float* __restrict__ c3,
+    int words, unsigned long long* __restrict__ M) {
+    // slots past the row hold 0xFFFFFFFF: above every value (excluded from
+    // the maximum by name), never matching a prefix (non-negative values have
+    // bit 31 clear), a NaN quotient in the mask (bit 0) -- so no per-slot
+    // validity predicate stays live across the kernel
+    constexpr unsigned PAD = 0xFFFFFFFFu;
+    __shared__ unsigned hist[2][4][256];  // two sets, one per pass parity
+    __shared__ unsigned red[16];
+    const unsigned* grow = reinterpret_cast<const unsigned*>(X) + (size_t)blockIdx.x * ld;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    unsigned v[kRowPer];
+    {
+        const int lim = n - 1 - tid;  // slot i holds frame tid + 256 i: valid while 256 i <= lim
+#pragma unroll
+        for (int i = 0; i < kRowPer; ++i) {
+            const unsigned x = grow[tid + min(kRowT * i, max(lim, 0))];  // clamped: always in the row
+            v[i] = kRowT * i <= lim ? x : PAD;
+        }
+    }
+    unsigned mn = v[0], mx = 0;
+#pragma unroll
+    for (int i = 0; i < kRowPer; ++i) {
+        mn = min(mn, v[i]);
+        mx = max(mx, v[i] == PAD ? 0u : v[i]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if (lane == 0) {
+        red[wv] = mn;
+        red[4 + wv] = mx;
+    }
+    uint4* h4 = reinterpret_cast<uint4*>(&hist[0][0][0]);  // 512 uint4
+    h4[tid] = make_uint4(0u, 0u, 0u, 0u);
+    h4[tid + kRowT] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    mn = min(min(red[0], red[1]), min(red[2], red[3]));
+    mx = max(max(red[4], red[5]), max(red[6], red[7]));
+    unsigned rlo = mn, rhi = mn;  // a constant row (block-uniform): its value
+    if (mn != mx) {
+        const int hb = 31 - __clz(mn ^ mx);
+        unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
+        unsigned prefix = mn & pmask, rank = (unsigned)(n - 1) / 2, cnt = 0;
+        int set = 0;
+#pragma unroll 1
+        for (int sh = hb - 7;; sh -= 8) {
+            const int shift = max(sh, 0);  // a last digit may repeat known prefix bits: harmless
+#pragma unroll
+            for (int i = 0; i < kRowPer; ++i) hist_add(&hist[set][wv][0], (v[i] >> shift) & 255u, (v[i] & pmask) == prefix);
+            __syncthreads();
+            const uint4* hs = reinterpret_cast<const uint4*>(&hist[set][0][0]);
+            uint4 c = hs[lane];
+#pragma unroll
+            for (int w = 1; w < 4; ++w) {
+                const uint4 u = hs[64 * w + lane];
+                c.x += u.x;
+                c.y += u.y;
+                c.z += u.z;
+                c.w += u.w;
+            }
+            h4[(set ^ 1) * 256 + tid] = make_uint4(0u, 0u, 0u, 0u);  // the next pass's set
+            unsigned below, cc;
+            const unsigned dig = hist_pick4(c, rank, lane, &below, &cc);
+            prefix = (prefix & ~(255u << shift)) | (dig << shift);
+            pmask |= 255u << shift;
+            rank -= below;
+            cnt = cc;
+            if (shift == 0) break;
+            __syncthreads();  // every wave has read this set; the next set is zero
+            set ^= 1;
+        }
+        rlo = rhi = prefix;
+        if ((n & 1) == 0 && rank + 1 >= cnt) {  // block-uniform: rank n/2 is the next larger value
+            unsigned m2 = PAD;
+#pragma unroll
+            for (int i = 0; i < kRowPer; ++i) m2 = min(m2, v[i] > prefix ? v[i] : PAD);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m2 = min(m2, (unsigned)__shfl_xor((int)m2, o, 64));
+            if (lane == 0) red[8 + wv] = m2;
+            __syncthreads();
+            rhi = min(min(red[8], red[9]), min(red[10], red[11]));
+        }
+    }
+    // ---- the row's mask (sn_select's numpy f32 steps): bit f % 64 of word
+    // f / 64; lane l of wave w holds frame 256 i + 64 w + l at iteration i ----
+    const float a = __uint_as_float(*gmax);
+    float dr = __fdiv_rn(__uint_as_float(rlo), a);
+    if ((n & 1) == 0) dr = __fmul_rn(__fadd_rn(dr, __fdiv_rn(__uint_as_float(rhi), a)), 0.5f);
+    const float rb = __fmul_rn(3.f, dr);
+    constexpr int CH = 8;  // c3 loads in flight per chunk
+    int t2 = tid;  // opaque: no frame index kept live from the load phase
+    __asm__ volatile("" : "+v"(t2));
+    const float* c3t = c3 + t2;
+    const int lim2 = n - 1 - t2;
+#pragma unroll
+    for (int i0 = 0; i0 < kRowPer; i0 += CH) {
+        float cv[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) cv[j] = c3t[min(kRowT * (i0 + j), max(lim2, 0))];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int i = i0 + j;
+            if (i >= kRowPer) break;
+            const int w = 4 * i + wv;
+            const float d = __fdiv_rn(__uint_as_float(v[i]), a);  // PAD: NaN, bit 0
+            const unsigned long long m = __ballot(d > cv[j] && d > rb);
+            if (lane == 0 && w < words) M[(size_t)blockIdx.x * words + w] = m;
+        }
     }
 }
 
@@ -1157,7 +1354,7 @@ static int sn_components(SnPlan& p, const SnWs& ws, const SnBatch& nb, bool with
 // sn_stft64 over one recording: persistent blocks (4 per CU, the LDS limit),
 // a multiple of 8 so every XCD owns an equal share of the blocks
 static int sn_launch_stft(SnPlan& p, const float* pcm, int64_t n, int F, float* S, int ld, unsigned* gmax,
-                          unsigned* colmed, hipStream_t st) {
+                          hipStream_t st) {
     int grid = std::min(F, 256 * 4);
     grid = (grid + 7) & ~7;
     const double2* tab = p.d_tab;
@@ -1165,7 +1362,7 @@ static int sn_launch_stft(SnPlan& p, const float* pcm, int64_t n, int F, float* 
     int rc = p.timer.begin(SN_STAGE_STFT, st, &e0);
     if (rc != AA_OK) return rc;
     hipLaunchKernelGGL(sn_stft64, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
-                       tab + kS64TabTw1, tab + kS64TabTw2, tab + kS64TabTw3, S, ld, gmax, colmed);
+                       tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax);
     AA_LAUNCH_CHECK();
     return p.timer.end(SN_STAGE_STFT, st, e0);
 }
@@ -1199,8 +1396,13 @@ static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const i
         unsigned* colmed = sn_at(ws.colmed, ws.pf, k);
         float* c3 = sn_at(ws.c3, ws.pf, k);
         unsigned long long* M0 = sn_at(ws.M0, ws.pf, k);
-        int rc = sn_launch_stft(*p, lens[k] ? pcm + offs[k] : pcm, lens[k], F, ws.S, kSnLd, gmax, colmed, st);
+        int rc = sn_launch_stft(*p, lens[k] ? pcm + offs[k] : pcm, lens[k], F, ws.S, kSnLd, gmax, st);
         if (rc != AA_OK) return rc;
+        hipEvent_t e1;
+        if ((rc = p->timer.begin(SN_STAGE_COLMED, st, &e1)) != AA_OK) return rc;
+        hipLaunchKernelGGL(sn_colmed, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
+        AA_LAUNCH_CHECK();
+        if ((rc = p->timer.end(SN_STAGE_COLMED, st, e1)) != AA_OK) return rc;
         const int words = (F + 63) / 64, ldt = words * 64;
         hipEvent_t e0;
         if ((rc = p->timer.begin(SN_STAGE_TRANSPOSE, st, &e0)) != AA_OK) return rc;
@@ -1209,8 +1411,11 @@ static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const i
         AA_LAUNCH_CHECK();
         if ((rc = p->timer.end(SN_STAGE_TRANSPOSE, st, e0)) != AA_OK) return rc;
         if ((rc = p->timer.begin(SN_STAGE_SELECT, st, &e0)) != AA_OK) return rc;
-        if (p->select_reg && F <= kSelT * kSelPer)
-            hipLaunchKernelGGL(sn_select_reg, dim3(kSnBins), dim3(kSelT), 0, st, ws.ST, ldt, F, gmax, c3, words, M0);
+        if (!p->select_reg && F <= kRowT * kRowPer)
+            hipLaunchKernelGGL(sn_select_row, dim3(kSnBins), dim3(kRowT), 0, st, ws.ST, ldt, F, gmax, c3, words, M0);
+        else if (p->select_reg && F <= kSelT * kSelPer)
+            hipLaunchKernelGGL(sn_select_reg, dim3(kSnBins), dim3(kSelT), 0, st, ws.ST, ldt, F, gmax, c3, words, M0,
+                               p->diag);
         else if (F <= kSnStageMax)
             hipLaunchKernelGGL(sn_select<true>, dim3(kSnBins), dim3(256), sizeof(unsigned) * F, st, ws.ST, ldt, F, gmax,
                                c3, words, M0);
@@ -1268,6 +1473,7 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
         return rc;
     }
     if (const char* e = std::getenv("AA_SN_SELECT")) p->select_reg = std::strcmp(e, "reg") == 0;
+    if (const char* e = std::getenv("AA_SN_DIAG")) p->diag = std::atoi(e);
     // sn_stft64's tables, rounded from long double
     auto wexp = [](long long e, long long m) {  // exp(-2 pi i e / m)
         const long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)(e % m) / (long double)m;
@@ -1286,11 +1492,10 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
         for (int n = 0; n < 2048; ++n) tab[n] = make_double2(0.5 * w[2 * n], 0.5 * w[2 * n + 1]);
     }
     for (int k1 = 1; k1 < 16; ++k1)
-        for (int t = 0; t < kS64T; ++t) tab[kS64TabTw1 + (k1 - 1) * kS64T + t] = wexp((long long)(t >> 3) * k1, 256);
-    for (int k2 = 0; k2 < 16; ++k2)
-        for (int t = 0; t < kS64T; ++t)
-            tab[kS64TabTw2 + k2 * kS64T + t] = wexp((long long)(t & 7) * ((t >> 3) + 16 * k2), 2048);
-    for (int t = 0; t < kS64T; ++t) tab[kS64TabTw3 + t] = wexp(t ? t : 128, 4096);
+        for (int n2 = 0; n2 < 16; ++n2) tab[kS64TabTw1 + (k1 - 1) * 16 + n2] = wexp((long long)n2 * k1, 256);
+    for (int n3 = 1; n3 < 8; ++n3)
+        for (int t = 0; t < kS64T; ++t) tab[kS64TabTw3 + (n3 - 1) * kS64T + t] = wexp((long long)n3 * t, 2048);
+    for (int t = 0; t < kS64T; ++t) tab[kS64TabTwS + t] = wexp(t ? t : 128, 4096);
     hipError_t e = hipMalloc((void**)&p->d_tab, sizeof(double2) * tab.size());
     if (e == hipSuccess) e = hipMemcpy(p->d_tab, tab.data(), sizeof(double2) * tab.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -1394,7 +1599,7 @@ extern "C" int aa_sn_spectrogram(void* plan, const float* pcm, int64_t n_samples
              "aa_sn_spectrogram: %lld samples (below 2^29)", (long long)n_samples);
     AA_CHECK(ld >= kSnBins && ld <= (int64_t(1) << 20), AA_ERR_INVALID, "aa_sn_spectrogram: ld %lld", (long long)ld);
     const int F = sn_frames(*p, n_samples);
-    return sn_launch_stft(*p, pcm, n_samples, F, out, (int)ld, nullptr, nullptr, static_cast<hipStream_t>(stream));
+    return sn_launch_stft(*p, pcm, n_samples, F, out, (int)ld, nullptr, static_cast<hipStream_t>(stream));
 }
 
 // Launch stages of aa_sn_run / aa_sn_run_batch and their timing (the
@@ -1417,6 +1622,7 @@ extern "C" int aa_sn_stage_info(const void* plan, int32_t stage, char* name, int
         case SN_STAGE_TRANSPOSE: nm = "sn_transpose"; by = 8 * B; break;
         case SN_STAGE_SELECT: nm = "sn_select"; by = 4 * B + B / 8; break;
         case SN_STAGE_MORPH: nm = "sn_morph"; by = B / 4; break;
+        case SN_STAGE_COLMED: nm = "sn_colmed"; by = 4 * B; break;
         default: nm = "sn_components"; by = B / 8; break;
     }
     if (name && name_len > 0) snprintf(name, name_len, "%s", nm);
