@@ -134,6 +134,9 @@ _SIGS = {
     "aa_graph_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                    C.c_size_t, C.c_void_p]),
     "aa_graph_n_stages": (C.c_int, [C.c_void_p]),
+    "aa_graph_set_timing": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "aa_graph_time_stage": (C.c_int, [C.c_void_p, C.c_int32]),
+    "aa_graph_stage_time": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "aa_graph_stage_info": (C.c_int, [C.c_void_p, C.c_int32, C.c_char_p, C.c_int32, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]),
     "aa_track_mean": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_void_p,
@@ -233,7 +236,12 @@ class StageTiming:
         return name.value.decode(), fl.value, by.value
 
     def set_timing(self, on=True, stages=None) -> None:
-        """Time every stage (``on``) or only the stage indices in ``stages``."""
+        """Time every stage (``on``) or only the stage indices in ``stages``
+        (graphs: one stage, or every one)."""
+        if self._timing_prefix == "aa_graph" and on and stages is not None:
+            st = list(stages)
+            check(lib().aa_graph_time_stage(self._h, int(st[0]) if len(st) == 1 else -1), "aa_graph_time_stage")
+            return
         mask = 0
         if on:
             mask = 0xFFFFFFFF if stages is None else sum(1 << int(i) for i in stages)

@@ -11,7 +11,7 @@
 // (first-fit over the freed intervals).  Kernels:
 //   conv (C_in >= 16, split-bf16)  gconv_x3 (aa_gconv.h, MFMA)
 //   conv (C_in < 16, or f32 mode)  gconv_f32 (exact f32 FMA chains)
-//   depthwise conv                 gdwconv (one lane per output element)
+//   depthwise conv                 gdwconv (one lane per output pixel and 4 channels)
 //   max / avg pool, global pools   gpool2d / ggpool
 //   add, broadcast multiply        gbinary
 //   affine / activation / pow      gaffine / gpow
@@ -26,41 +26,63 @@
 
 namespace aa {
 
+// depthwise conv: one lane per (output pixel, 4 channels) when C % 4 == 0
+// (float4 taps and weights), else per (pixel, channel)
+template <int V>
 __global__ __launch_bounds__(256) void gdwconv(const float* __restrict__ in, const float* __restrict__ w,
                                                const float* __restrict__ bias, float* __restrict__ out, int Hin,
                                                int Win, int C, int Hout, int Wout, int kh, int kw, int sh, int sw,
                                                int pt, int pl, int act, float alpha) {
+    typedef __attribute__((ext_vector_type(V))) float fv;
+    const int CV = C / V;
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     const int n = blockIdx.y;
-    if (i >= (size_t)Hout * Wout * C) return;
-    const int c = (int)(i % C);
-    const int P = (int)(i / C);
+    if (i >= (size_t)Hout * Wout * CV) return;
+    const int c = (int)(i % CV) * V;
+    const int P = (int)(i / CV);
     const int oy = P / Wout, ox = P - (P / Wout) * Wout;
     const float* img = in + (size_t)n * Hin * Win * C;
-    float acc = bias ? bias[c] : 0.f;
+    fv acc;
+    for (int e = 0; e < V; ++e) acc[e] = bias ? bias[c + e] : 0.f;
     for (int ky = 0; ky < kh; ++ky) {
         const int iy = oy * sh - pt + ky;
         if (iy < 0 || iy >= Hin) continue;
         for (int kx = 0; kx < kw; ++kx) {
             const int ix = ox * sw - pl + kx;
             if (ix < 0 || ix >= Win) continue;
-            acc = fmaf(w[(ky * kw + kx) * C + c], img[((size_t)iy * Win + ix) * C + c], acc);
+            const fv wv = *reinterpret_cast<const fv*>(w + (ky * kw + kx) * C + c);
+            const fv xv = *reinterpret_cast<const fv*>(img + ((size_t)iy * Win + ix) * C + c);
+            for (int e = 0; e < V; ++e) acc[e] = fmaf(wv[e], xv[e], acc[e]);
         }
     }
-    out[(size_t)n * Hout * Wout * C + i] = gact(acc, act, alpha);
+    fv o;
+    for (int e = 0; e < V; ++e) o[e] = gact(acc[e], act, alpha);
+    *reinterpret_cast<fv*>(out + (size_t)n * Hout * Wout * C + (size_t)P * C + c) = o;
 }
 
-// global pool over H x W: one lane per (window, channel), sequential over pixels
+// global pool over H x W: a block per (window, 64 channels), 4 pixel stripes
+// of 64 lanes (coalesced channel reads), each stripe summed in pixel order,
+// the four stripes combined in a fixed order (deterministic: the same sums
+// whatever the batch)
 __global__ __launch_bounds__(256) void ggpool(const float* __restrict__ in, float* __restrict__ out, int HW, int C,
                                               int avg, int act, float alpha) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, s = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
     const int n = blockIdx.y;
-    if (c >= C) return;
-    const float* p = in + (size_t)n * HW * C + c;
     float m = avg ? 0.f : -INFINITY;
-    for (int i = 0; i < HW; ++i) m = avg ? m + p[(size_t)i * C] : fmaxf(m, p[(size_t)i * C]);
-    if (avg) m = m / (float)HW;
-    out[(size_t)n * C + c] = gact(m, act, alpha);
+    if (c < C) {
+        const float* p = in + (size_t)n * HW * C + c;
+        for (int i = s; i < HW; i += 4) m = avg ? m + p[(size_t)i * C] : fmaxf(m, p[(size_t)i * C]);
+    }
+    part[s][lane] = m;
+    __syncthreads();
+    if (s == 0 && c < C) {
+        float r = avg ? ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]))
+                      : fmaxf(fmaxf(part[0][lane], part[1][lane]), fmaxf(part[2][lane], part[3][lane]));
+        if (avg) r = r / (float)HW;
+        out[(size_t)n * C + c] = gact(r, act, alpha);
+    }
 }
 
 // a (+|*) b; b_bcast: b is [n][C] broadcast over the pixels
@@ -93,18 +115,24 @@ __global__ __launch_bounds__(256) void gpow(const float* __restrict__ in, float*
     if (i < total) out[i] = powf(in[i], e);
 }
 
-// [n][K] x [K][Cout] + bias: one lane per (window, output)
+// [n][K] x [K][Cout] + bias: one wave per (window, output), lanes striding
+// K, a fixed-order butterfly reduction (deterministic)
 __global__ __launch_bounds__(256) void gdense(const float* __restrict__ in, const float* __restrict__ w,
                                               const float* __restrict__ bias, float* __restrict__ out, int K,
                                               int Cout, int act, float alpha) {
-    const int o = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int n = blockIdx.y;
-    if (o >= Cout) return;
+    if (o >= Cout) return;  // wave-uniform
     const float* x = in + (size_t)n * K;
     float acc = 0.f;
-    for (int k = 0; k < K; ++k) acc = fmaf(x[k], w[(size_t)k * Cout + o], acc);
-    if (bias) acc += bias[o];
-    out[(size_t)n * Cout + o] = gact(acc, act, alpha);
+    for (int k = lane; k < K; k += 64) acc = fmaf(x[k], w[(size_t)k * Cout + o], acc);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) {
+        if (bias) acc += bias[o];
+        out[(size_t)n * Cout + o] = gact(acc, act, alpha);
+    }
 }
 
 __global__ __launch_bounds__(256) void gfinal(const float* __restrict__ x, float* __restrict__ logits,
@@ -138,10 +166,15 @@ struct Graph {
     size_t per_win = 0;  // workspace f32 elements per window
     int L = 0;
     int sigmoid_out = 0;
+    // HIP events around node launches (aa_graph_set_timing / aa_graph_time_stage):
+    // time_stage -1 every node, >= 0 that node only, -2 none
+    int time_stage = -2;
+    StageTimer timer;
 };
 
 static void free_graph(Graph* g) {
     if (!g) return;
+    g->timer.release();
     for (auto& nd : g->nodes) {
         (void)hipFree(nd.d_w);
         (void)hipFree(nd.d_b);
@@ -396,9 +429,14 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
             }
             break;
         case AA_G_DWCONV:
-            hipLaunchKernelGGL(gdwconv, dim3((unsigned)((per + 255) / 256), n), dim3(256), 0, st, a,
-                               (const float*)N.d_w, N.d_b, out, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw, d.pt,
-                               d.pl, act, d.alpha);
+            if ((Cin & 3) == 0)
+                hipLaunchKernelGGL(gdwconv<4>, dim3((unsigned)((per / 4 + 255) / 256), n), dim3(256), 0, st, a,
+                                   (const float*)N.d_w, N.d_b, out, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw,
+                                   d.pt, d.pl, act, d.alpha);
+            else
+                hipLaunchKernelGGL(gdwconv<1>, dim3((unsigned)((per + 255) / 256), n), dim3(256), 0, st, a,
+                                   (const float*)N.d_w, N.d_b, out, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw,
+                                   d.pt, d.pl, act, d.alpha);
             break;
         case AA_G_MAXPOOL:
         case AA_G_AVGPOOL:
@@ -408,7 +446,7 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
             break;
         case AA_G_GMAXPOOL:
         case AA_G_GAVGPOOL:
-            hipLaunchKernelGGL(ggpool, dim3((Cin + 255) / 256, n), dim3(256), 0, st, a, out, Hin * Win, Cin,
+            hipLaunchKernelGGL(ggpool, dim3((Cin + 63) / 64, n), dim3(256), 0, st, a, out, Hin * Win, Cin,
                                d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
             break;
         case AA_G_ADD:
@@ -428,7 +466,7 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                                d.alpha);
             break;
         case AA_G_DENSE:
-            hipLaunchKernelGGL(gdense, dim3((N.C + 255) / 256, n), dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
+            hipLaunchKernelGGL(gdense, dim3((N.C + 3) / 4, n), dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
                                out, Hin * Win * Cin, N.C, act, d.alpha);
             break;
         default:
@@ -489,9 +527,20 @@ extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* l
     for (int32_t c0 = 0; c0 < n; c0 += CHUNK) {
         const int32_t nc = std::min(CHUNK, n - c0);
         float* ws = static_cast<float*>(workspace);
-        for (const GNode& N : G->nodes) {
-            const int rc = graph_run_node(*G, N, x + (size_t)c0 * in_per, ws, nc, st);
+        G->timer.mask = 0xFFFFFFFFu;  // the node filter is time_stage (graphs exceed 32 stages)
+        for (size_t i = 0; i < G->nodes.size(); ++i) {
+            const bool timed = G->time_stage == -1 || G->time_stage == (int)i;
+            hipEvent_t e0 = nullptr;
+            if (timed) {
+                const int rc = G->timer.begin(0, st, &e0);
+                if (rc != AA_OK) return rc;
+            }
+            const int rc = graph_run_node(*G, G->nodes[i], x + (size_t)c0 * in_per, ws, nc, st);
             if (rc != AA_OK) return rc;
+            if (timed) {
+                const int rc2 = G->timer.end((int)i, st, e0);
+                if (rc2 != AA_OK) return rc2;
+            }
         }
         const GNode& O = G->nodes.back();
         const size_t total = (size_t)G->L * nc;
@@ -516,4 +565,27 @@ extern "C" int aa_graph_stage_info(const void* graph, int32_t stage, char* name,
     if (flops_per_item) *flops_per_item = N.flops;
     if (bytes_per_item) *bytes_per_item = N.bytes;
     return AA_OK;
+}
+
+// Node timing (the aa_model_stage_* contract, per node; a graph has more nodes
+// than a 32-bit stage mask holds): set_timing(mask != 0) times every node,
+// time_stage(k) only node k (-1 every node, -2 none).
+extern "C" int aa_graph_set_timing(void* graph, uint32_t stage_mask) {
+    Graph* G = static_cast<Graph*>(graph);
+    AA_CHECK(G, AA_ERR_INVALID, "aa_graph_set_timing: null graph");
+    G->time_stage = stage_mask ? -1 : -2;
+    return AA_OK;
+}
+
+extern "C" int aa_graph_time_stage(void* graph, int32_t stage) {
+    Graph* G = static_cast<Graph*>(graph);
+    AA_CHECK(G && stage >= -2 && stage < (int)G->nodes.size(), AA_ERR_INVALID, "aa_graph_time_stage: bad stage");
+    G->time_stage = stage;
+    return AA_OK;
+}
+
+extern "C" int aa_graph_stage_time(void* graph, int32_t stage, double* total_ms, int64_t* count) {
+    Graph* G = static_cast<Graph*>(graph);
+    AA_CHECK(G && stage >= 0 && stage < (int)G->nodes.size(), AA_ERR_INVALID, "aa_graph_stage_time: bad stage");
+    return G->timer.collect(stage, total_ms, count);
 }

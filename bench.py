@@ -62,6 +62,13 @@ VALU_F64_PEAK = 78.6                    # FP64 VALU TFLOP/s (AMD MI355X spec; ha
 HBM_PEAK_GBS = 8000.0
 WORKLOAD = ("config2: 64 windows/step (39 of clip A + 25 of clip B, 60 s 48 kHz mono), "
             "htk log-mel n_fft 4096 hop 640 160 mel + model1 CNN")
+# --model effnetv2: the "efficientnet" route of classify() (reference
+# src/identify_tracks.py:539-540: the log-mel repeated to 3 channels) through
+# an EfficientNetV2-B0-shaped graph (tools/make_models.graph_arch) on the graph
+# executor, hop 281 (T = 513)
+WORKLOADS = {"model1": WORKLOAD,
+             "effnetv2": ("config2-effnetv2: 64 windows/step (39 of clip A + 25 of clip B, 60 s 48 kHz mono), "
+                          "htk log-mel n_fft 4096 hop 281 160 mel x3 channels + EfficientNetV2-B0-shaped graph")}
 COLD_POOL = 16  # clip pairs of the cold-PCM variant: 16 x 23 MB > the 256 MiB Infinity Cache
 # clip pairs the headline rotates over (resident, 92 MB: inside the Infinity
 # Cache): kernel times depend on the data (MFMA power and clock), and one
@@ -75,6 +82,9 @@ def parse(argv=None):
                     help="ranks; without torchrun's env, bench.py spawns one process per GPU itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="model1", choices=sorted(WORKLOADS),
+                    help="model1: the build-defined sparrow-style CNN (headline); effnetv2: an EfficientNetV2-B0-"
+                         "shaped graph on 3-channel log-mel (the efficientnet route)")
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "f32", "bf16", "fp8"],
                     help="bf16x3: split-bf16 (gated, default); fp8: OCP e4m3fn CNN (BASELINE configs[4])")
     ap.add_argument("--logmel", default="f32", choices=["f32", "f16"],
@@ -107,8 +117,10 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def fe_settings():
+def fe_settings(model="model1"):
     from aa_amd.frontend import FeSettings
+    if model == "effnetv2":
+        return FeSettings(htk=True, hop_length=281, n_fft=4096, n_mels=160, break_freq=1750, channels=3)
     return FeSettings(htk=True, hop_length=640, n_fft=4096, n_mels=160, break_freq=1750)
 
 
@@ -187,7 +199,7 @@ def reference_logits(pcm, views, model_path, cfg):
     return cnn_oracle.forward(model_path, mels)[0]
 
 
-def load_traffic(n_dispatch, precision):
+def load_traffic(n_dispatch, precision, workload=WORKLOAD):
     """HBM bytes per launch of each kernel of one step, in dispatch order, from
     the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE summary of this same
     workload (tools/pmc_traffic.py; FETCH_SIZE doubled per
@@ -197,7 +209,7 @@ def load_traffic(n_dispatch, precision):
             d = json.loads(path.read_text())
         except (OSError, ValueError):
             continue
-        if (d.get("workload") == WORKLOAD and d.get("precision", "bf16") == precision
+        if (d.get("workload") == workload and d.get("precision", "bf16") == precision
                 and len(d.get("kernels", [])) == n_dispatch):
             return d, path.relative_to(ROOT).as_posix()
     return None, None
@@ -240,13 +252,15 @@ class Step:
     buffers of ``pairs`` resident clip pairs (1 = the headline; COLD_POOL =
     the cold-PCM variant, one pair per step in rotation)."""
 
-    def __init__(self, dev, rank, model_path, precision, pairs=1, first=None, lm16=False, pipeline=False):
+    def __init__(self, dev, rank, model_path, precision, pairs=1, first=None, lm16=False, pipeline=False,
+                 fe_s=None):
         from aa_amd.frontend import FrontEnd
         from aa_amd.model import Model
-        self.fe_s = fe_settings()
+        self.fe_s = fe_s or fe_settings()
         lm_dtype = torch.float16 if lm16 else torch.float32  # configs[4]: fp16 log-mel
         self.fe = FrontEnd(self.fe_s, dev, out_dtype=lm_dtype)
-        self.model = Model(model_path, (self.fe_s.n_mels, self.fe.T, 1), precision=precision, device=dev)
+        self.model = Model(model_path, (self.fe_s.n_mels, self.fe.T, self.fe_s.channels), precision=precision,
+                           device=dev)
         batches = [first] if first is not None else []
         for k in range(len(batches), pairs):
             batches.append(make_batch(rank, self.fe_s, pair=k))
@@ -361,6 +375,19 @@ def collect(owner_stages, n_win):
     return out
 
 
+def graph_stage_bound(name, flops, precision):
+    """(bound, peak, unit) of a model stage: MFMA convs against the
+    precision's matrix peak, exact-f32 VALU convs (conv_gf32_*) against the
+    FP32 VALU peak, the memory-streaming graph nodes (depthwise convs, pools,
+    add / multiply, affine, dense) against HBM."""
+    if name.startswith("conv_gf32"):
+        return "valu", VALU_F32_PEAK, "TFLOP/s"
+    if flops == 0 or name.startswith(("dwconv", "maxpool", "avgpool", "gmaxpool", "gavgpool", "add", "mul",
+                                      "affine", "pow", "dense", "head", "pool")):
+        return "hbm", HBM_PEAK_GBS, "GB/s"
+    return "mfma", PEAK[precision], "TFLOP/s"
+
+
 def stage_bound(name, precision):
     """(bound, peak, unit) of a launch stage by kernel name."""
     if name.startswith("fe_stft"):
@@ -397,11 +424,17 @@ def stage_table(owners, precision):
 def main_step(args, world, rank, dev):
     from tools.make_models import make_model
     tmp = tempfile.mkdtemp(prefix="aa_bench_")
-    model_path = make_model(Path(tmp) / "model1", "model1", seed=1)
-    first = make_batch(rank, fe_settings())
+    fe_s = fe_settings(args.model)
+    workload = WORKLOADS[args.model]
+    if args.model == "effnetv2":
+        from tools.make_models import make_graph
+        model_path = make_graph(Path(tmp) / "effnetv2", "effnetv2", in_channels=3, T=fe_s.n_frames, seed=5)
+    else:
+        model_path = make_model(Path(tmp) / "model1", "model1", seed=1)
+    first = make_batch(rank, fe_s)
     pcm_np, _, views = first
     step = Step(dev, rank, model_path, args.precision, pairs=HEAD_PAIRS, first=first, lm16=args.logmel == "f16",
-                pipeline=args.pipeline)
+                pipeline=args.pipeline, fe_s=fe_s)
     fe, model, n_win = step.fe, step.model, step.n_win
 
     for _ in range(args.warmup):
@@ -435,6 +468,12 @@ def main_step(args, world, rank, dev):
         owner.set_timing(False)
     step.pipeline, step.lanes = pipelined, lanes
     step.k, step.issued = 0, -1
+    seen_names = {}
+    for c in calib:  # a graph repeats kernel shapes: stage names made unique
+        k = seen_names.get(c["name"], 0)
+        seen_names[c["name"]] = k + 1
+        if k:
+            c["name"] = f"{c['name']}#{k}"
     dom = max(calib, key=lambda x: x["avg_ms"])
     # the dominant kernel's roofline: HIP events around its launches over a
     # timed run of the SERIAL step (K steps, back to back on one stream: the
@@ -471,11 +510,11 @@ def main_step(args, world, rank, dev):
     elif is_fe:
         bound, peak, unit = "hbm", HBM_PEAK_GBS, "GB/s"
     else:
-        bound, peak, unit = "mfma", PEAK[args.precision], "TFLOP/s"
+        bound, peak, unit = graph_stage_bound(dom["name"], dom["flops"], args.precision)
     avg_s = dom_serial["avg_ms"] * 1e-3
     achieved = (dom["bytes"] / avg_s / 1e9) if unit == "GB/s" else (dom["flops"] / avg_s / 1e12)
     traffic, traffic_src = None, None
-    tr, tr_path = load_traffic(len(launches) + 1, args.precision)  # + track_mean
+    tr, tr_path = load_traffic(len(launches) + 1, args.precision, workload)  # + track_mean
     if tr is not None:
         traffic = tr["kernels"][launches.index((dom["owner"], dom["idx"]))]["hbm_bytes"]
         traffic_src = tr_path
@@ -498,7 +537,9 @@ def main_step(args, world, rank, dev):
         elif fe_stage or c["flops"] == 0 or c["name"].startswith("head"):
             b, pk, a = "hbm", HBM_PEAK_GBS, c["bytes"] / (c["avg_ms"] * 1e-3) / 1e9
         else:
-            b, pk, a = "mfma", PEAK[args.precision], c["flops"] / (c["avg_ms"] * 1e-3) / 1e12
+            b, pk, unit_c = graph_stage_bound(c["name"], c["flops"], args.precision)
+            a = (c["bytes"] / (c["avg_ms"] * 1e-3) / 1e9) if unit_c == "GB/s" else \
+                c["flops"] / (c["avg_ms"] * 1e-3) / 1e12
         per[c["name"]] = {"bound": b, "achieved": round(a, 1), "frac": round(a / pk, 4)}
     roofline["stages"] = per
     # the same stages from a profile pass: rocprofv3's kernel trace of the
@@ -526,8 +567,8 @@ def main_step(args, world, rank, dev):
         "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": args.precision + (" (fp16 log-mel)" if args.logmel == "f16" else ""),
-        "data": "synthetic (48 kHz int16-quantised noise+chirps, seeded), seeded random-init model1",
-        "config": {"workload": WORKLOAD, "model": "model1", "global_batch": n_win * world,
+        "data": f"synthetic (48 kHz int16-quantised noise+chirps, seeded), seeded random-init {args.model}",
+        "config": {"workload": workload, "model": args.model, "global_batch": n_win * world,
                    "seq_len": step.fe_s.win_len, "parallelism": f"dp{world}",
                    "pipeline": f"{len(step.lanes)} batches in flight on {len(step.lanes)} streams"
                                if step.lanes is not None else
@@ -553,6 +594,8 @@ def main_step(args, world, rank, dev):
                     gate_fail = f"{args.precision}: max|dlogit| {d:.3e} > {LOGIT_GATE}"
         sec = {}
         modes = [m for m in args.secondary.split(",") if m]
+        if args.model != "model1":  # the other workloads are model1's
+            modes = [m for m in modes if m in ("serial", "f32")]
         for mode in [m for m in modes if m.startswith("config")]:
             # BASELINE configs[2] / configs[3] as bounded runs on this GPU, each
             # with the roofline of its own dominant kernel
@@ -570,7 +613,7 @@ def main_step(args, world, rank, dev):
                 prec = args.precision
             s2 = Step(dev, rank, model_path, prec, pairs=pairs, first=first,
                       lm16=mode.endswith("_f16mel") or (mode in ("cold", "serial") and args.logmel == "f16"),
-                      pipeline=0 if mode == "serial" else args.pipeline)
+                      pipeline=0 if mode == "serial" else args.pipeline, fe_s=fe_s)
             n2 = args.steps if mode in ("cold", "serial") or mode.startswith("pool") else max(10, args.steps // 2)
             if mode == "cold":
                 # cold and the headline step alternated three times, medians:
@@ -608,7 +651,7 @@ def main_step(args, world, rank, dev):
             out["cpu_baseline"] = {"value": round(v, 2), "unit": "audio-s/s", "cores": args.cpu_workers,
                                    "kind": "port",
                                    "sample": f"{nw} windows (the step's 64, cycled; oracle numpy FE on "
-                                             f"{args.cpu_workers} processes + torch-CPU fp32 model1 on "
+                                             f"{args.cpu_workers} processes + torch-CPU fp32 {args.model} on "
                                              f"{args.cpu_workers} threads), {dt:.1f} s"}
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -233,6 +233,13 @@ int aa_graph_forward(void* graph, const float* x, int32_t n, float* logits, floa
 /* launches of one forward ("conv_gx3_*", "dwconv_*", ...), their algorithmic
  * flops / bytes per window */
 int aa_graph_n_stages(const void* graph);
+/* Node timing (HIP events around node launches): set_timing(mask != 0) times
+ * every node, 0 none; time_stage(k) node k only (-1 every node, -2 none) --
+ * a graph has more nodes than a 32-bit mask holds.  stage_time as
+ * aa_model_stage_time. */
+int aa_graph_set_timing(void* graph, uint32_t stage_mask);
+int aa_graph_time_stage(void* graph, int32_t stage);
+int aa_graph_stage_time(void* graph, int32_t stage, double* total_ms, int64_t* count);
 int aa_graph_stage_info(const void* graph, int32_t stage, char* name, int32_t name_len, double* flops_per_item,
                         double* bytes_per_item);
 

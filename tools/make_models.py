@@ -318,6 +318,42 @@ def graph_arch(kind="effnet", n_labels=len(LABELS)):
         h = add({"type": "dropout", "name": "top_dropout", "inputs": [h]})
         add({"type": "dense", "name": "predictions", "units": n_labels, "use_bias": True, "activation": "sigmoid",
              "inputs": [h]})
+    elif kind == "effnetv2":
+        # EfficientNetV2-B0's block table (Keras applications): stem 3x3/2 -> 32,
+        # Fused-MBConv (expand conv 3x3 + project 1x1; no SE) x (1, 2, 2),
+        # MBConv (expand 1x1, depthwise 3x3, SE 0.25 of the block input, project)
+        # x (3, 5, 8), residual adds where stride 1 and widths match, head 1x1
+        # -> 1280, global average pooling, Dense + sigmoid
+        def fused(x, n, cin, cout, e, s):
+            if e == 1:
+                y = act(bn(conv(x, n + "_conv", cout, (3, 3), s=s), n + "_bn"), n + "_act")
+            else:
+                y = act(bn(conv(x, n + "_expand", cin * e, (3, 3), s=s), n + "_expand_bn"), n + "_expand_act")
+                y = bn(conv(y, n + "_project", cout, (1, 1)), n + "_project_bn")
+            if s == 1 and cin == cout:
+                y = add({"type": "add", "name": n + "_add", "inputs": [y, x]})
+            return y
+
+        def mb(x, n, cin, cout, e, s):
+            y = act(bn(conv(x, n + "_expand", cin * e, (1, 1)), n + "_expand_bn"), n + "_expand_act")
+            y = act(bn(dw(y, n + "_dw", 3, s), n + "_bn"), n + "_act")
+            y = se(y, n + "_se", cin * e, max(1, int(cin * 0.25)))
+            y = bn(conv(y, n + "_project", cout, (1, 1)), n + "_project_bn")
+            if s == 1 and cin == cout:
+                y = add({"type": "add", "name": n + "_add", "inputs": [y, x]})
+            return y
+
+        x = act(bn(conv("input", "stem_conv", 32, (3, 3), s=2), "stem_bn"), "stem_act")
+        table = [("f", 1, 3, 1, 32, 16, 1), ("f", 4, 3, 2, 16, 32, 2), ("f", 4, 3, 2, 32, 48, 2),
+                 ("m", 4, 3, 2, 48, 96, 3), ("m", 6, 3, 1, 96, 112, 5), ("m", 6, 3, 2, 112, 192, 8)]
+        for si, (typ, e, k, s, cin, cout, reps) in enumerate(table):
+            for r in range(reps):
+                n = f"block{si + 1}{chr(ord('a') + r)}"
+                x = (fused if typ == "f" else mb)(x, n, cin if r == 0 else cout, cout, e, s if r == 0 else 1)
+        h = act(bn(conv(x, "top_conv", 1280, (1, 1)), "top_bn"), "top_act")
+        h = add({"type": "globalavgpool2d", "name": "avg_pool", "inputs": [h]})
+        add({"type": "dense", "name": "predictions", "units": n_labels, "use_bias": True, "activation": "sigmoid",
+             "inputs": [h]})
     elif kind == "resnet":
         x = add({"type": "rescaling", "name": "rescale", "scale": 1.0 / 80.0, "offset": 1.0, "inputs": ["input"]})
         x = add({"type": "normalization", "name": "norm", "inputs": [x]})
@@ -387,7 +423,9 @@ def make_graph(out_dir, kind="effnet", name=None, seed=1, in_channels=1, n_mels=
     arch = graph_arch(kind, len(labels))
     rng = np.random.default_rng(seed)
     tensors = _graph_weights(arch, in_channels, rng)
-    x = calibration_input(6, n_mels, T, True, rng)
+    # (BatchNorm statistics are per channel: a deep network calibrates on a
+    # shorter excerpt, each BN needs a forward of everything before it)
+    x = calibration_input(6 if len(arch) < 80 else 3, n_mels, T if len(arch) < 80 else min(T, 160), True, rng)
     if in_channels > 1:
         x = np.repeat(x, in_channels, axis=3)
     xt = torch.from_numpy(x).double().permute(0, 3, 1, 2)
