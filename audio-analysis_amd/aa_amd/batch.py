@@ -51,7 +51,9 @@ SR = 48000
 class Decoded:
     """A decoded recording: ``s16`` (interleaved int16 samples as a view of a
     pinned slot, ``channels`` of them per frame) or ``f32`` (mono samples at
-    ``sr_in``, resampled to 48 kHz on the device as they are uploaded)."""
+    ``sr_in``, resampled to 48 kHz on the device as they are uploaded; parity
+    unpinned for those: aa_amd.resample is held to libsoxr HQ's specification,
+    not to its samples, see its header)."""
     n: int                   # frames at 48 kHz
     sr: int                  # 48000
     s16: object = None       # numpy int16 [n * channels] (view into a pinned slot)

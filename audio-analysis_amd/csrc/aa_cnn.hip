@@ -1313,9 +1313,9 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
             const bool pooled = s.ph > 1 || s.pw > 1;
             float* conv_out = pooled ? tmp : static_cast<float*>(out);
             const int gact_ = s.act == ACT_LEAKY ? GACT_LEAKY : s.act == ACT_RELU ? GACT_RELU : GACT_NONE;
-            hipLaunchKernelGGL(gconv_x3, dim3((s.Hc * s.Wc + 63) / 64, s.cout_pad / 64, n), dim3(256), 0, st,
+            hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2>), dim3((s.Hc * s.Wc + 63) / 64, s.cout_pad / 64, n), dim3(256), 0, st,
                                (const float*)in, (const uint16_t*)s.d_w, s.d_b, conv_out, g, s.cout_pad, gact_,
-                               s.alpha);
+                               s.alpha, nullptr, nullptr);
             AA_LAUNCH_CHECK();
             if (pooled) {  // max pool after the (monotonic) activation: the pool of the activated values
                 const size_t items = (size_t)s.Hout * s.Wout * s.cout;

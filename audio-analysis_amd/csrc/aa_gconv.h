@@ -47,100 +47,159 @@ typedef __attribute__((ext_vector_type(4))) float gf32x4;
 
 constexpr int GX_ROW = 48;  // bf16 per LDS row: 32 + 16 B of padding (96 B)
 
-// weights: [tap][cin_pad / 32][cout_pad][64] bf16, per row 32 hi then 32 lo
-static __global__ __launch_bounds__(256) void gconv_x3(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
-                                                const float* __restrict__ bias, float* __restrict__ out,
-                                                ConvGeom g, int cout_pad, int act, float alpha) {
-    __shared__ __attribute__((aligned(16))) uint16_t Ah[64 * GX_ROW], Al[64 * GX_ROW];
-    __shared__ __attribute__((aligned(16))) uint16_t Bh[64 * GX_ROW], Bl[64 * GX_ROW];
+// weights: [tap][cin_pad / 32][cout_pad][64] bf16, per row 32 hi then 32 lo.
+// Tile: BM = WM MF 16 output pixels x BN = WN NF 16 output channels, the four
+// waves WM x WN over it, each MF x NF fragments (64 x 64 by default; narrow
+// layers take 128 x 32 or 256 x 16 so that C_out = 16 / 32 does not pay for 64
+// padded channels).  cout_pad is a multiple of BN.
+// Optional fusions (nullptr: off): in_scale [n][Cin] multiplies the input
+// channels as they are staged (a squeeze-and-excite Multiply before the conv,
+// the same f32 product the separate node computes), res [n][HWo][Cout] is
+// added after the bias and before the activation (a residual Add after a
+// conv without activation; the add's own activation is `act`).  The next K
+// step's pixels and weights are loaded into registers before this step's
+// MFMAs, so their latency hides behind the matrix work.
+template <int WM, int WN, int MF, int NF>
+__global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
+                                                 const float* __restrict__ bias, float* __restrict__ out,
+                                                 ConvGeom g, int cout_pad, int act, float alpha,
+                                                 const float* __restrict__ in_scale, const float* __restrict__ res) {
+    static_assert(WM * WN == 4, "four waves");
+    constexpr int BM = WM * MF * 16, BN = WN * NF * 16, AI = BM / 64;
+    __shared__ __attribute__((aligned(16))) uint16_t Ah[BM * GX_ROW], Al[BM * GX_ROW];
+    __shared__ __attribute__((aligned(16))) uint16_t Bh[BN * GX_ROW], Bl[BN * GX_ROW];
     const int n = blockIdx.z;
-    const int pix0 = blockIdx.x * 64, ch0 = blockIdx.y * 64;
+    const int pix0 = blockIdx.x * BM, ch0 = blockIdx.y * BN;
     const int HWo = g.Hout * g.Wout;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave & 1, wn = wave >> 1;
-    // staging role: row r (pixel / channel of the tile), 8-element quad q
+    const int wm = wave % WM, wn = wave / WM;
+    // staging role: rows r + 64 it (pixels) and r (weights, r < BN), 8-element quad q
     const int r = t >> 2, q = t & 3;
-    const int P = pix0 + r;
-    const bool pv = P < HWo;
-    const int oy = pv ? P / g.Wout : 0, ox = pv ? P - (P / g.Wout) * g.Wout : 0;
+    int oy[AI], ox[AI];
+    bool pv[AI];
+#pragma unroll
+    for (int it = 0; it < AI; ++it) {
+        const int P = pix0 + r + 64 * it;
+        pv[it] = P < HWo;
+        oy[it] = pv[it] ? P / g.Wout : 0;
+        ox[it] = pv[it] ? P - (P / g.Wout) * g.Wout : 0;
+    }
+    const bool bload = r < BN;
     const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
+    const float* scl = in_scale ? in_scale + (size_t)n * g.Cin : nullptr;
     const int ncc = g.cin_pad / 32;
-    gf32x4 acc[2][2];
+    const int nsteps = g.kh * g.kw * ncc;
+    gf32x4 acc[NF][MF];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NF; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < MF; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
     const bool vec = (g.Cin & 7) == 0;
-    for (int tap = 0; tap < g.kh * g.kw; ++tap) {
+    float v[AI][8];
+    uint4 wh = {0, 0, 0, 0}, wl = {0, 0, 0, 0};
+    // step s = (tap, 32-channel chunk cc): this thread's 8 channels of AI
+    // pixels and its 8 hi + 8 lo weights
+    auto load = [&](int s) {
+        const int tap = s / ncc, cc = s - (s / ncc) * ncc;
         const int ky = tap / g.kw, kx = tap - (tap / g.kw) * g.kw;
-        const int iy = oy * g.sh - g.pt + ky, ix = ox * g.sw - g.pl + kx;
-        const bool inside = pv && iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
-        const float* px = img + ((size_t)(inside ? iy : 0) * g.Win + (inside ? ix : 0)) * g.Cin;
-        for (int cc = 0; cc < ncc; ++cc) {
-            const int c0 = cc * 32 + 8 * q;
-            float v[8];
+        const int c0 = cc * 32 + 8 * q;
+#pragma unroll
+        for (int it = 0; it < AI; ++it) {
+            const int iy = oy[it] * g.sh - g.pt + ky, ix = ox[it] * g.sw - g.pl + kx;
+            const bool inside = pv[it] && iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
+            const float* px = img + ((size_t)(inside ? iy : 0) * g.Win + (inside ? ix : 0)) * g.Cin;
             if (inside && vec && c0 + 8 <= g.Cin) {
                 const float4 a = *reinterpret_cast<const float4*>(px + c0);
                 const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
-                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-                v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+                v[it][0] = a.x; v[it][1] = a.y; v[it][2] = a.z; v[it][3] = a.w;
+                v[it][4] = b.x; v[it][5] = b.y; v[it][6] = b.z; v[it][7] = b.w;
+                if (scl) {
+                    const float4 sa = *reinterpret_cast<const float4*>(scl + c0);
+                    const float4 sb = *reinterpret_cast<const float4*>(scl + c0 + 4);
+                    v[it][0] *= sa.x; v[it][1] *= sa.y; v[it][2] *= sa.z; v[it][3] *= sa.w;
+                    v[it][4] *= sb.x; v[it][5] *= sb.y; v[it][6] *= sb.z; v[it][7] *= sb.w;
+                }
             } else {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = (inside && c0 + e < g.Cin) ? px[c0 + e] : 0.f;
+                for (int e = 0; e < 8; ++e) {
+                    const bool ok = inside && c0 + e < g.Cin;
+                    v[it][e] = ok ? (scl ? px[c0 + e] * scl[c0 + e] : px[c0 + e]) : 0.f;
+                }
             }
-            gbf16x8 h, l;
+        }
+        if (bload) {
+            const uint16_t* wrow = wpk + (((size_t)s * cout_pad) + ch0 + r) * 64;
+            wh = *reinterpret_cast<const uint4*>(wrow + 8 * q);
+            wl = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
+        }
+    };
+    load(0);
+    for (int s = 0; s < nsteps; ++s) {
+        gbf16x8 h[AI], l[AI];
+#pragma unroll
+        for (int it = 0; it < AI; ++it)
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                h[e] = (__bf16)v[e];
-                l[e] = (__bf16)(v[e] - (float)h[e]);
+                h[it][e] = (__bf16)v[it][e];
+                l[it][e] = (__bf16)(v[it][e] - (float)h[it][e]);
             }
-            const uint16_t* wrow = wpk + (((size_t)(tap * ncc + cc) * cout_pad) + ch0 + r) * 64;
-            const uint4 wh = *reinterpret_cast<const uint4*>(wrow + 8 * q);
-            const uint4 wl = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
-            __syncthreads();  // the previous step's fragments are read
-            *reinterpret_cast<gbf16x8*>(Ah + r * GX_ROW + 8 * q) = h;
-            *reinterpret_cast<gbf16x8*>(Al + r * GX_ROW + 8 * q) = l;
+        __syncthreads();  // the previous step's fragments are read
+#pragma unroll
+        for (int it = 0; it < AI; ++it) {
+            *reinterpret_cast<gbf16x8*>(Ah + (r + 64 * it) * GX_ROW + 8 * q) = h[it];
+            *reinterpret_cast<gbf16x8*>(Al + (r + 64 * it) * GX_ROW + 8 * q) = l[it];
+        }
+        if (bload) {
             *reinterpret_cast<uint4*>(Bh + r * GX_ROW + 8 * q) = wh;
             *reinterpret_cast<uint4*>(Bl + r * GX_ROW + 8 * q) = wl;
-            __syncthreads();
-            const int ko = 8 * (lane >> 4);
+        }
+        __syncthreads();
+        if (s + 1 < nsteps) load(s + 1);
+        const int ko = 8 * (lane >> 4);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int wr = (wn * 32 + i * 16 + (lane & 15)) * GX_ROW + ko;
-                const gbf16x8 w_h = *reinterpret_cast<const gbf16x8*>(Bh + wr);
-                const gbf16x8 w_l = *reinterpret_cast<const gbf16x8*>(Bl + wr);
+        for (int i = 0; i < NF; ++i) {
+            const int wr = (wn * NF * 16 + i * 16 + (lane & 15)) * GX_ROW + ko;
+            const gbf16x8 w_h = *reinterpret_cast<const gbf16x8*>(Bh + wr);
+            const gbf16x8 w_l = *reinterpret_cast<const gbf16x8*>(Bl + wr);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int xr = (wm * 32 + j * 16 + (lane & 15)) * GX_ROW + ko;
-                    const gbf16x8 x_h = *reinterpret_cast<const gbf16x8*>(Ah + xr);
-                    const gbf16x8 x_l = *reinterpret_cast<const gbf16x8*>(Al + xr);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_h, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_l, x_h, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_l, acc[i][j], 0, 0, 0);
-                }
+            for (int j = 0; j < MF; ++j) {
+                const int xr = (wm * MF * 16 + j * 16 + (lane & 15)) * GX_ROW + ko;
+                const gbf16x8 x_h = *reinterpret_cast<const gbf16x8*>(Ah + xr);
+                const gbf16x8 x_l = *reinterpret_cast<const gbf16x8*>(Al + xr);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_h, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_l, x_h, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_l, acc[i][j], 0, 0, 0);
             }
         }
     }
     // D[channel][pixel]: lane holds channels 4 (lane >> 4) .. + 3 of pixel lane & 15
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int Pj = pix0 + wm * 32 + j * 16 + (lane & 15);
+    for (int j = 0; j < MF; ++j) {
+        const int Pj = pix0 + wm * MF * 16 + j * 16 + (lane & 15);
         if (Pj >= HWo) continue;
         float* o = out + ((size_t)n * HWo + Pj) * g.Cout;
+        const float* rp = res ? res + ((size_t)n * HWo + Pj) * g.Cout : nullptr;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = ch0 + wn * 32 + i * 16 + 4 * (lane >> 4);
-            float v[4];
+        for (int i = 0; i < NF; ++i) {
+            const int c = ch0 + wn * NF * 16 + i * 16 + 4 * (lane >> 4);
+            float y[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = gact(acc[i][j][e] + (c + e < g.Cout ? bias[c + e] : 0.f), act, alpha);
+            for (int e = 0; e < 4; ++e) {
+                float z = acc[i][j][e] + (c + e < g.Cout ? bias[c + e] : 0.f);
+                if (rp && c + e < g.Cout) z += rp[c + e];
+                y[e] = gact(z, act, alpha);
+            }
             if (c + 4 <= g.Cout && (g.Cout & 3) == 0) {
-                *reinterpret_cast<float4*>(o + c) = make_float4(v[0], v[1], v[2], v[3]);
+                *reinterpret_cast<float4*>(o + c) = make_float4(y[0], y[1], y[2], y[3]);
             } else {
-                for (int e = 0; e < 4 && c + e < g.Cout; ++e) o[c + e] = v[e];
+                for (int e = 0; e < 4 && c + e < g.Cout; ++e) o[c + e] = y[e];
             }
         }
     }
 }
+
+// tile of a layer with C_out output channels: BN = 16, 32 or 64
+static inline int gconv_bn(int cout) { return cout <= 16 ? 16 : cout <= 32 ? 32 : 64; }
 
 // exact f32: one thread per (output pixel, 8 output channels); weights [Cout][kh][kw][Cin]
 static __global__ __launch_bounds__(256) void gconv_f32(const float* __restrict__ in, const float* __restrict__ w,
@@ -175,6 +234,66 @@ static __global__ __launch_bounds__(256) void gconv_f32(const float* __restrict_
 #pragma unroll
     for (int c = 0; c < 8; ++c)
         if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], act, alpha);
+}
+
+// exact f32 for small K = kh kw Cin (<= GF32_KMAX, e.g. a 3-channel stem):
+// one thread per output pixel and 32 output channels (blockIdx.y), the
+// group's weights staged once per block in LDS as [K][32] and read as
+// broadcast float4s.  Each output is the same chain as gconv_f32 (bias, then
+// fma over ky, kx, ci in order): the results are identical.
+constexpr int GF32_KMAX = 384;
+static __global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restrict__ in, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, float* __restrict__ out,
+                                                     ConvGeom g, int act, float alpha) {
+    __shared__ __attribute__((aligned(16))) float sw[GF32_KMAX * 32];
+    const int n = blockIdx.z;
+    const int c0 = blockIdx.y * 32;
+    const int K = g.kh * g.kw * g.Cin;
+    for (int i = threadIdx.x; i < K * 32; i += 256) {
+        const int k = i >> 5, c = i & 31;
+        sw[i] = c0 + c < g.Cout ? w[(size_t)(c0 + c) * K + k] : 0.f;
+    }
+    __syncthreads();
+    const int P = blockIdx.x * 256 + threadIdx.x;
+    if (P >= g.Hout * g.Wout) return;
+    const int oy = P / g.Wout, ox = P - (P / g.Wout) * g.Wout;
+    const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
+    float acc[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) acc[c] = c0 + c < g.Cout ? bias[c0 + c] : 0.f;
+    for (int ky = 0; ky < g.kh; ++ky) {
+        const int iy = oy * g.sh - g.pt + ky;
+        if (iy < 0 || iy >= g.Hin) continue;
+        for (int kx = 0; kx < g.kw; ++kx) {
+            const int ix = ox * g.sw - g.pl + kx;
+            if (ix < 0 || ix >= g.Win) continue;
+            const float* px = img + ((size_t)iy * g.Win + ix) * g.Cin;
+            const float4* wk = reinterpret_cast<const float4*>(sw + (size_t)(ky * g.kw + kx) * g.Cin * 32);
+            for (int ci = 0; ci < g.Cin; ++ci) {
+                const float x = px[ci];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const float4 wv = wk[ci * 8 + c];
+                    acc[4 * c + 0] = fmaf(wv.x, x, acc[4 * c + 0]);
+                    acc[4 * c + 1] = fmaf(wv.y, x, acc[4 * c + 1]);
+                    acc[4 * c + 2] = fmaf(wv.z, x, acc[4 * c + 2]);
+                    acc[4 * c + 3] = fmaf(wv.w, x, acc[4 * c + 3]);
+                }
+            }
+        }
+    }
+    float* o = out + ((size_t)n * g.Hout * g.Wout + P) * g.Cout;
+    if ((g.Cout & 3) == 0 && c0 + 32 <= g.Cout) {
+#pragma unroll
+        for (int c = 0; c < 32; c += 4)
+            *reinterpret_cast<float4*>(o + c0 + c) = make_float4(gact(acc[c], act, alpha), gact(acc[c + 1], act, alpha),
+                                                                 gact(acc[c + 2], act, alpha),
+                                                                 gact(acc[c + 3], act, alpha));
+    } else {
+#pragma unroll
+        for (int c = 0; c < 32; ++c)
+            if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], act, alpha);
+    }
 }
 
 // max / average pooling with explicit padding (average over the taps inside

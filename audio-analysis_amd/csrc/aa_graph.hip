@@ -18,6 +18,7 @@
 //   dense                          gdense
 // every one with its activation fused.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 
@@ -60,28 +61,113 @@ __global__ __launch_bounds__(256) void gdwconv(const float* __restrict__ in, con
     *reinterpret_cast<fv*>(out + (size_t)n * Hout * Wout * C + (size_t)P * C + c) = o;
 }
 
-// global pool over H x W: a block per (window, 64 channels), 4 pixel stripes
-// of 64 lanes (coalesced channel reads), each stripe summed in pixel order,
-// the four stripes combined in a fixed order (deterministic: the same sums
-// whatever the batch)
-__global__ __launch_bounds__(256) void ggpool(const float* __restrict__ in, float* __restrict__ out, int HW, int C,
-                                              int avg, int act, float alpha) {
-    __shared__ float part[4][64];
+// global pool over H x W: a block per (window, 64 channels), 16 pixel
+// stripes of 64 lanes (coalesced channel reads), each stripe summed in pixel
+// order, the stripes combined by a fixed tree (deterministic: the same sums
+// whatever the batch; gdwconv_pool reproduces this order exactly)
+constexpr int GP_STRIPES = 16;
+__device__ __forceinline__ float gpool_combine(float (*part)[64], int lane, int avg) {
+    float v[GP_STRIPES];
+#pragma unroll
+    for (int i = 0; i < GP_STRIPES; ++i) v[i] = part[i][lane];
+#pragma unroll
+    for (int w = GP_STRIPES / 2; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; ++i) v[i] = avg ? v[i] + v[i + w] : fmaxf(v[i], v[i + w]);
+    return v[0];
+}
+
+__global__ __launch_bounds__(64 * GP_STRIPES) void ggpool(const float* __restrict__ in, float* __restrict__ out,
+                                                          int HW, int C, int avg, int act, float alpha) {
+    __shared__ float part[GP_STRIPES][64];
     const int lane = threadIdx.x & 63, s = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
     const int n = blockIdx.y;
     float m = avg ? 0.f : -INFINITY;
     if (c < C) {
         const float* p = in + (size_t)n * HW * C + c;
-        for (int i = s; i < HW; i += 4) m = avg ? m + p[(size_t)i * C] : fmaxf(m, p[(size_t)i * C]);
+        for (int i = s; i < HW; i += GP_STRIPES) m = avg ? m + p[(size_t)i * C] : fmaxf(m, p[(size_t)i * C]);
     }
     part[s][lane] = m;
     __syncthreads();
     if (s == 0 && c < C) {
-        float r = avg ? ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]))
-                      : fmaxf(fmaxf(part[0][lane], part[1][lane]), fmaxf(part[2][lane], part[3][lane]));
+        float r = gpool_combine(part, lane, avg);
         if (avg) r = r / (float)HW;
         out[(size_t)n * C + c] = gact(r, act, alpha);
+    }
+}
+
+// depthwise conv fused with the global average pool that reads it (the
+// squeeze of squeeze-and-excite): ggpool's block shape, each lane computing
+// its stripe's output pixels of one channel (exactly gdwconv's chain), storing
+// them and summing them in ggpool's order -- the map and the pooled vector
+// equal the unfused pair bit for bit.
+__global__ __launch_bounds__(64 * GP_STRIPES) void gdwconv_pool(
+    const float* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out,
+    float* __restrict__ pooled, int Hin, int Win, int C, int Hout, int Wout, int kh, int kw, int sh, int sw, int pt,
+    int pl, int act, float alpha, int pact, float palpha) {
+    __shared__ float part[GP_STRIPES][64];
+    const int lane = threadIdx.x & 63, s = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    const int n = blockIdx.y;
+    const int HW = Hout * Wout;
+    float m = 0.f;
+    if (c < C) {
+        const float* img = in + (size_t)n * Hin * Win * C + c;
+        float* o = out + (size_t)n * HW * C + c;
+        const float b = bias ? bias[c] : 0.f;
+        for (int P = s; P < HW; P += GP_STRIPES) {
+            const int oy = P / Wout, ox = P - (P / Wout) * Wout;
+            float acc = b;
+            for (int ky = 0; ky < kh; ++ky) {
+                const int iy = oy * sh - pt + ky;
+                if (iy < 0 || iy >= Hin) continue;
+                for (int kx = 0; kx < kw; ++kx) {
+                    const int ix = ox * sw - pl + kx;
+                    if (ix < 0 || ix >= Win) continue;
+                    acc = fmaf(w[(ky * kw + kx) * C + c], img[((size_t)iy * Win + ix) * C], acc);
+                }
+            }
+            const float y = gact(acc, act, alpha);
+            o[(size_t)P * C] = y;
+            m += y;
+        }
+    }
+    part[s][lane] = m;
+    __syncthreads();
+    if (s == 0 && c < C) pooled[(size_t)n * C + c] = gact(gpool_combine(part, lane, 1) / (float)HW, pact, palpha);
+}
+
+// [n][K] x W[Cout][K] + bias: one wave per (window, output), lanes striding
+// K by float4s, a fixed-order butterfly reduction (deterministic).  Dense
+// layers, and 1x1 convs on 1x1 maps (the squeeze-and-excite reduce / expand).
+__global__ __launch_bounds__(256) void gmatvec(const float* __restrict__ in, const float* __restrict__ w,
+                                               const float* __restrict__ bias, float* __restrict__ out, int K,
+                                               int Cout, int act, float alpha) {
+    const int lane = threadIdx.x & 63;
+    const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int n = blockIdx.y;
+    if (o >= Cout) return;  // wave-uniform
+    const float* x = in + (size_t)n * K;
+    const float* wr = w + (size_t)o * K;
+    float acc = 0.f;
+    if ((K & 3) == 0) {
+        for (int k = 4 * lane; k < K; k += 256) {
+            const float4 a = *reinterpret_cast<const float4*>(x + k);
+            const float4 b = *reinterpret_cast<const float4*>(wr + k);
+            acc = fmaf(a.x, b.x, acc);
+            acc = fmaf(a.y, b.y, acc);
+            acc = fmaf(a.z, b.z, acc);
+            acc = fmaf(a.w, b.w, acc);
+        }
+    } else {
+        for (int k = lane; k < K; k += 64) acc = fmaf(x[k], wr[k], acc);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) {
+        if (bias) acc += bias[o];
+        out[(size_t)n * Cout + o] = gact(acc, act, alpha);
     }
 }
 
@@ -115,26 +201,6 @@ __global__ __launch_bounds__(256) void gpow(const float* __restrict__ in, float*
     if (i < total) out[i] = powf(in[i], e);
 }
 
-// [n][K] x [K][Cout] + bias: one wave per (window, output), lanes striding
-// K, a fixed-order butterfly reduction (deterministic)
-__global__ __launch_bounds__(256) void gdense(const float* __restrict__ in, const float* __restrict__ w,
-                                              const float* __restrict__ bias, float* __restrict__ out, int K,
-                                              int Cout, int act, float alpha) {
-    const int lane = threadIdx.x & 63;
-    const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int n = blockIdx.y;
-    if (o >= Cout) return;  // wave-uniform
-    const float* x = in + (size_t)n * K;
-    float acc = 0.f;
-    for (int k = lane; k < K; k += 64) acc = fmaf(x[k], w[(size_t)k * Cout + o], acc);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    if (lane == 0) {
-        if (bias) acc += bias[o];
-        out[(size_t)n * Cout + o] = gact(acc, act, alpha);
-    }
-}
-
 __global__ __launch_bounds__(256) void gfinal(const float* __restrict__ x, float* __restrict__ logits,
                                               float* __restrict__ probs, size_t total, int sigmoid) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -147,13 +213,22 @@ __global__ __launch_bounds__(256) void gfinal(const float* __restrict__ x, float
 struct GNode {
     aa_node d;
     int H = 0, W = 0, C = 0;  // output shape
-    int mfma = 0;             // conv on gconv_x3
+    int mfma = 0;             // conv on gconv_x3t
+    int bn = 64;              // its tile's output channels (16, 32, 64)
     ConvGeom g{};
     int cout_pad = 0;
     void* d_w = nullptr;
     float* d_b = nullptr;
     float* d_b2 = nullptr;    // affine shift
     size_t off = 0;           // workspace offset (f32 elements per window)
+    // fusions (graph_build): a skipped node launches nothing; a conv may read
+    // a squeeze-and-excite scale [n][Cin] (the Multiply it replaces) and add a
+    // residual map (the Add it replaces) in its epilogue
+    bool skip = false;        // fused into a consumer: no launch, no buffer
+    bool nolaunch = false;    // written by its producer's launch (a pool fused into a dwconv)
+    int scale_src = -2, res_src = -2;
+    int pool_into = -2;       // dwconv: the global average pool node it also writes
+    int matvec = 0;           // 1x1 conv on a 1x1 map, or Dense: gmatvec on W[Cout][K]
     int last_use = 0;
     std::string name;
     double flops = 0, bytes = 0;
@@ -207,6 +282,86 @@ static const char* gop_name(int op) {
     }
 }
 
+// Fusions on the built node list (bit-identical to the unfused graph: the
+// fused kernel computes the same f32 products and sums in the same order):
+// * Multiply(x [H][W][C], s [1][1][C]) whose only consumer is an MFMA conv:
+//   the conv scales its input channels while staging (squeeze-and-excite);
+// * Add(conv, r) where the conv has no activation and no other consumer and r
+//   is computed before the conv: the conv adds r in its epilogue and applies
+//   the add's activation (the residual of an inverted-bottleneck block).
+static void graph_fuse(Graph* G) {
+    const int n = (int)G->nodes.size();
+    std::vector<int> uses(n, 0);
+    for (const GNode& N : G->nodes)
+        for (int k : {N.d.in0, N.d.in1})
+            if (k >= 0) ++uses[k];
+    auto redirect = [&](int from, int to) {
+        for (GNode& N : G->nodes) {
+            if (N.d.in0 == from) N.d.in0 = to;
+            if (N.d.in1 == from) N.d.in1 = to;
+        }
+    };
+    for (int i = 0; i < n - 1; ++i) {
+        GNode& M = G->nodes[i];
+        if (M.d.op != AA_G_MUL || M.d.act != AA_GACT_NONE || uses[i] != 1 || M.d.in1 < 0) continue;
+        const GNode& S = G->nodes[M.d.in1];
+        if (!(S.H == 1 && S.W == 1 && (M.H != 1 || M.W != 1))) continue;
+        for (int j = i + 1; j < n; ++j) {
+            GNode& K = G->nodes[j];
+            if (K.d.in0 != i && K.d.in1 != i) continue;
+            if (K.d.op == AA_G_CONV && K.mfma && K.d.in0 == i && K.scale_src == -2) {
+                K.d.in0 = M.d.in0;
+                K.scale_src = M.d.in1;
+                M.skip = true;
+            }
+            break;
+        }
+    }
+    for (int i = 0; i < n - 1; ++i) {
+        GNode& A = G->nodes[i];
+        if (A.d.op != AA_G_ADD || A.d.in1 < 0) continue;
+        for (int side = 0; side < 2; ++side) {
+            const int x = side ? A.d.in1 : A.d.in0, r = side ? A.d.in0 : A.d.in1;
+            if (x < 0) continue;
+            GNode& X = G->nodes[x];
+            if (X.d.op != AA_G_CONV || !X.mfma || X.skip || X.d.act != AA_GACT_NONE || uses[x] != 1 ||
+                X.res_src != -2 || r >= x)
+                continue;
+            const bool same = r < 0 ? (G->in_h == X.H && G->in_w == X.W && G->in_c == X.C)
+                                    : (G->nodes[r].H == X.H && G->nodes[r].W == X.W && G->nodes[r].C == X.C);
+            if (!same || r < 0) continue;  // the graph input is not a workspace buffer
+            X.res_src = r;
+            X.d.act = A.d.act;
+            X.d.alpha = A.d.alpha;
+            X.bytes += 4.0 * X.H * X.W * X.C;
+            X.name += "+add";
+            A.skip = true;
+            redirect(i, x);
+            break;
+        }
+    }
+    for (int i = 0; i + 1 < n; ++i) {
+        GNode& D = G->nodes[i];
+        GNode& P = G->nodes[i + 1];
+        if (D.d.op == AA_G_DWCONV && P.d.op == AA_G_GAVGPOOL && P.d.in0 == i && i + 1 != n - 1) {
+            D.pool_into = i + 1;
+            P.nolaunch = true;
+            D.name += "+gap";
+        }
+    }
+    for (GNode& N : G->nodes) {
+        if (N.scale_src >= 0) N.name += "+se";
+        if (N.nolaunch) {
+            N.name += "(fused)";
+            N.flops = N.bytes = 0;
+        }
+        if (N.skip) {
+            N.name += "(fused)";
+            N.flops = N.bytes = 0;
+        }
+    }
+}
+
 static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float* blob, int64_t blob_len) {
     auto get = [&](int64_t off, int64_t n) -> const float* {
         if (off < 0 || n < 0 || off + n > blob_len) return nullptr;
@@ -246,11 +401,15 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                 const float* b = d.off[1] >= 0 ? get(d.off[1], d.filters) : nullptr;
                 AA_CHECK(d.off[1] < 0 || b, AA_ERR_INVALID, "node %d: bias outside the blob", i);
                 N.g = ConvGeom{H, W, C, N.H, N.W, N.C, d.kh, d.kw, d.sh, d.sw, d.pt, d.pl, (C + 31) / 32 * 32};
-                N.mfma = G->prec == AA_PREC_BF16X3 && C >= 16;
+                // a 1x1 conv on a 1x1 map is a matrix-vector product per window
+                // (squeeze-and-excite): exact f32 on gmatvec, not a 64-pixel MFMA tile
+                N.matvec = H == 1 && W == 1 && d.kh == 1 && d.kw == 1 && d.pt == 0 && d.pl == 0;
+                N.mfma = G->prec == AA_PREC_BF16X3 && C >= 16 && !N.matvec;
                 const int ntap = d.kh * d.kw;
                 int rc;
                 if (N.mfma) {
-                    N.cout_pad = (N.C + 63) / 64 * 64;
+                    N.bn = gconv_bn(N.C);
+                    N.cout_pad = (N.C + N.bn - 1) / N.bn * N.bn;
                     std::vector<float> w_tco((size_t)ntap * N.C * C);
                     for (int t = 0; t < ntap; ++t)
                         for (int o = 0; o < N.C; ++o)
@@ -271,7 +430,8 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                 }
                 N.flops = 2.0 * N.H * N.W * K * N.C;
                 N.bytes = 4.0 * (H * W * C + N.H * N.W * N.C);
-                snprintf(nm, sizeof nm, "%s_%dx%d_s%d_%d_%d", N.mfma ? "conv_gx3" : "conv_gf32", d.kh, d.kw, d.sh, C, N.C);
+                snprintf(nm, sizeof nm, "%s_%dx%d_s%d_%d_%d", N.mfma ? "conv_gx3" : N.matvec ? "matvec" : "conv_gf32",
+                         d.kh, d.kw, d.sh, C, N.C);
                 break;
             }
             case AA_G_DWCONV: {
@@ -344,8 +504,12 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                 const float* b = d.off[1] >= 0 ? get(d.off[1], d.filters) : nullptr;
                 AA_CHECK(d.off[1] < 0 || b, AA_ERR_INVALID, "node %d: bias outside the blob", i);
                 int rc;
-                if ((rc = gupload(&N.d_w, k, (size_t)K * d.filters * 4)) != AA_OK) return rc;
+                std::vector<float> w_ok((size_t)K * d.filters);  // [Cout][K] for gmatvec
+                for (int kk = 0; kk < K; ++kk)
+                    for (int o = 0; o < d.filters; ++o) w_ok[(size_t)o * K + kk] = k[(size_t)kk * d.filters + o];
+                if ((rc = gupload(&N.d_w, w_ok.data(), w_ok.size() * 4)) != AA_OK) return rc;
                 if (b && (rc = gupload((void**)&N.d_b, b, (size_t)d.filters * 4)) != AA_OK) return rc;
+                N.matvec = 1;
                 N.H = N.W = 1;
                 N.C = d.filters;
                 N.flops = 2.0 * K * d.filters;
@@ -359,11 +523,16 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
         AA_CHECK(N.H >= 1 && N.W >= 1 && N.C >= 1, AA_ERR_INVALID, "node %d: empty output", i);
         N.name = nm;
     }
-    // liveness: a node's buffer is free after its last consumer; first fit
     const int last = n_nodes - 1;
+    if (getenv("AA_GRAPH_NOFUSE") == nullptr) graph_fuse(G);
+    // liveness: a node's buffer is free after its last consumer; first fit
+    auto inputs = [&](const GNode& N) {
+        return std::array<int, 4>{N.d.in0, N.d.in1, N.scale_src, N.res_src};
+    };
     for (int i = 0; i < n_nodes; ++i) G->nodes[i].last_use = i;
     for (int i = 0; i < n_nodes; ++i) {
-        for (int k : {G->nodes[i].d.in0, G->nodes[i].d.in1})
+        if (G->nodes[i].skip || G->nodes[i].nolaunch) continue;
+        for (int k : inputs(G->nodes[i]))
             if (k >= 0) G->nodes[k].last_use = std::max(G->nodes[k].last_use, i);
     }
     G->nodes[last].last_use = n_nodes;  // the output survives the forward
@@ -373,20 +542,27 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
     // per-window sizes rounded up to 16 floats: every buffer starts 64-B
     // aligned, so the float4 loads / stores of the kernels never straddle
     auto node_sz = [&](int k) { return align_up((size_t)G->nodes[k].H * G->nodes[k].W * G->nodes[k].C, 16); };
-    for (int i = 0; i < n_nodes; ++i) {
-        GNode& N = G->nodes[i];
-        const size_t sz = node_sz(i);
+    auto alloc = [&](int k) {
+        const size_t sz = node_sz(k);
         std::sort(live.begin(), live.end());
         size_t at = 0;
         for (auto& iv : live) {
             if (iv.first >= at + sz) break;
             at = std::max(at, iv.second);
         }
-        N.off = at;
+        G->nodes[k].off = at;
         peak = std::max(peak, at + sz);
         live.emplace_back(at, at + sz);
+        return at;
+    };
+    for (int i = 0; i < n_nodes; ++i) {
+        GNode& N = G->nodes[i];
+        if (N.skip || N.nolaunch) continue;  // (a nolaunch node is allocated with its producer)
+        const size_t sz = node_sz(i);
+        const size_t at = alloc(i);
+        if (N.pool_into >= 0) alloc(N.pool_into);
         // release the inputs whose last use is this node
-        for (int k : {N.d.in0, N.d.in1}) {
+        for (int k : inputs(N)) {
             if (k < 0 || G->nodes[k].last_use != i) continue;
             auto it = std::find(live.begin(), live.end(), std::make_pair(G->nodes[k].off, G->nodes[k].off + node_sz(k)));
             if (it != live.end()) live.erase(it);
@@ -421,15 +597,48 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
     switch (d.op) {
         case AA_G_CONV:
             if (N.mfma) {
-                hipLaunchKernelGGL(gconv_x3, dim3((N.H * N.W + 63) / 64, N.cout_pad / 64, n), dim3(256), 0, st, a,
-                                   (const uint16_t*)N.d_w, N.d_b, out, N.g, N.cout_pad, act, d.alpha);
+                ConvGeom g = N.g;
+                int nz = n;
+                if (d.kh == 1 && d.kw == 1 && d.sh == 1 && d.sw == 1 && d.pt == 0 && d.pl == 0 && N.scale_src < 0) {
+                    // pointwise: the n windows' pixels are one [1][n H W] image
+                    // (NHWC is [n][H][W][C] either way), so small maps fill whole tiles
+                    g.Hin = g.Hout = 1;
+                    g.Win = g.Wout = N.H * N.W * n;
+                    nz = 1;
+                }
+                const float* scl = N.scale_src >= 0 ? buf(N.scale_src) : nullptr;
+                const float* res = N.res_src >= 0 ? buf(N.res_src) : nullptr;
+                const int HWo = g.Hout * g.Wout;
+                if (N.bn == 16)
+                    hipLaunchKernelGGL((gconv_x3t<4, 1, 4, 1>), dim3((HWo + 255) / 256, N.cout_pad / 16, nz), dim3(256),
+                                       0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
+                                       res);
+                else if (N.bn == 32)
+                    hipLaunchKernelGGL((gconv_x3t<4, 1, 2, 2>), dim3((HWo + 127) / 128, N.cout_pad / 32, nz), dim3(256),
+                                       0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
+                                       res);
+                else
+                    hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2>), dim3((HWo + 63) / 64, N.cout_pad / 64, nz), dim3(256), 0,
+                                       st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
+                                       res);
+            } else if (N.matvec) {
+                hipLaunchKernelGGL(gmatvec, dim3((N.C + 3) / 4, n), dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
+                                   out, Cin, N.C, act, d.alpha);
+            } else if (d.kh * d.kw * Cin <= GF32_KMAX) {
+                hipLaunchKernelGGL(gconv_f32_lds, dim3((N.H * N.W + 255) / 256, (N.C + 31) / 32, n), dim3(256), 0, st,
+                                   a, (const float*)N.d_w, N.d_b, out, N.g, act, d.alpha);
             } else {
                 hipLaunchKernelGGL(gconv_f32, dim3((N.H * N.W + 255) / 256, (N.C + 7) / 8, n), dim3(256), 0, st, a,
                                    (const float*)N.d_w, N.d_b, out, N.g, act, d.alpha);
             }
             break;
         case AA_G_DWCONV:
-            if ((Cin & 3) == 0)
+            if (N.pool_into >= 0) {
+                const GNode& P = G.nodes[N.pool_into];
+                hipLaunchKernelGGL(gdwconv_pool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a,
+                                   (const float*)N.d_w, N.d_b, out, ws + P.off * (size_t)n, Hin, Win, Cin, N.H, N.W,
+                                   d.kh, d.kw, d.sh, d.sw, d.pt, d.pl, act, d.alpha, P.d.act, P.d.alpha);
+            } else if ((Cin & 3) == 0)
                 hipLaunchKernelGGL(gdwconv<4>, dim3((unsigned)((per / 4 + 255) / 256), n), dim3(256), 0, st, a,
                                    (const float*)N.d_w, N.d_b, out, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw,
                                    d.pt, d.pl, act, d.alpha);
@@ -446,7 +655,7 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
             break;
         case AA_G_GMAXPOOL:
         case AA_G_GAVGPOOL:
-            hipLaunchKernelGGL(ggpool, dim3((Cin + 63) / 64, n), dim3(256), 0, st, a, out, Hin * Win, Cin,
+            hipLaunchKernelGGL(ggpool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a, out, Hin * Win, Cin,
                                d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
             break;
         case AA_G_ADD:
@@ -466,7 +675,7 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                                d.alpha);
             break;
         case AA_G_DENSE:
-            hipLaunchKernelGGL(gdense, dim3((N.C + 3) / 4, n), dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
+            hipLaunchKernelGGL(gmatvec, dim3((N.C + 3) / 4, n), dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
                                out, Hin * Win * Cin, N.C, act, d.alpha);
             break;
         default:
@@ -529,6 +738,7 @@ extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* l
         float* ws = static_cast<float*>(workspace);
         G->timer.mask = 0xFFFFFFFFu;  // the node filter is time_stage (graphs exceed 32 stages)
         for (size_t i = 0; i < G->nodes.size(); ++i) {
+            if (G->nodes[i].skip || G->nodes[i].nolaunch) continue;
             const bool timed = G->time_stage == -1 || G->time_stage == (int)i;
             hipEvent_t e0 = nullptr;
             if (timed) {

@@ -375,15 +375,21 @@ def collect(owner_stages, n_win):
     return out
 
 
-def graph_stage_bound(name, flops, precision):
+def graph_stage_bound(name, flops, precision, nbytes=0.0):
     """(bound, peak, unit) of a model stage: MFMA convs against the
-    precision's matrix peak, exact-f32 VALU convs (conv_gf32_*) against the
-    FP32 VALU peak, the memory-streaming graph nodes (depthwise convs, pools,
-    add / multiply, affine, dense) against HBM."""
+    precision's matrix peak -- or against HBM when their f32 activations take
+    longer to stream at 8 TB/s than their MACs at the matrix peak (a 1x1 conv
+    over 112 channels is memory-bound) -- exact-f32 VALU convs (conv_gf32_*)
+    against the FP32 VALU peak, the memory-streaming graph nodes (depthwise
+    convs, pools, add / multiply, affine, dense, matrix-vector) against HBM."""
     if name.startswith("conv_gf32"):
+        if nbytes / (HBM_PEAK_GBS * 1e9) > flops / (VALU_F32_PEAK * 1e12):
+            return "hbm", HBM_PEAK_GBS, "GB/s"
         return "valu", VALU_F32_PEAK, "TFLOP/s"
     if flops == 0 or name.startswith(("dwconv", "maxpool", "avgpool", "gmaxpool", "gavgpool", "add", "mul",
-                                      "affine", "pow", "dense", "head", "pool")):
+                                      "affine", "pow", "dense", "head", "pool", "matvec")):
+        return "hbm", HBM_PEAK_GBS, "GB/s"
+    if nbytes / (HBM_PEAK_GBS * 1e9) > flops / (PEAK[precision] * 1e12):
         return "hbm", HBM_PEAK_GBS, "GB/s"
     return "mfma", PEAK[precision], "TFLOP/s"
 
@@ -426,12 +432,20 @@ def main_step(args, world, rank, dev):
     tmp = tempfile.mkdtemp(prefix="aa_bench_")
     fe_s = fe_settings(args.model)
     workload = WORKLOADS[args.model]
+    first = make_batch(rank, fe_s)
     if args.model == "effnetv2":
+        # BatchNorm statistics from the log-mels of the bench's own clips
+        # (3 windows of another seed's batch, through the oracle front end)
+        from oracle import fe_oracle
         from tools.make_models import make_graph
-        model_path = make_graph(Path(tmp) / "effnetv2", "effnetv2", in_channels=3, T=fe_s.n_frames, seed=5)
+        cal_pcm, _, cal_views = make_batch(rank + 1000, fe_s)
+        cfg = fe_config(fe_s)
+        calib = np.stack([fe_oracle.window_logmel(window_samples(cal_pcm, v, cfg["win_len"]), cfg)
+                          for v in cal_views[::len(cal_views) // 3][:3]])
+        model_path = make_graph(Path(tmp) / "effnetv2", "effnetv2", in_channels=3, T=fe_s.n_frames, seed=5,
+                                calib=calib)
     else:
         model_path = make_model(Path(tmp) / "model1", "model1", seed=1)
-    first = make_batch(rank, fe_s)
     pcm_np, _, views = first
     step = Step(dev, rank, model_path, args.precision, pairs=HEAD_PAIRS, first=first, lm16=args.logmel == "f16",
                 pipeline=args.pipeline, fe_s=fe_s)
@@ -510,7 +524,7 @@ def main_step(args, world, rank, dev):
     elif is_fe:
         bound, peak, unit = "hbm", HBM_PEAK_GBS, "GB/s"
     else:
-        bound, peak, unit = graph_stage_bound(dom["name"], dom["flops"], args.precision)
+        bound, peak, unit = graph_stage_bound(dom["name"], dom["flops"], args.precision, dom["bytes"])
     avg_s = dom_serial["avg_ms"] * 1e-3
     achieved = (dom["bytes"] / avg_s / 1e9) if unit == "GB/s" else (dom["flops"] / avg_s / 1e12)
     traffic, traffic_src = None, None
@@ -537,7 +551,7 @@ def main_step(args, world, rank, dev):
         elif fe_stage or c["flops"] == 0 or c["name"].startswith("head"):
             b, pk, a = "hbm", HBM_PEAK_GBS, c["bytes"] / (c["avg_ms"] * 1e-3) / 1e9
         else:
-            b, pk, unit_c = graph_stage_bound(c["name"], c["flops"], args.precision)
+            b, pk, unit_c = graph_stage_bound(c["name"], c["flops"], args.precision, c["bytes"])
             a = (c["bytes"] / (c["avg_ms"] * 1e-3) / 1e9) if unit_c == "GB/s" else \
                 c["flops"] / (c["avg_ms"] * 1e-3) / 1e12
         per[c["name"]] = {"bound": b, "achieved": round(a, 1), "frac": round(a / pk, 4)}

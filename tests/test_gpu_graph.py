@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 LOGIT_TOL = 1e-3
 
 
-@pytest.mark.parametrize("kind,ch,T", [("effnet", 1, 226), ("effnet", 3, 513), ("resnet", 3, 226)])
+@pytest.mark.parametrize("kind,ch,T", [("effnet", 1, 226), ("effnet", 3, 513), ("resnet", 3, 226),
+                                       ("effnetv2", 3, 226)])
 @pytest.mark.parametrize("precision", ["bf16x3", "f32"])
 def test_graph_model_matches_oracle(gpu, tmp_path, kind, ch, T, precision):
     from aa_amd.model import Model
@@ -39,6 +40,27 @@ def test_graph_model_matches_oracle(gpu, tmp_path, kind, ch, T, precision):
         assert any(n.startswith("conv_gx3_") for n in names)
     if kind == "effnet":
         assert sum(n.startswith("dwconv_") for n in names) == 3
+    if kind == "effnetv2" and precision == "bf16x3":  # SE multiply / residual add fused into the convs
+        assert any(n.endswith("+se") for n in names) and any("+add" in n for n in names)
+
+
+def test_graph_fusions_are_bit_identical(gpu, tmp_path, monkeypatch):
+    """The squeeze-excite Multiply and residual Add fused into the MFMA convs
+    (graph_fuse) give exactly the unfused graph's logits."""
+    from aa_amd.model import Model
+    p = make_graph(tmp_path / "v2", "effnetv2", in_channels=3, T=160, seed=6)
+    x = np.repeat(calibration_input(6, 160, 160, True, np.random.default_rng(2)), 3, axis=3)
+    xt = torch.from_numpy(x).cuda()
+    fused = Model(p, x.shape[1:])
+    names = [fused.stage_info(i)[0] for i in range(fused.n_stages())]
+    n_fused = sum(n.endswith("(fused)") for n in names)
+    monkeypatch.setenv("AA_GRAPH_NOFUSE", "1")
+    plain = Model(p, x.shape[1:])
+    assert not any(plain.stage_info(i)[0].endswith("(fused)") for i in range(plain.n_stages()))
+    a = fused.forward(xt)[0].cpu().numpy()
+    b = plain.forward(xt)[0].cpu().numpy()
+    print(f"{n_fused} nodes fused away")
+    assert n_fused > 10 and np.array_equal(a, b)
 
 
 def test_graph_model_large_batch_is_batch_invariant(gpu, tmp_path):

@@ -411,11 +411,16 @@ def _graph_weights(arch, in_ch, rng):
 
 
 def make_graph(out_dir, kind="effnet", name=None, seed=1, in_channels=1, n_mels=160, T=226, labels=None,
-               meta_overrides=None):
+               meta_overrides=None, calib=None):
     """A graph model (graph_arch) with seeded weights, BatchNormalization
     statistics calibrated layer by layer on dB-like inputs (float64, through
     the oracle's graph semantics) and centred logits; writes
-    audioModel.safetensors + metadata.txt like make_model."""
+    audioModel.safetensors + metadata.txt like make_model.  ``calib``
+    ([N][n_mels][T][C] log-mels, e.g. the front end's output on the inputs
+    the model will see) replaces the synthetic dB-like calibration input: a
+    deep network whose statistics were taken on another input distribution
+    amplifies its activations layer after layer (logits in the thousands),
+    which no trained network does."""
     import torch
     from safetensors.numpy import save_file
     from oracle.cnn_oracle import _forward_graph
@@ -425,9 +430,14 @@ def make_graph(out_dir, kind="effnet", name=None, seed=1, in_channels=1, n_mels=
     tensors = _graph_weights(arch, in_channels, rng)
     # (BatchNorm statistics are per channel: a deep network calibrates on a
     # shorter excerpt, each BN needs a forward of everything before it)
-    x = calibration_input(6 if len(arch) < 80 else 3, n_mels, T if len(arch) < 80 else min(T, 160), True, rng)
-    if in_channels > 1:
-        x = np.repeat(x, in_channels, axis=3)
+    if calib is not None:
+        x = np.asarray(calib, np.float32)[:, :, :T]  # full windows: a crop's statistics do not carry over
+        if x.shape[3] != in_channels:
+            x = np.repeat(x[..., :1], in_channels, axis=3)
+    else:
+        x = calibration_input(6 if len(arch) < 80 else 3, n_mels, T if len(arch) < 80 else min(T, 160), True, rng)
+        if in_channels > 1:
+            x = np.repeat(x, in_channels, axis=3)
     xt = torch.from_numpy(x).double().permute(0, 3, 1, 2)
     for i, ly in enumerate(arch):
         if ly["type"] != "batchnorm":
@@ -439,6 +449,13 @@ def make_graph(out_dir, kind="effnet", name=None, seed=1, in_channels=1, n_mels=
         tensors[ly["name"] + ".moving_variance"] = h.var(dim=(0, 2, 3), unbiased=False).float().numpy()
     dense = [ly for ly in arch if ly["type"] == "dense"][-1]["name"]
     lg, _ = _forward_graph(arch, tensors, xt, torch.float64)
+    if calib is not None:
+        # logits of a trained classifier's scale (a few units): the Dense kernel
+        # rescaled to a spread of about 2 on the calibration windows
+        sd = float(np.std(lg - lg.mean(axis=0)))
+        if sd > 2.0:
+            tensors[dense + ".kernel"] = (tensors[dense + ".kernel"] * (2.0 / sd)).astype(np.float32)
+            lg, _ = _forward_graph(arch, tensors, xt, torch.float64)
     shift = lg.mean(axis=0) - rng.normal(-0.8, 1.2, lg.shape[1])
     tensors[dense + ".bias"] = (tensors[dense + ".bias"] - shift).astype(np.float32)
     out = Path(out_dir)
