@@ -138,6 +138,112 @@ __global__ __launch_bounds__(64 * GP_STRIPES) void gdwconv_pool(
     if (s == 0 && c < C) pooled[(size_t)n * C + c] = gact(gpool_combine(part, lane, 1) / (float)HW, pact, palpha);
 }
 
+// The same two kernels 4 channels per lane (C % 4 == 0): thread t of a block
+// owns channel quad t % Q of the block's 4 Q channels and stripe t / Q
+// (GP_STRIPES stripes).  Per channel the stripes and their sums are exactly
+// the scalar kernels' (pixel order within a stripe, the same combine tree), so
+// results do not depend on Q or on which kernel ran: float4 loads give 16 lanes
+// 256 contiguous bytes per pixel, and a block of Q = 4 (64 threads) keeps a
+// small batch's grid wide enough to fill the chip.
+template <int Q>
+__global__ __launch_bounds__(Q * GP_STRIPES) void ggpool4(const float* __restrict__ in, float* __restrict__ out,
+                                                         int HW, int C, int avg, int act, float alpha) {
+    __shared__ float part[GP_STRIPES][4 * Q];
+    const int cq = threadIdx.x % Q, s = threadIdx.x / Q;
+    const int c = blockIdx.x * 4 * Q + 4 * cq;
+    const int n = blockIdx.y;
+    float4 m = avg ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    if (c < C) {
+        const float* p = in + (size_t)n * HW * C + c;
+        for (int i = s; i < HW; i += GP_STRIPES) {
+            const float4 v = *reinterpret_cast<const float4*>(p + (size_t)i * C);
+            if (avg) { m.x += v.x; m.y += v.y; m.z += v.z; m.w += v.w; }
+            else { m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w); }
+        }
+    }
+    part[s][4 * cq] = m.x; part[s][4 * cq + 1] = m.y; part[s][4 * cq + 2] = m.z; part[s][4 * cq + 3] = m.w;
+    __syncthreads();
+    const int k = threadIdx.x;  // one channel of the block per thread
+    if (k < 4 * Q && blockIdx.x * 4 * Q + k < C) {
+        float v[GP_STRIPES];
+#pragma unroll
+        for (int i = 0; i < GP_STRIPES; ++i) v[i] = part[i][k];
+#pragma unroll
+        for (int w = GP_STRIPES / 2; w >= 1; w >>= 1)
+#pragma unroll
+            for (int i = 0; i < w; ++i) v[i] = avg ? v[i] + v[i + w] : fmaxf(v[i], v[i + w]);
+        float r = v[0];
+        if (avg) r = r / (float)HW;
+        out[(size_t)n * C + blockIdx.x * 4 * Q + k] = gact(r, act, alpha);
+    }
+}
+
+// KS = 3: a 3x3 kernel, the taps unrolled and their weights held in
+// registers for every pixel; KS = 0: any kernel, weights re-read per tap
+template <int Q, int KS>
+__global__ __launch_bounds__(Q * GP_STRIPES) void gdwconv_pool4(
+    const float* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out,
+    float* __restrict__ pooled, int Hin, int Win, int C, int Hout, int Wout, int kh, int kw, int sh, int sw, int pt,
+    int pl, int act, float alpha, int pact, float palpha) {
+    __shared__ float part[GP_STRIPES][4 * Q];
+    const int cq = threadIdx.x % Q, s = threadIdx.x / Q;
+    const int c = blockIdx.x * 4 * Q + 4 * cq;
+    const int n = blockIdx.y;
+    const int HW = Hout * Wout;
+    float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < C) {
+        const float* img = in + (size_t)n * Hin * Win * C + c;
+        float* o = out + (size_t)n * HW * C + c;
+        const float4 b = bias ? *reinterpret_cast<const float4*>(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        constexpr int NW = KS ? KS * KS : 1;
+        float4 wr[NW];  // the taps' weights of this lane's channels, held for every pixel
+        if constexpr (KS > 0) {
+#pragma unroll
+            for (int t = 0; t < NW; ++t) wr[t] = *reinterpret_cast<const float4*>(w + t * C + c);
+        }
+        const int KH = KS ? KS : kh, KW = KS ? KS : kw;
+        for (int P = s; P < HW; P += GP_STRIPES) {
+            const int oy = P / Wout, ox = P - (P / Wout) * Wout;
+            float4 acc = b;
+#pragma unroll
+            for (int ky = 0; ky < KH; ++ky) {
+                const int iy = oy * sh - pt + ky;
+                if (iy < 0 || iy >= Hin) continue;
+#pragma unroll
+                for (int kx = 0; kx < KW; ++kx) {
+                    const int ix = ox * sw - pl + kx;
+                    if (ix < 0 || ix >= Win) continue;
+                    float4 wv;
+                    if constexpr (KS > 0) wv = wr[ky * KS + kx];
+                    else wv = *reinterpret_cast<const float4*>(w + (ky * kw + kx) * C + c);
+                    const float4 x = *reinterpret_cast<const float4*>(img + ((size_t)iy * Win + ix) * C);
+                    acc.x = fmaf(wv.x, x.x, acc.x);
+                    acc.y = fmaf(wv.y, x.y, acc.y);
+                    acc.z = fmaf(wv.z, x.z, acc.z);
+                    acc.w = fmaf(wv.w, x.w, acc.w);
+                }
+            }
+            const float4 y = make_float4(gact(acc.x, act, alpha), gact(acc.y, act, alpha), gact(acc.z, act, alpha),
+                                         gact(acc.w, act, alpha));
+            *reinterpret_cast<float4*>(o + (size_t)P * C) = y;
+            m.x += y.x; m.y += y.y; m.z += y.z; m.w += y.w;
+        }
+    }
+    part[s][4 * cq] = m.x; part[s][4 * cq + 1] = m.y; part[s][4 * cq + 2] = m.z; part[s][4 * cq + 3] = m.w;
+    __syncthreads();
+    const int k = threadIdx.x;
+    if (k < 4 * Q && blockIdx.x * 4 * Q + k < C) {
+        float v[GP_STRIPES];
+#pragma unroll
+        for (int i = 0; i < GP_STRIPES; ++i) v[i] = part[i][k];
+#pragma unroll
+        for (int ww = GP_STRIPES / 2; ww >= 1; ww >>= 1)
+#pragma unroll
+            for (int i = 0; i < ww; ++i) v[i] = v[i] + v[i + ww];
+        pooled[(size_t)n * C + blockIdx.x * 4 * Q + k] = gact(v[0] / (float)HW, pact, palpha);
+    }
+}
+
 // [n][K] x W[Cout][K] + bias: one wave per (window, output), lanes striding
 // K by float4s, a fixed-order butterfly reduction (deterministic).  Dense
 // layers, and 1x1 convs on 1x1 maps (the squeeze-and-excite reduce / expand).
@@ -635,9 +741,24 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
         case AA_G_DWCONV:
             if (N.pool_into >= 0) {
                 const GNode& P = G.nodes[N.pool_into];
-                hipLaunchKernelGGL(gdwconv_pool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a,
-                                   (const float*)N.d_w, N.d_b, out, ws + P.off * (size_t)n, Hin, Win, Cin, N.H, N.W,
-                                   d.kh, d.kw, d.sh, d.sw, d.pt, d.pl, act, d.alpha, P.d.act, P.d.alpha);
+                float* pooled = ws + P.off * (size_t)n;
+                if ((Cin & 3) == 0) {
+                    const bool wide = (size_t)n * ((Cin + 63) / 64) >= 1024;  // enough 256-thread blocks
+                    const bool k9 = d.kh == 3 && d.kw == 3;
+#define AA_DWP(QQ, NT)                                                                                              \
+    hipLaunchKernelGGL((gdwconv_pool4<QQ, NT>), dim3((Cin + 4 * QQ - 1) / (4 * QQ), n), dim3(QQ * GP_STRIPES), 0, st, a, \
+                       (const float*)N.d_w, N.d_b, out, pooled, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw, d.pt,  \
+                       d.pl, act, d.alpha, P.d.act, P.d.alpha)
+                    if (wide && k9) AA_DWP(16, 3);
+                    else if (wide) AA_DWP(16, 0);
+                    else if (k9) AA_DWP(4, 3);
+                    else AA_DWP(4, 0);
+#undef AA_DWP
+                } else {
+                    hipLaunchKernelGGL(gdwconv_pool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a,
+                                       (const float*)N.d_w, N.d_b, out, pooled, Hin, Win, Cin, N.H, N.W, d.kh, d.kw,
+                                       d.sh, d.sw, d.pt, d.pl, act, d.alpha, P.d.act, P.d.alpha);
+                }
             } else if ((Cin & 3) == 0)
                 hipLaunchKernelGGL(gdwconv<4>, dim3((unsigned)((per / 4 + 255) / 256), n), dim3(256), 0, st, a,
                                    (const float*)N.d_w, N.d_b, out, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw,
@@ -655,8 +776,15 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
             break;
         case AA_G_GMAXPOOL:
         case AA_G_GAVGPOOL:
-            hipLaunchKernelGGL(ggpool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a, out, Hin * Win, Cin,
-                               d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
+            if ((Cin & 3) == 0 && (size_t)n * ((Cin + 63) / 64) >= 1024)
+                hipLaunchKernelGGL((ggpool4<16>), dim3((Cin + 63) / 64, n), dim3(16 * GP_STRIPES), 0, st, a, out,
+                                   Hin * Win, Cin, d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
+            else if ((Cin & 3) == 0)
+                hipLaunchKernelGGL((ggpool4<4>), dim3((Cin + 15) / 16, n), dim3(4 * GP_STRIPES), 0, st, a, out,
+                                   Hin * Win, Cin, d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
+            else
+                hipLaunchKernelGGL(ggpool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a, out, Hin * Win,
+                                   Cin, d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
             break;
         case AA_G_ADD:
         case AA_G_MUL: {
