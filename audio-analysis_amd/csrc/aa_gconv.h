@@ -198,6 +198,154 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
     }
 }
 
+// gconv_x3p: the same split-bf16 conv for kernels larger than 1x1, with the
+// input patch of a TH x TW output tile staged once per 32-channel chunk (hi /
+// lo planes in LDS, 96-B rows) and every tap's A fragments read from it --
+// gconv_x3t gathers the tile's pixels again for every tap, i.e. reads its
+// input kh kw times through L2.  B fragments come straight from L2 (16-B
+// loads per lane), one tap ahead in registers, so the tap loop has no
+// barrier.  TH = BM / TW; patch PH x PW = ((TH - 1) sh + kh) x ((TW - 1) sw +
+// kw) pixels, dynamic LDS.  Accumulation runs chunk-major (all taps of chunk
+// 0, then chunk 1, ...).
+template <int WM, int WN, int MF, int NF>
+__global__ __launch_bounds__(256) void gconv_x3p(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
+                                                 const float* __restrict__ bias, float* __restrict__ out,
+                                                 ConvGeom g, int cout_pad, int act, float alpha, int TW, int tiles_w,
+                                                 const float* __restrict__ in_scale, const float* __restrict__ res) {
+    static_assert(WM * WN == 4, "four waves");
+    constexpr int BM = WM * MF * 16, BN = WN * NF * 16;
+    extern __shared__ __attribute__((aligned(16))) uint16_t gsm[];
+    const int TH = BM / TW;
+    const int PH = (TH - 1) * g.sh + g.kh, PW = (TW - 1) * g.sw + g.kw, NP = PH * PW;
+    uint16_t* Ph = gsm;
+    uint16_t* Pl = gsm + NP * GX_ROW;
+    const int n = blockIdx.z;
+    const int ty = blockIdx.x / tiles_w, tx = blockIdx.x - (blockIdx.x / tiles_w) * tiles_w;
+    const int oy0 = ty * TH, ox0 = tx * TW;
+    const int ch0 = blockIdx.y * BN;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave % WM, wn = wave / WM;
+    const int iy0 = oy0 * g.sh - g.pt, ix0 = ox0 * g.sw - g.pl;
+    const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
+    const float* scl = in_scale ? in_scale + (size_t)n * g.Cin : nullptr;
+    const int ncc = g.cin_pad / 32;
+    const int ntap = g.kh * g.kw;
+    // the lane's fragment pixels: patch index of tap (0, 0)
+    int pb[MF];
+#pragma unroll
+    for (int j = 0; j < MF; ++j) {
+        const int p = wm * MF * 16 + j * 16 + (lane & 15);
+        const int py = p / TW, px = p - (p / TW) * TW;
+        pb[j] = py * g.sh * PW + px * g.sw;
+    }
+    const int ko = 8 * (lane >> 4);
+    gf32x4 acc[NF][MF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+        for (int j = 0; j < MF; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
+    const bool vec = (g.Cin & 7) == 0;
+    gbf16x8 b0h[NF], b0l[NF], b1h[NF], b1l[NF];  // B of this tap / the next (slots fixed by unrolling)
+    auto load_b = [&](int s, gbf16x8 (&h)[NF], gbf16x8 (&l)[NF]) {
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const uint16_t* wrow = wpk + ((size_t)s * cout_pad + ch0 + wn * NF * 16 + i * 16 + (lane & 15)) * 64 + ko;
+            h[i] = *reinterpret_cast<const gbf16x8*>(wrow);
+            l[i] = *reinterpret_cast<const gbf16x8*>(wrow + 32);
+        }
+    };
+    auto tap_step = [&](int tap, int cc, const gbf16x8 (&h)[NF], const gbf16x8 (&l)[NF], gbf16x8 (&nh)[NF],
+                        gbf16x8 (&nl)[NF]) {
+        if (tap + 1 < ntap) load_b((tap + 1) * ncc + cc, nh, nl);
+        const int ky = tap / g.kw, kx = tap - (tap / g.kw) * g.kw;
+        const int toff = ky * PW + kx;
+#pragma unroll
+        for (int j = 0; j < MF; ++j) {
+            const int xr = (pb[j] + toff) * GX_ROW + ko;
+            const gbf16x8 x_h = *reinterpret_cast<const gbf16x8*>(Ph + xr);
+            const gbf16x8 x_l = *reinterpret_cast<const gbf16x8*>(Pl + xr);
+#pragma unroll
+            for (int i = 0; i < NF; ++i) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h[i], x_h, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(l[i], x_h, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h[i], x_l, acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+    for (int cc = 0; cc < ncc; ++cc) {
+        load_b(cc, b0h, b0l);  // tap 0 of this chunk: in flight during the staging
+        if (cc > 0) __syncthreads();  // every wave is done with the previous chunk's patch
+        // ---- stage the chunk: item = (patch pixel, 8-channel quad) ----
+        for (int it = t; it < NP * 4; it += 256) {
+            const int pix = it >> 2, q = it & 3;
+            const int R = pix / PW, C = pix - (pix / PW) * PW;
+            const int iy = iy0 + R, ix = ix0 + C;
+            const bool inside = iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
+            const int c0 = cc * 32 + 8 * q;
+            const float* px = img + ((size_t)(inside ? iy : 0) * g.Win + (inside ? ix : 0)) * g.Cin;
+            float v[8];
+            if (inside && vec && c0 + 8 <= g.Cin) {
+                const float4 a = *reinterpret_cast<const float4*>(px + c0);
+                const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
+                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+                v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+                if (scl) {
+                    const float4 sa = *reinterpret_cast<const float4*>(scl + c0);
+                    const float4 sb = *reinterpret_cast<const float4*>(scl + c0 + 4);
+                    v[0] *= sa.x; v[1] *= sa.y; v[2] *= sa.z; v[3] *= sa.w;
+                    v[4] *= sb.x; v[5] *= sb.y; v[6] *= sb.z; v[7] *= sb.w;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const bool ok = inside && c0 + e < g.Cin;
+                    v[e] = ok ? (scl ? px[c0 + e] * scl[c0 + e] : px[c0 + e]) : 0.f;
+                }
+            }
+            gbf16x8 h, l;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                h[e] = (__bf16)v[e];
+                l[e] = (__bf16)(v[e] - (float)h[e]);
+            }
+            *reinterpret_cast<gbf16x8*>(Ph + pix * GX_ROW + 8 * q) = h;
+            *reinterpret_cast<gbf16x8*>(Pl + pix * GX_ROW + 8 * q) = l;
+        }
+        __syncthreads();
+        // ---- the chunk's taps, two per iteration (B slots alternate) ----
+        for (int tap = 0; tap < ntap; tap += 2) {
+            tap_step(tap, cc, b0h, b0l, b1h, b1l);
+            if (tap + 1 < ntap) tap_step(tap + 1, cc, b1h, b1l, b0h, b0l);
+        }
+    }
+    const int HWo = g.Hout * g.Wout;
+#pragma unroll
+    for (int j = 0; j < MF; ++j) {
+        const int p = wm * MF * 16 + j * 16 + (lane & 15);
+        const int oy = oy0 + p / TW, ox = ox0 + p - (p / TW) * TW;
+        if (oy >= g.Hout || ox >= g.Wout) continue;
+        const int Pj = oy * g.Wout + ox;
+        float* o = out + ((size_t)n * HWo + Pj) * g.Cout;
+        const float* rp = res ? res + ((size_t)n * HWo + Pj) * g.Cout : nullptr;
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int c = ch0 + wn * NF * 16 + i * 16 + 4 * (lane >> 4);
+            float y[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float z = acc[i][j][e] + (c + e < g.Cout ? bias[c + e] : 0.f);
+                if (rp && c + e < g.Cout) z += rp[c + e];
+                y[e] = gact(z, act, alpha);
+            }
+            if (c + 4 <= g.Cout && (g.Cout & 3) == 0) {
+                *reinterpret_cast<float4*>(o + c) = make_float4(y[0], y[1], y[2], y[3]);
+            } else {
+                for (int e = 0; e < 4 && c + e < g.Cout; ++e) o[c + e] = y[e];
+            }
+        }
+    }
+}
+
 // tile of a layer with C_out output channels: BN = 16, 32 or 64
 static inline int gconv_bn(int cout) { return cout <= 16 ? 16 : cout <= 32 ? 32 : 64; }
 
@@ -241,7 +389,7 @@ static __global__ __launch_bounds__(256) void gconv_f32(const float* __restrict_
 // group's weights staged once per block in LDS as [K][32] and read as
 // broadcast float4s.  Each output is the same chain as gconv_f32 (bias, then
 // fma over ky, kx, ci in order): the results are identical.
-constexpr int GF32_KMAX = 384;
+constexpr int GF32_KMAX = 96;  // 12 KiB of LDS: 8 waves per SIMD
 static __global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restrict__ in, const float* __restrict__ w,
                                                      const float* __restrict__ bias, float* __restrict__ out,
                                                      ConvGeom g, int act, float alpha) {

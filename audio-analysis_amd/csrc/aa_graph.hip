@@ -138,24 +138,25 @@ __global__ __launch_bounds__(64 * GP_STRIPES) void gdwconv_pool(
     if (s == 0 && c < C) pooled[(size_t)n * C + c] = gact(gpool_combine(part, lane, 1) / (float)HW, pact, palpha);
 }
 
+constexpr int GP4_STRIPES = 32;
 // The same two kernels 4 channels per lane (C % 4 == 0): thread t of a block
 // owns channel quad t % Q of the block's 4 Q channels and stripe t / Q
-// (GP_STRIPES stripes).  Per channel the stripes and their sums are exactly
-// the scalar kernels' (pixel order within a stripe, the same combine tree), so
-// results do not depend on Q or on which kernel ran: float4 loads give 16 lanes
-// 256 contiguous bytes per pixel, and a block of Q = 4 (64 threads) keeps a
-// small batch's grid wide enough to fill the chip.
+// (GP4_STRIPES stripes: twice the scalar kernels', for twice the waves on
+// the small maps of a network's last stages).  Per channel the sum order is
+// fixed (pixel order within a stripe, a fixed combine tree), the same in the
+// pool and in the fused dwconv + pool: float4 loads give 16 lanes 256
+// contiguous bytes per pixel.
 template <int Q>
-__global__ __launch_bounds__(Q * GP_STRIPES) void ggpool4(const float* __restrict__ in, float* __restrict__ out,
+__global__ __launch_bounds__(Q * GP4_STRIPES) void ggpool4(const float* __restrict__ in, float* __restrict__ out,
                                                          int HW, int C, int avg, int act, float alpha) {
-    __shared__ float part[GP_STRIPES][4 * Q];
+    __shared__ float part[GP4_STRIPES][4 * Q];
     const int cq = threadIdx.x % Q, s = threadIdx.x / Q;
     const int c = blockIdx.x * 4 * Q + 4 * cq;
     const int n = blockIdx.y;
     float4 m = avg ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
     if (c < C) {
         const float* p = in + (size_t)n * HW * C + c;
-        for (int i = s; i < HW; i += GP_STRIPES) {
+        for (int i = s; i < HW; i += GP4_STRIPES) {
             const float4 v = *reinterpret_cast<const float4*>(p + (size_t)i * C);
             if (avg) { m.x += v.x; m.y += v.y; m.z += v.z; m.w += v.w; }
             else { m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w); }
@@ -165,11 +166,11 @@ __global__ __launch_bounds__(Q * GP_STRIPES) void ggpool4(const float* __restric
     __syncthreads();
     const int k = threadIdx.x;  // one channel of the block per thread
     if (k < 4 * Q && blockIdx.x * 4 * Q + k < C) {
-        float v[GP_STRIPES];
+        float v[GP4_STRIPES];
 #pragma unroll
-        for (int i = 0; i < GP_STRIPES; ++i) v[i] = part[i][k];
+        for (int i = 0; i < GP4_STRIPES; ++i) v[i] = part[i][k];
 #pragma unroll
-        for (int w = GP_STRIPES / 2; w >= 1; w >>= 1)
+        for (int w = GP4_STRIPES / 2; w >= 1; w >>= 1)
 #pragma unroll
             for (int i = 0; i < w; ++i) v[i] = avg ? v[i] + v[i + w] : fmaxf(v[i], v[i + w]);
         float r = v[0];
@@ -181,11 +182,11 @@ __global__ __launch_bounds__(Q * GP_STRIPES) void ggpool4(const float* __restric
 // KS = 3: a 3x3 kernel, the taps unrolled and their weights held in
 // registers for every pixel; KS = 0: any kernel, weights re-read per tap
 template <int Q, int KS>
-__global__ __launch_bounds__(Q * GP_STRIPES) void gdwconv_pool4(
+__global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
     const float* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out,
     float* __restrict__ pooled, int Hin, int Win, int C, int Hout, int Wout, int kh, int kw, int sh, int sw, int pt,
     int pl, int act, float alpha, int pact, float palpha) {
-    __shared__ float part[GP_STRIPES][4 * Q];
+    __shared__ float part[GP4_STRIPES][4 * Q];
     const int cq = threadIdx.x % Q, s = threadIdx.x / Q;
     const int c = blockIdx.x * 4 * Q + 4 * cq;
     const int n = blockIdx.y;
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(Q * GP_STRIPES) void gdwconv_pool4(
             for (int t = 0; t < NW; ++t) wr[t] = *reinterpret_cast<const float4*>(w + t * C + c);
         }
         const int KH = KS ? KS : kh, KW = KS ? KS : kw;
-        for (int P = s; P < HW; P += GP_STRIPES) {
+        for (int P = s; P < HW; P += GP4_STRIPES) {
             const int oy = P / Wout, ox = P - (P / Wout) * Wout;
             float4 acc = b;
 #pragma unroll
@@ -233,11 +234,11 @@ __global__ __launch_bounds__(Q * GP_STRIPES) void gdwconv_pool4(
     __syncthreads();
     const int k = threadIdx.x;
     if (k < 4 * Q && blockIdx.x * 4 * Q + k < C) {
-        float v[GP_STRIPES];
+        float v[GP4_STRIPES];
 #pragma unroll
-        for (int i = 0; i < GP_STRIPES; ++i) v[i] = part[i][k];
+        for (int i = 0; i < GP4_STRIPES; ++i) v[i] = part[i][k];
 #pragma unroll
-        for (int ww = GP_STRIPES / 2; ww >= 1; ww >>= 1)
+        for (int ww = GP4_STRIPES / 2; ww >= 1; ww >>= 1)
 #pragma unroll
             for (int i = 0; i < ww; ++i) v[i] = v[i] + v[i + ww];
         pooled[(size_t)n * C + blockIdx.x * 4 * Q + k] = gact(v[0] / (float)HW, pact, palpha);
@@ -715,7 +716,39 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                 const float* scl = N.scale_src >= 0 ? buf(N.scale_src) : nullptr;
                 const float* res = N.res_src >= 0 ? buf(N.res_src) : nullptr;
                 const int HWo = g.Hout * g.Wout;
-                if (N.bn == 16)
+                // kernels larger than 1x1 with C_out <= 16: the patch-staged
+                // kernel when its patch fits 64 KiB (two blocks per CU at least).
+                // (Measured on the EfficientNetV2 graph: 3x3/32->16 212 -> 149
+                // us; at 64 channels per block it lost -- 3x3/32->128 161 ->
+                // 178, 3x3/2 16->64 97 -> 176 us -- its per-tap B loads from L2
+                // stall the short tap loop: gconv_x3t keeps those.)
+                int BM = 0, TW = 0;
+                static const bool nopatch = getenv("AA_GRAPH_NOPATCH") != nullptr;  // (A/B knob)
+                if (d.kh * d.kw > 1 && N.bn == 16 && !nopatch) {
+                    BM = 256;
+                    TW = BM == 64 ? 8 : 16;
+                    const int TH = BM / TW;
+                    const size_t lds = (size_t)((TH - 1) * d.sh + d.kh) * ((TW - 1) * d.sw + d.kw) * GX_ROW * 4;
+                    if (lds > 65536) BM = 0;
+                }
+                if (BM) {
+                    const int TH = BM / TW;
+                    const int tiles_w = (N.W + TW - 1) / TW, tiles_h = (N.H + TH - 1) / TH;
+                    const size_t lds = (size_t)((TH - 1) * d.sh + d.kh) * ((TW - 1) * d.sw + d.kw) * GX_ROW * 4;
+                    const dim3 grid((unsigned)(tiles_w * tiles_h), N.cout_pad / N.bn, n);
+                    if (N.bn == 16)
+                        hipLaunchKernelGGL((gconv_x3p<4, 1, 4, 1>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res);
+                    else if (N.bn == 32)
+                        hipLaunchKernelGGL((gconv_x3p<4, 1, 2, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res);
+                    else if (BM == 128)
+                        hipLaunchKernelGGL((gconv_x3p<2, 2, 4, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res);
+                    else
+                        hipLaunchKernelGGL((gconv_x3p<2, 2, 2, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res);
+                } else if (N.bn == 16)
                     hipLaunchKernelGGL((gconv_x3t<4, 1, 4, 1>), dim3((HWo + 255) / 256, N.cout_pad / 16, nz), dim3(256),
                                        0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
                                        res);
@@ -743,16 +776,12 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                 const GNode& P = G.nodes[N.pool_into];
                 float* pooled = ws + P.off * (size_t)n;
                 if ((Cin & 3) == 0) {
-                    const bool wide = (size_t)n * ((Cin + 63) / 64) >= 1024;  // enough 256-thread blocks
-                    const bool k9 = d.kh == 3 && d.kw == 3;
-#define AA_DWP(QQ, NT)                                                                                              \
-    hipLaunchKernelGGL((gdwconv_pool4<QQ, NT>), dim3((Cin + 4 * QQ - 1) / (4 * QQ), n), dim3(QQ * GP_STRIPES), 0, st, a, \
-                       (const float*)N.d_w, N.d_b, out, pooled, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw, d.pt,  \
+#define AA_DWP(KS)                                                                                             \
+    hipLaunchKernelGGL((gdwconv_pool4<16, KS>), dim3((Cin + 63) / 64, n), dim3(16 * GP4_STRIPES), 0, st, a,     \
+                       (const float*)N.d_w, N.d_b, out, pooled, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw, d.pt, \
                        d.pl, act, d.alpha, P.d.act, P.d.alpha)
-                    if (wide && k9) AA_DWP(16, 3);
-                    else if (wide) AA_DWP(16, 0);
-                    else if (k9) AA_DWP(4, 3);
-                    else AA_DWP(4, 0);
+                    if (d.kh == 3 && d.kw == 3) AA_DWP(3);
+                    else AA_DWP(0);
 #undef AA_DWP
                 } else {
                     hipLaunchKernelGGL(gdwconv_pool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a,
@@ -776,11 +805,8 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
             break;
         case AA_G_GMAXPOOL:
         case AA_G_GAVGPOOL:
-            if ((Cin & 3) == 0 && (size_t)n * ((Cin + 63) / 64) >= 1024)
-                hipLaunchKernelGGL((ggpool4<16>), dim3((Cin + 63) / 64, n), dim3(16 * GP_STRIPES), 0, st, a, out,
-                                   Hin * Win, Cin, d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
-            else if ((Cin & 3) == 0)
-                hipLaunchKernelGGL((ggpool4<4>), dim3((Cin + 15) / 16, n), dim3(4 * GP_STRIPES), 0, st, a, out,
+            if ((Cin & 3) == 0)
+                hipLaunchKernelGGL((ggpool4<16>), dim3((Cin + 63) / 64, n), dim3(16 * GP4_STRIPES), 0, st, a, out,
                                    Hin * Win, Cin, d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
             else
                 hipLaunchKernelGGL(ggpool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a, out, Hin * Win,

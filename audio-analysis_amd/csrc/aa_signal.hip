@@ -72,6 +72,7 @@ struct SnPlan {
     double2* d_tab = nullptr;  // sn_stft64's tables (kS64Tab*)
     StageTimer timer;          // HIP events around the launches of the stages in timer.mask
     bool select_reg = false;   // row medians by sn_select_reg (AA_SN_SELECT=reg; A/B knob) or sn_select
+    bool stft_r8 = false;      // the transform by sn_stft64r8 (AA_SN_STFT=r8; A/B knob) or sn_stft64
     int diag = 0;              // AA_SN_DIAG: ablation bits of sn_select_reg (tools only; results then invalid)
 };
 
@@ -446,6 +447,136 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
             wmax = max(wmax, __float_as_uint(m));
         }
         __syncthreads();  // the buffer is rewritten by the next frame
+    }
+    if (gmax) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (unsigned)__shfl_xor((int)wmax, o, 64));
+        if ((t & 63) == 0 && wmax) atomicMax(gmax, wmax);
+    }
+}
+
+// sn_stft64r8: the same transform on 256 threads per frame, 2048 = 8 x 8 x 8 x
+// 4, every stage on all threads (8 points each), so a thread holds half the
+// registers of sn_stft64 and a CU keeps 4 frames of 4 waves in flight (LDS
+// 36,864 B per block) instead of 4 frames of 2 waves.  n = 256 a + m, m = 32 b
+// + r, r = 4 c + d; k = k1 + 8 k2 + 64 k3 + 512 k4:
+//   1. thread m: DFT-8 over a, twiddle W2048^(m k1)            -> [k1][m]
+//   2. thread (r, k1): DFT-8 over b, twiddle W256^(r k2)       -> [k2][k1][r]
+//   3. thread (d, k1, k2): DFT-8 over c, twiddle W32^(d k3)    -> [d][k1 + 8 k2 + 64 k3]
+//   4. thread q, q + 256 (q = k1 + 8 k2 + 64 k3): DFT-4 over d -> Z[q + 512 k4]
+//   then thread t splits bins k = t + 256 i and 2048 - k (i < 4; thread 0 also
+//   bin 1024), writing the magnitudes straight to the S row (both runs
+//   coalesced).  Exchange layouts padded so every ds_read/write_b128 wave
+//   group touches 16 distinct 16-B bank groups: [k2][k1][r] with strides 288 /
+//   36 (36 = 4 mod 16: stage 3's lanes (d, k1 < 4) land on 4 k1 + d), [d][q]
+//   with stride 516.
+constexpr int kR8T = 256;
+constexpr int kR8K1 = 36, kR8K2 = 288, kR8D = 516, kR8Buf = 8 * kR8K2;
+// SnPlan::d_tab after sn_stft64's tables: tw1 [7][256] W2048^(m k1) | tw2 [7][32]
+// W256^(r k2) | tw3 [7][4] W32^(d k3) | split bases [256] W4096^t
+constexpr int kR8Tw1 = kS64TabN, kR8Tw2 = kR8Tw1 + 7 * 256, kR8Tw3 = kR8Tw2 + 7 * 32, kR8TwS = kR8Tw3 + 7 * 4,
+              kR8TabN = kR8TwS + 256;
+static_assert(7 * kR8K2 + 7 * kR8K1 + 32 <= kR8Buf && 3 * kR8D + 512 <= kR8Buf, "sn_stft64r8 LDS");
+
+__global__ __launch_bounds__(kR8T) __attribute__((amdgpu_waves_per_eu(4, 4))) void sn_stft64r8(
+    const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const double2* __restrict__ win2,
+    const double2* __restrict__ tw1, const double2* __restrict__ tw2, const double2* __restrict__ tw3,
+    const double2* __restrict__ twS, float* __restrict__ S, int ld, unsigned* __restrict__ gmax) {
+    __shared__ double2 buf[kR8Buf];
+    const int t = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)pcm, 0, n_samples * 4, 0x00020000);
+    const double2 tb = twS[t];
+    const int r2 = t & 31, k1b = t >> 5;                         // stage 2
+    const int d3 = t & 3, k1c = (t >> 2) & 7, k2c = t >> 5;      // stage 3
+    unsigned wmax = 0;
+    const int nbx = gridDim.x >> 3;
+    const int xcd = blockIdx.x & 7;
+    const int f_end = (int)((long long)(xcd + 1) * n_frames / 8);
+#pragma unroll 1
+    for (int fi = (int)((long long)xcd * n_frames / 8) + (blockIdx.x >> 3); fi < f_end; fi += nbx) {
+        // opaque table indices: the loop-invariant twiddle loads stay per frame
+        int iw = t, i1 = t, i2 = r2, i3 = d3;
+        __asm__ volatile("" : "+v"(iw), "+v"(i1), "+v"(i2), "+v"(i3));
+        double2 v[8];
+        {
+            const int off = fi * hop - 2048 + 2 * t;
+            int offo = off + 1;  // (a merged dwordx2 would be range-checked as a unit)
+            __asm__ volatile("" : "+v"(offo));
+#pragma unroll
+            for (int a = 0; a < 8; ++a) {
+                const float xe = load_view(rs, off + 512 * a), xo = load_view(rs, offo + 512 * a);
+                const double2 w = win2[256 * a + iw];
+                v[a] = make_double2((double)xe * w.x, (double)xo * w.y);
+            }
+        }
+        // ---- 1 ----
+        ddft8(v);
+#pragma unroll
+        for (int k = 1; k < 8; ++k) v[k] = dmul(v[k], tw1[(k - 1) * 256 + i1]);
+        __syncthreads();  // the previous frame's split has read the buffer
+#pragma unroll
+        for (int k = 0; k < 8; ++k) buf[k * 256 + t] = v[k];
+        __syncthreads();
+        // ---- 2 ----
+#pragma unroll
+        for (int b = 0; b < 8; ++b) v[b] = buf[k1b * 256 + 32 * b + r2];
+        ddft8(v);
+#pragma unroll
+        for (int k = 1; k < 8; ++k) v[k] = dmul(v[k], tw2[(k - 1) * 32 + i2]);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) buf[k * kR8K2 + k1b * kR8K1 + r2] = v[k];
+        __syncthreads();
+        // ---- 3 ----
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = buf[k2c * kR8K2 + k1c * kR8K1 + 4 * c + d3];
+        ddft8(v);
+#pragma unroll
+        for (int k = 1; k < 8; ++k) v[k] = dmul(v[k], tw3[(k - 1) * 4 + i3]);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) buf[d3 * kR8D + k1c + 8 * k2c + 64 * k] = v[k];
+        __syncthreads();
+        // ---- 4 ----
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) v[4 * h + d] = buf[d * kR8D + t + 256 * h];
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            ddft4(v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) buf[t + 256 * h + 512 * k] = v[4 * h + k];
+        }
+        __syncthreads();
+        // ---- real split (the window carries its 1/2): a = Z[k], b = Z[2048 - k],
+        // X[k] = E + W4096^k O, X[2048 - k] = conj(E - W4096^k O); k = 0 gives the
+        // DC and Nyquist bins (a = b = Z[0], W = 1) ----
+        float* srow = S + (size_t)fi * ld;
+        auto split = [&](int ka, double2 w) {
+            const double2 a = buf[ka], b = buf[(2048 - ka) & 2047];
+            const double2 E = make_double2(a.x + b.x, a.y - b.y);
+            const double2 O = make_double2(a.y + b.y, b.x - a.x);
+            const double2 q = dmul(w, O);
+            const float m1 = np_cabsf(E.x + q.x, E.y + q.y), m2 = np_cabsf(E.x - q.x, q.y - E.y);
+            srow[ka] = m1;
+            srow[2048 - ka] = m2;
+            // (bit patterns of non-negative floats order like the values; NaN / inf on top)
+            wmax = max(wmax, max(__float_as_uint(m1), __float_as_uint(m2)));
+        };
+        split(t, tb);
+        split(t + 256, w16<1>(tb));
+        split(t + 512, w16<2>(tb));
+        split(t + 768, w16<3>(tb));
+        if (t == 0) {  // bin 1024 pairs with itself: W4096^1024 = -i
+            const double2 a = buf[1024];
+            const double2 E = make_double2(a.x + a.x, 0.0);
+            const double2 q = dnegi(make_double2(a.y + a.y, 0.0));
+            const float m = np_cabsf(E.x + q.x, E.y + q.y);
+            srow[1024] = m;
+            wmax = max(wmax, __float_as_uint(m));
+        }
     }
     if (gmax) {
 #pragma unroll
@@ -1361,8 +1492,12 @@ static int sn_launch_stft(SnPlan& p, const float* pcm, int64_t n, int F, float* 
     hipEvent_t e0;
     int rc = p.timer.begin(SN_STAGE_STFT, st, &e0);
     if (rc != AA_OK) return rc;
-    hipLaunchKernelGGL(sn_stft64, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
-                       tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax);
+    if (p.stft_r8)
+        hipLaunchKernelGGL(sn_stft64r8, dim3(grid), dim3(kR8T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
+                           tab + kR8Tw1, tab + kR8Tw2, tab + kR8Tw3, tab + kR8TwS, S, ld, gmax);
+    else
+        hipLaunchKernelGGL(sn_stft64, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
+                           tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax);
     AA_LAUNCH_CHECK();
     return p.timer.end(SN_STAGE_STFT, st, e0);
 }
@@ -1474,12 +1609,13 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
     }
     if (const char* e = std::getenv("AA_SN_SELECT")) p->select_reg = std::strcmp(e, "reg") == 0;
     if (const char* e = std::getenv("AA_SN_DIAG")) p->diag = std::atoi(e);
+    if (const char* e = std::getenv("AA_SN_STFT")) p->stft_r8 = std::strcmp(e, "r8") == 0;
     // sn_stft64's tables, rounded from long double
     auto wexp = [](long long e, long long m) {  // exp(-2 pi i e / m)
         const long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)(e % m) / (long double)m;
         return make_double2((double)cosl(a), (double)sinl(a));
     };
-    std::vector<double2> tab(kS64TabN);
+    std::vector<double2> tab(kR8TabN);
     {  // scipy.signal.get_window('hann', 4096, fftbins=True) (librosa 0.11's window, :654): general_cosine
        // over np.linspace(-pi, pi, 4097)[:4096], w = 0.5 + 0.5 cos(fac) in float64
         const double start = -M_PI, step = (M_PI - start) / 4096.0;
@@ -1496,6 +1632,12 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
     for (int n3 = 1; n3 < 8; ++n3)
         for (int t = 0; t < kS64T; ++t) tab[kS64TabTw3 + (n3 - 1) * kS64T + t] = wexp((long long)n3 * t, 2048);
     for (int t = 0; t < kS64T; ++t) tab[kS64TabTwS + t] = wexp(t ? t : 128, 4096);
+    for (int k = 1; k < 8; ++k) {  // sn_stft64r8
+        for (int m = 0; m < 256; ++m) tab[kR8Tw1 + (k - 1) * 256 + m] = wexp((long long)m * k, 2048);
+        for (int r = 0; r < 32; ++r) tab[kR8Tw2 + (k - 1) * 32 + r] = wexp((long long)r * k, 256);
+        for (int d = 0; d < 4; ++d) tab[kR8Tw3 + (k - 1) * 4 + d] = wexp((long long)d * k, 32);
+    }
+    for (int t = 0; t < 256; ++t) tab[kR8TwS + t] = wexp(t, 4096);
     hipError_t e = hipMalloc((void**)&p->d_tab, sizeof(double2) * tab.size());
     if (e == hipSuccess) e = hipMemcpy(p->d_tab, tab.data(), sizeof(double2) * tab.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {

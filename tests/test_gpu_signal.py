@@ -86,6 +86,27 @@ def test_spectrogram_bit_exact(gpu, n, seed):
     _assert_s_equal(got, want)
 
 
+@pytest.mark.parametrize("variant", ["r8", "base"])
+@pytest.mark.parametrize("n,seed", [(60 * SR, 35), (7 * SR + 999, 36), (5000, 37)])
+def test_spectrogram_variants_bit_exact(gpu, monkeypatch, variant, n, seed):
+    """Both STFT kernels (sn_stft64: 128 threads, 16 x 16 x 8; sn_stft64r8: 256
+    threads, 8 x 8 x 8 x 4; AA_SN_STFT picks one at plan creation) give the
+    reference's magnitudes, and the detector built on either gives its mask."""
+    monkeypatch.setenv("AA_SN_STFT", variant)
+    x = _clip(n / SR, seed)
+    det = _det(gpu)
+    got = det.spectrogram(torch.from_numpy(x).to(gpu)).cpu().numpy()
+    from oracle.fe_oracle import stft_mag
+    _assert_s_equal(got, stft_mag(x, 4096, HOP))
+    if n == 60 * SR:
+        F = det.n_frames(len(x))
+        mask_dev = torch.empty((2049, det.words(F)), dtype=torch.int64, device=gpu)
+        stats = det.components(torch.from_numpy(x).to(gpu), mask_out=mask_dev)
+        _, ref_mask, ref_stats = so.signal_noise(x, SR, HOP)
+        assert int((_unpack(mask_dev.cpu().numpy(), F) != ref_mask).sum()) == 0
+        assert stats.tolist() == ref_stats.tolist()
+
+
 def _assert_s_equal(got, want):
     d = got.view(np.uint32) != want.view(np.uint32)
     ulps = np.abs(got.view(np.int32)[d].astype(np.int64) - want.view(np.int32)[d].astype(np.int64))

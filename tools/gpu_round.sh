@@ -11,6 +11,9 @@
 #                                             1), its kernel-trace summary
 #   bash tools/gpu_round.sh sn                signal_noise: GPU parity tests, per-clip
 #                                             time and its kernel-trace summary
+#   bash tools/gpu_round.sh graph             graph executor: GPU parity tests, the
+#                                             EfficientNetV2-shaped bench line and the
+#                                             kernel-trace summary of its serial step
 #   bash tools/gpu_round.sh ab NAME [rounds]  CNN parity tests, then alternating bench
 #                                             runs of the in-tree library against
 #                                             tools/ab/libaa_NAME.so (tools/ab.sh)
@@ -72,6 +75,13 @@ sn)
   cat gpurun_out/sn_bench.txt
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/snprof -o run -- python3 tools/sn_bench.py > gpurun_out/snp.log 2>&1 || exit 3
   python tools/prof_summary.py gpurun_out/snprof > gpurun_out/sn_kernel_stats.txt && cat gpurun_out/sn_kernel_stats.txt
+  ;;
+graph)
+  timeout -k 10 400 $PT tests/test_gpu_graph.py > gpurun_out/graph_tests.log 2>&1 || { tail -30 gpurun_out/graph_tests.log; exit 1; }
+  tail -1 gpurun_out/graph_tests.log
+  timeout -k 10 300 python bench.py --model effnetv2 --steps 20 --warmup 5 --cpu-seconds 0 --secondary=serial > gpurun_out/graph_bench.json 2> gpurun_out/graph_bench.err || { tail -20 gpurun_out/graph_bench.err; exit 2; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/graphprof -o run -- python3 bench.py --model effnetv2 --steps 20 --warmup 5 --cpu-seconds 0 --secondary= --pipeline 0 --no-parity > gpurun_out/graphp.log 2>&1 || exit 3
+  python tools/prof_summary.py gpurun_out/graphprof > gpurun_out/graph_kernel_stats_serial.txt && head -30 gpurun_out/graph_kernel_stats_serial.txt
   ;;
 ab)
   NAME=$1
