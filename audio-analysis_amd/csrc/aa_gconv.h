@@ -59,15 +59,24 @@ constexpr int GX_ROW = 48;  // bf16 per LDS row: 32 + 16 B of padding (96 B)
 // conv without activation; the add's own activation is `act`).  The next K
 // step's pixels and weights are loaded into registers before this step's
 // MFMAs, so their latency hides behind the matrix work.
-template <int WM, int WN, int MF, int NF>
+//
+// KC: 32-channel chunks per K step (1, 2, 3 or 4; the layer's chunk count a
+// multiple of it): KC x the MFMAs per barrier pair and per L2 round trip --
+// a 1x1 conv over 1152 channels on a small map is otherwise 36 dependent
+// steps of 12 MFMAs.  scale_hw > 0: the pixels of n windows run flattened as
+// one image (pointwise convs) and pixel P's squeeze-and-excite scale is that
+// of window P / scale_hw.
+template <int WM, int WN, int MF, int NF, int KC = 1>
 __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
                                                  const float* __restrict__ bias, float* __restrict__ out,
                                                  ConvGeom g, int cout_pad, int act, float alpha,
-                                                 const float* __restrict__ in_scale, const float* __restrict__ res) {
+                                                 const float* __restrict__ in_scale, const float* __restrict__ res,
+                                                 int scale_hw = 0) {
     static_assert(WM * WN == 4, "four waves");
     constexpr int BM = WM * MF * 16, BN = WN * NF * 16, AI = BM / 64;
-    __shared__ __attribute__((aligned(16))) uint16_t Ah[BM * GX_ROW], Al[BM * GX_ROW];
-    __shared__ __attribute__((aligned(16))) uint16_t Bh[BN * GX_ROW], Bl[BN * GX_ROW];
+    constexpr int ROW = KC * 32 + 16;  // bf16 per LDS row (+32 B: conflict-free ds_read_b128 runs)
+    __shared__ __attribute__((aligned(16))) uint16_t Ah[BM * ROW], Al[BM * ROW];
+    __shared__ __attribute__((aligned(16))) uint16_t Bh[BN * ROW], Bl[BN * ROW];
     const int n = blockIdx.z;
     const int pix0 = blockIdx.x * BM, ch0 = blockIdx.y * BN;
     const int HWo = g.Hout * g.Wout;
@@ -77,98 +86,121 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
     const int r = t >> 2, q = t & 3;
     int oy[AI], ox[AI];
     bool pv[AI];
+    const float* sclp[AI];
 #pragma unroll
     for (int it = 0; it < AI; ++it) {
         const int P = pix0 + r + 64 * it;
         pv[it] = P < HWo;
         oy[it] = pv[it] ? P / g.Wout : 0;
         ox[it] = pv[it] ? P - (P / g.Wout) * g.Wout : 0;
+        sclp[it] = !in_scale ? nullptr
+                   : scale_hw > 0 ? in_scale + (size_t)((pv[it] ? P : 0) / scale_hw) * g.Cin
+                                  : in_scale + (size_t)n * g.Cin;
     }
     const bool bload = r < BN;
     const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
-    const float* scl = in_scale ? in_scale + (size_t)n * g.Cin : nullptr;
     const int ncc = g.cin_pad / 32;
-    const int nsteps = g.kh * g.kw * ncc;
+    const int ngs = ncc / KC;  // K steps per tap
+    const int nsteps = g.kh * g.kw * ngs;
     gf32x4 acc[NF][MF];
 #pragma unroll
     for (int i = 0; i < NF; ++i)
 #pragma unroll
         for (int j = 0; j < MF; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
     const bool vec = (g.Cin & 7) == 0;
-    float v[AI][8];
-    uint4 wh = {0, 0, 0, 0}, wl = {0, 0, 0, 0};
-    // step s = (tap, 32-channel chunk cc): this thread's 8 channels of AI
-    // pixels and its 8 hi + 8 lo weights
+    float v[AI][KC][8];
+    uint4 wh[KC], wl[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) wh[k] = wl[k] = make_uint4(0, 0, 0, 0);
+    // step s = (tap, chunks KC gs .. KC gs + KC - 1): this thread's 8 channels
+    // of AI pixels per chunk and its 8 hi + 8 lo weights per chunk
     auto load = [&](int s) {
-        const int tap = s / ncc, cc = s - (s / ncc) * ncc;
+        const int tap = s / ngs, gs = s - (s / ngs) * ngs;
         const int ky = tap / g.kw, kx = tap - (tap / g.kw) * g.kw;
-        const int c0 = cc * 32 + 8 * q;
 #pragma unroll
         for (int it = 0; it < AI; ++it) {
             const int iy = oy[it] * g.sh - g.pt + ky, ix = ox[it] * g.sw - g.pl + kx;
             const bool inside = pv[it] && iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
             const float* px = img + ((size_t)(inside ? iy : 0) * g.Win + (inside ? ix : 0)) * g.Cin;
-            if (inside && vec && c0 + 8 <= g.Cin) {
-                const float4 a = *reinterpret_cast<const float4*>(px + c0);
-                const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
-                v[it][0] = a.x; v[it][1] = a.y; v[it][2] = a.z; v[it][3] = a.w;
-                v[it][4] = b.x; v[it][5] = b.y; v[it][6] = b.z; v[it][7] = b.w;
-                if (scl) {
-                    const float4 sa = *reinterpret_cast<const float4*>(scl + c0);
-                    const float4 sb = *reinterpret_cast<const float4*>(scl + c0 + 4);
-                    v[it][0] *= sa.x; v[it][1] *= sa.y; v[it][2] *= sa.z; v[it][3] *= sa.w;
-                    v[it][4] *= sb.x; v[it][5] *= sb.y; v[it][6] *= sb.z; v[it][7] *= sb.w;
-                }
-            } else {
+            const float* scl = sclp[it];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const bool ok = inside && c0 + e < g.Cin;
-                    v[it][e] = ok ? (scl ? px[c0 + e] * scl[c0 + e] : px[c0 + e]) : 0.f;
+            for (int k = 0; k < KC; ++k) {
+                const int c0 = (gs * KC + k) * 32 + 8 * q;
+                if (inside && vec && c0 + 8 <= g.Cin) {
+                    const float4 a = *reinterpret_cast<const float4*>(px + c0);
+                    const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
+                    v[it][k][0] = a.x; v[it][k][1] = a.y; v[it][k][2] = a.z; v[it][k][3] = a.w;
+                    v[it][k][4] = b.x; v[it][k][5] = b.y; v[it][k][6] = b.z; v[it][k][7] = b.w;
+                    if (scl) {
+                        const float4 sa = *reinterpret_cast<const float4*>(scl + c0);
+                        const float4 sb = *reinterpret_cast<const float4*>(scl + c0 + 4);
+                        v[it][k][0] *= sa.x; v[it][k][1] *= sa.y; v[it][k][2] *= sa.z; v[it][k][3] *= sa.w;
+                        v[it][k][4] *= sb.x; v[it][k][5] *= sb.y; v[it][k][6] *= sb.z; v[it][k][7] *= sb.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const bool ok = inside && c0 + e < g.Cin;
+                        v[it][k][e] = ok ? (scl ? px[c0 + e] * scl[c0 + e] : px[c0 + e]) : 0.f;
+                    }
                 }
             }
         }
         if (bload) {
-            const uint16_t* wrow = wpk + (((size_t)s * cout_pad) + ch0 + r) * 64;
-            wh = *reinterpret_cast<const uint4*>(wrow + 8 * q);
-            wl = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                const uint16_t* wrow = wpk + (((size_t)(tap * ncc + gs * KC + k) * cout_pad) + ch0 + r) * 64;
+                wh[k] = *reinterpret_cast<const uint4*>(wrow + 8 * q);
+                wl[k] = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
+            }
         }
     };
     load(0);
     for (int s = 0; s < nsteps; ++s) {
-        gbf16x8 h[AI], l[AI];
+        gbf16x8 h[AI][KC], l[AI][KC];
 #pragma unroll
         for (int it = 0; it < AI; ++it)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                h[it][e] = (__bf16)v[it][e];
-                l[it][e] = (__bf16)(v[it][e] - (float)h[it][e]);
-            }
+            for (int k = 0; k < KC; ++k)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    h[it][k][e] = (__bf16)v[it][k][e];
+                    l[it][k][e] = (__bf16)(v[it][k][e] - (float)h[it][k][e]);
+                }
         __syncthreads();  // the previous step's fragments are read
 #pragma unroll
-        for (int it = 0; it < AI; ++it) {
-            *reinterpret_cast<gbf16x8*>(Ah + (r + 64 * it) * GX_ROW + 8 * q) = h[it];
-            *reinterpret_cast<gbf16x8*>(Al + (r + 64 * it) * GX_ROW + 8 * q) = l[it];
-        }
+        for (int it = 0; it < AI; ++it)
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                *reinterpret_cast<gbf16x8*>(Ah + (r + 64 * it) * ROW + 32 * k + 8 * q) = h[it][k];
+                *reinterpret_cast<gbf16x8*>(Al + (r + 64 * it) * ROW + 32 * k + 8 * q) = l[it][k];
+            }
         if (bload) {
-            *reinterpret_cast<uint4*>(Bh + r * GX_ROW + 8 * q) = wh;
-            *reinterpret_cast<uint4*>(Bl + r * GX_ROW + 8 * q) = wl;
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                *reinterpret_cast<uint4*>(Bh + r * ROW + 32 * k + 8 * q) = wh[k];
+                *reinterpret_cast<uint4*>(Bl + r * ROW + 32 * k + 8 * q) = wl[k];
+            }
         }
         __syncthreads();
         if (s + 1 < nsteps) load(s + 1);
-        const int ko = 8 * (lane >> 4);
 #pragma unroll
-        for (int i = 0; i < NF; ++i) {
-            const int wr = (wn * NF * 16 + i * 16 + (lane & 15)) * GX_ROW + ko;
-            const gbf16x8 w_h = *reinterpret_cast<const gbf16x8*>(Bh + wr);
-            const gbf16x8 w_l = *reinterpret_cast<const gbf16x8*>(Bl + wr);
+        for (int k = 0; k < KC; ++k) {
+            const int ko = 32 * k + 8 * (lane >> 4);
 #pragma unroll
-            for (int j = 0; j < MF; ++j) {
-                const int xr = (wm * MF * 16 + j * 16 + (lane & 15)) * GX_ROW + ko;
-                const gbf16x8 x_h = *reinterpret_cast<const gbf16x8*>(Ah + xr);
-                const gbf16x8 x_l = *reinterpret_cast<const gbf16x8*>(Al + xr);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_h, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_l, x_h, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_l, acc[i][j], 0, 0, 0);
+            for (int i = 0; i < NF; ++i) {
+                const int wr = (wn * NF * 16 + i * 16 + (lane & 15)) * ROW + ko;
+                const gbf16x8 w_h = *reinterpret_cast<const gbf16x8*>(Bh + wr);
+                const gbf16x8 w_l = *reinterpret_cast<const gbf16x8*>(Bl + wr);
+#pragma unroll
+                for (int j = 0; j < MF; ++j) {
+                    const int xr = (wm * MF * 16 + j * 16 + (lane & 15)) * ROW + ko;
+                    const gbf16x8 x_h = *reinterpret_cast<const gbf16x8*>(Ah + xr);
+                    const gbf16x8 x_l = *reinterpret_cast<const gbf16x8*>(Al + xr);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_h, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_l, x_h, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h, x_l, acc[i][j], 0, 0, 0);
+                }
             }
         }
     }
@@ -197,6 +229,9 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
         }
     }
 }
+
+// tile of a layer with C_out output channels: BN = 16, 32 or 64
+static inline int gconv_bn(int cout) { return cout <= 16 ? 16 : cout <= 32 ? 32 : 64; }
 
 // gconv_x3p: the same split-bf16 conv for kernels larger than 1x1, with the
 // input patch of a TH x TW output tile staged once per 32-channel chunk (hi /
@@ -346,8 +381,6 @@ __global__ __launch_bounds__(256) void gconv_x3p(const float* __restrict__ in, c
     }
 }
 
-// tile of a layer with C_out output channels: BN = 16, 32 or 64
-static inline int gconv_bn(int cout) { return cout <= 16 ? 16 : cout <= 32 ? 32 : 64; }
 
 // exact f32: one thread per (output pixel, 8 output channels); weights [Cout][kh][kw][Cin]
 static __global__ __launch_bounds__(256) void gconv_f32(const float* __restrict__ in, const float* __restrict__ w,
@@ -385,11 +418,13 @@ static __global__ __launch_bounds__(256) void gconv_f32(const float* __restrict_
 }
 
 // exact f32 for small K = kh kw Cin (<= GF32_KMAX, e.g. a 3-channel stem):
-// one thread per output pixel and 32 output channels (blockIdx.y), the
-// group's weights staged once per block in LDS as [K][32] and read as
-// broadcast float4s.  Each output is the same chain as gconv_f32 (bias, then
-// fma over ky, kx, ci in order): the results are identical.
-constexpr int GF32_KMAX = 96;  // 12 KiB of LDS: 8 waves per SIMD
+// a block = 32 output pixels x 32 output channels (blockIdx.y), thread =
+// (pixel, 4-channel quad), so a wave stores 8 pixels' 128 contiguous bytes
+// each (1 KiB runs) and the 8 lanes of a pixel share its input loads; the
+// group's weights staged once per block in LDS as [K][32].  Each output is the
+// same chain as gconv_f32 (bias, then fma over ky, kx, ci in order): the
+// results are identical.
+constexpr int GF32_KMAX = 96;  // 12 KiB of LDS
 static __global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restrict__ in, const float* __restrict__ w,
                                                      const float* __restrict__ bias, float* __restrict__ out,
                                                      ConvGeom g, int act, float alpha) {
@@ -402,13 +437,17 @@ static __global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restr
         sw[i] = c0 + c < g.Cout ? w[(size_t)(c0 + c) * K + k] : 0.f;
     }
     __syncthreads();
-    const int P = blockIdx.x * 256 + threadIdx.x;
+    const int q = threadIdx.x & 7;
+    const int P = blockIdx.x * 32 + (threadIdx.x >> 3);
     if (P >= g.Hout * g.Wout) return;
     const int oy = P / g.Wout, ox = P - (P / g.Wout) * g.Wout;
     const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
-    float acc[32];
-#pragma unroll
-    for (int c = 0; c < 32; ++c) acc[c] = c0 + c < g.Cout ? bias[c0 + c] : 0.f;
+    const int cq = c0 + 4 * q;
+    float4 acc;
+    acc.x = cq < g.Cout ? bias[cq] : 0.f;
+    acc.y = cq + 1 < g.Cout ? bias[cq + 1] : 0.f;
+    acc.z = cq + 2 < g.Cout ? bias[cq + 2] : 0.f;
+    acc.w = cq + 3 < g.Cout ? bias[cq + 3] : 0.f;
     for (int ky = 0; ky < g.kh; ++ky) {
         const int iy = oy * g.sh - g.pt + ky;
         if (iy < 0 || iy >= g.Hin) continue;
@@ -416,31 +455,27 @@ static __global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restr
             const int ix = ox * g.sw - g.pl + kx;
             if (ix < 0 || ix >= g.Win) continue;
             const float* px = img + ((size_t)iy * g.Win + ix) * g.Cin;
-            const float4* wk = reinterpret_cast<const float4*>(sw + (size_t)(ky * g.kw + kx) * g.Cin * 32);
+            const float4* wk = reinterpret_cast<const float4*>(sw + (size_t)(ky * g.kw + kx) * g.Cin * 32) + q;
             for (int ci = 0; ci < g.Cin; ++ci) {
                 const float x = px[ci];
-#pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    const float4 wv = wk[ci * 8 + c];
-                    acc[4 * c + 0] = fmaf(wv.x, x, acc[4 * c + 0]);
-                    acc[4 * c + 1] = fmaf(wv.y, x, acc[4 * c + 1]);
-                    acc[4 * c + 2] = fmaf(wv.z, x, acc[4 * c + 2]);
-                    acc[4 * c + 3] = fmaf(wv.w, x, acc[4 * c + 3]);
-                }
+                const float4 wv = wk[ci * 8];
+                acc.x = fmaf(wv.x, x, acc.x);
+                acc.y = fmaf(wv.y, x, acc.y);
+                acc.z = fmaf(wv.z, x, acc.z);
+                acc.w = fmaf(wv.w, x, acc.w);
             }
         }
     }
     float* o = out + ((size_t)n * g.Hout * g.Wout + P) * g.Cout;
-    if ((g.Cout & 3) == 0 && c0 + 32 <= g.Cout) {
-#pragma unroll
-        for (int c = 0; c < 32; c += 4)
-            *reinterpret_cast<float4*>(o + c0 + c) = make_float4(gact(acc[c], act, alpha), gact(acc[c + 1], act, alpha),
-                                                                 gact(acc[c + 2], act, alpha),
-                                                                 gact(acc[c + 3], act, alpha));
+    const float4 y = make_float4(gact(acc.x, act, alpha), gact(acc.y, act, alpha), gact(acc.z, act, alpha),
+                                 gact(acc.w, act, alpha));
+    if ((g.Cout & 3) == 0 && cq + 4 <= g.Cout) {
+        *reinterpret_cast<float4*>(o + cq) = y;
     } else {
-#pragma unroll
-        for (int c = 0; c < 32; ++c)
-            if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], act, alpha);
+        if (cq < g.Cout) o[cq] = y.x;
+        if (cq + 1 < g.Cout) o[cq + 1] = y.y;
+        if (cq + 2 < g.Cout) o[cq + 2] = y.z;
+        if (cq + 3 < g.Cout) o[cq + 3] = y.w;
     }
 }
 

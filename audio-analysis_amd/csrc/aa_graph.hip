@@ -687,6 +687,26 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
     return AA_OK;
 }
 
+// 128 x 64 tiles (A/B knob AA_GRAPH_WIDE: "k" for kernels larger than 1x1,
+// "all" for every MFMA conv with 64-channel blocks)
+static bool wide_tile(bool spatial) {
+    static const int mode = [] {
+        const char* e = getenv("AA_GRAPH_WIDE");
+        return !e ? 0 : std::strcmp(e, "k") == 0 ? 1 : std::strcmp(e, "all") == 0 ? 2 : 0;
+    }();
+    return mode == 2 || (mode == 1 && spatial);
+}
+
+// largest KC of the 64 x 64 tiles (A/B knob AA_GRAPH_KC, default 2: KC = 4
+// halves the blocks per CU)
+static int kc_max() {
+    static const int k = [] {
+        const char* e = getenv("AA_GRAPH_KC");
+        return e ? std::max(1, std::min(4, std::atoi(e))) : 2;
+    }();
+    return k;
+}
+
 static int graph_run_node(const Graph& G, const GNode& N, const float* x, float* ws, int n, hipStream_t st) {
     const aa_node& d = N.d;
     auto buf = [&](int k) -> const float* {
@@ -705,13 +725,15 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
         case AA_G_CONV:
             if (N.mfma) {
                 ConvGeom g = N.g;
-                int nz = n;
-                if (d.kh == 1 && d.kw == 1 && d.sh == 1 && d.sw == 1 && d.pt == 0 && d.pl == 0 && N.scale_src < 0) {
+                int nz = n, scale_hw = 0;
+                if (d.kh == 1 && d.kw == 1 && d.sh == 1 && d.sw == 1 && d.pt == 0 && d.pl == 0) {
                     // pointwise: the n windows' pixels are one [1][n H W] image
-                    // (NHWC is [n][H][W][C] either way), so small maps fill whole tiles
+                    // (NHWC is [n][H][W][C] either way), so small maps fill whole
+                    // tiles; a squeeze-and-excite scale is looked up per pixel's window
                     g.Hin = g.Hout = 1;
                     g.Win = g.Wout = N.H * N.W * n;
                     nz = 1;
+                    scale_hw = N.H * N.W;
                 }
                 const float* scl = N.scale_src >= 0 ? buf(N.scale_src) : nullptr;
                 const float* res = N.res_src >= 0 ? buf(N.res_src) : nullptr;
@@ -751,20 +773,35 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                 } else if (N.bn == 16)
                     hipLaunchKernelGGL((gconv_x3t<4, 1, 4, 1>), dim3((HWo + 255) / 256, N.cout_pad / 16, nz), dim3(256),
                                        0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res);
+                                       res, scale_hw);
                 else if (N.bn == 32)
                     hipLaunchKernelGGL((gconv_x3t<4, 1, 2, 2>), dim3((HWo + 127) / 128, N.cout_pad / 32, nz), dim3(256),
                                        0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res);
-                else
-                    hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2>), dim3((HWo + 63) / 64, N.cout_pad / 64, nz), dim3(256), 0,
-                                       st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res);
+                                       res, scale_hw);
+                else if (wide_tile(d.kh * d.kw > 1))
+                    hipLaunchKernelGGL((gconv_x3t<2, 2, 4, 2>), dim3((HWo + 127) / 128, N.cout_pad / 64, nz), dim3(256),
+                                       0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
+                                       res, scale_hw);
+                else {
+                    // 64 x 64 tiles, KC 32-channel chunks per K step (the same
+                    // products summed in the same order whatever KC is)
+                    const int ncc = N.g.cin_pad / 32, kmax = kc_max();
+                    const int KC = ncc % 4 == 0 && kmax >= 4 ? 4 : ncc % 3 == 0 && kmax >= 3 ? 3
+                                   : ncc % 2 == 0 && kmax >= 2 ? 2 : 1;
+#define AA_GX(K_)                                                                                                   \
+    hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, K_>), dim3((HWo + 63) / 64, N.cout_pad / 64, nz), dim3(256), 0, st, a, \
+                       (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw)
+                    if (KC == 4) AA_GX(4);
+                    else if (KC == 3) AA_GX(3);
+                    else if (KC == 2) AA_GX(2);
+                    else AA_GX(1);
+#undef AA_GX
+                }
             } else if (N.matvec) {
                 hipLaunchKernelGGL(gmatvec, dim3((N.C + 3) / 4, n), dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
                                    out, Cin, N.C, act, d.alpha);
             } else if (d.kh * d.kw * Cin <= GF32_KMAX) {
-                hipLaunchKernelGGL(gconv_f32_lds, dim3((N.H * N.W + 255) / 256, (N.C + 31) / 32, n), dim3(256), 0, st,
+                hipLaunchKernelGGL(gconv_f32_lds, dim3((N.H * N.W + 31) / 32, (N.C + 31) / 32, n), dim3(256), 0, st,
                                    a, (const float*)N.d_w, N.d_b, out, N.g, act, d.alpha);
             } else {
                 hipLaunchKernelGGL(gconv_f32, dim3((N.H * N.W + 255) / 256, (N.C + 7) / 8, n), dim3(256), 0, st, a,

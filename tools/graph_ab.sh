@@ -1,0 +1,19 @@
+#!/bin/bash
+# Graph-executor A/B on one GPU box: alternating EfficientNetV2-shaped bench
+# runs under environment variants (kernel-choice knobs read at run time).
+# usage (through gpurun): bash tools/graph_ab.sh ROUNDS "ENV=.. ENV2=.." "..." ...   ("-": no variables)
+set -o pipefail
+R=$1; shift
+mkdir -p gpurun_out
+for r in $(seq 1 $R); do
+  for V in "$@"; do
+    [ "$V" = "-" ] && V=""
+    env $V timeout -k 10 200 python bench.py --model effnetv2 --steps 20 --warmup 5 --cpu-seconds 0 --secondary= --no-parity > gpurun_out/gab.log 2>&1 || { tail -5 gpurun_out/gab.log; exit 1; }
+    python - "${V:--}" <<'PY'
+import json, sys
+d = json.loads(open("gpurun_out/gab.log").read().strip().splitlines()[-1])
+st = sorted(d["roofline"]["stages_ms"].items(), key=lambda kv: -kv[1])[:6]
+print(f"{sys.argv[1]:28s} {d['value']:9.1f} sum={1e3 * d['roofline']['stages_sum_ms']:7.1f}us  " + " ".join(f"{k}={1e3*v:.0f}" for k, v in st), flush=True)
+PY
+  done
+done
