@@ -418,14 +418,16 @@ static __global__ __launch_bounds__(256) void gconv_f32(const float* __restrict_
 }
 
 // exact f32 for small K = kh kw Cin (<= GF32_KMAX, e.g. a 3-channel stem):
-// a block = 32 output pixels x 32 output channels (blockIdx.y), thread =
-// (pixel, 4-channel quad), so a wave stores 8 pixels' 128 contiguous bytes
-// each (1 KiB runs) and the 8 lanes of a pixel share its input loads; the
-// group's weights staged once per block in LDS as [K][32].  Each output is the
-// same chain as gconv_f32 (bias, then fma over ky, kx, ci in order): the
-// results are identical.
+// one thread per output pixel and 32 output channels (blockIdx.y), the
+// group's weights staged once per block in LDS as [K][32] and read as
+// broadcast float4s.  KH x KW x CI > 0: that shape at compile time -- the
+// pixel's K inputs are all loaded up front (clamped addresses, zero outside
+// the image), so their latency is paid once, not once per tap.  Each output is
+// the same chain as gconv_f32 (bias, then fma over ky, kx, ci in order, taps
+// outside the image skipped in both): the results are identical.
 constexpr int GF32_KMAX = 96;  // 12 KiB of LDS
-static __global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restrict__ in, const float* __restrict__ w,
+template <int KH = 0, int KW = 0, int CI = 0>
+__global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restrict__ in, const float* __restrict__ w,
                                                      const float* __restrict__ bias, float* __restrict__ out,
                                                      ConvGeom g, int act, float alpha) {
     __shared__ __attribute__((aligned(16))) float sw[GF32_KMAX * 32];
@@ -437,45 +439,67 @@ static __global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restr
         sw[i] = c0 + c < g.Cout ? w[(size_t)(c0 + c) * K + k] : 0.f;
     }
     __syncthreads();
-    const int q = threadIdx.x & 7;
-    const int P = blockIdx.x * 32 + (threadIdx.x >> 3);
+    const int P = blockIdx.x * 256 + threadIdx.x;
     if (P >= g.Hout * g.Wout) return;
     const int oy = P / g.Wout, ox = P - (P / g.Wout) * g.Wout;
     const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
-    const int cq = c0 + 4 * q;
-    float4 acc;
-    acc.x = cq < g.Cout ? bias[cq] : 0.f;
-    acc.y = cq + 1 < g.Cout ? bias[cq + 1] : 0.f;
-    acc.z = cq + 2 < g.Cout ? bias[cq + 2] : 0.f;
-    acc.w = cq + 3 < g.Cout ? bias[cq + 3] : 0.f;
-    for (int ky = 0; ky < g.kh; ++ky) {
-        const int iy = oy * g.sh - g.pt + ky;
-        if (iy < 0 || iy >= g.Hin) continue;
-        for (int kx = 0; kx < g.kw; ++kx) {
-            const int ix = ox * g.sw - g.pl + kx;
-            if (ix < 0 || ix >= g.Win) continue;
-            const float* px = img + ((size_t)iy * g.Win + ix) * g.Cin;
-            const float4* wk = reinterpret_cast<const float4*>(sw + (size_t)(ky * g.kw + kx) * g.Cin * 32) + q;
-            for (int ci = 0; ci < g.Cin; ++ci) {
-                const float x = px[ci];
-                const float4 wv = wk[ci * 8];
-                acc.x = fmaf(wv.x, x, acc.x);
-                acc.y = fmaf(wv.y, x, acc.y);
-                acc.z = fmaf(wv.z, x, acc.z);
-                acc.w = fmaf(wv.w, x, acc.w);
+    float acc[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) acc[c] = c0 + c < g.Cout ? bias[c0 + c] : 0.f;
+    auto fma32 = [&](float x, int k) {
+        const float4* wk = reinterpret_cast<const float4*>(sw + k * 32);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float4 wv = wk[c];
+            acc[4 * c + 0] = fmaf(wv.x, x, acc[4 * c + 0]);
+            acc[4 * c + 1] = fmaf(wv.y, x, acc[4 * c + 1]);
+            acc[4 * c + 2] = fmaf(wv.z, x, acc[4 * c + 2]);
+            acc[4 * c + 3] = fmaf(wv.w, x, acc[4 * c + 3]);
+        }
+    };
+    if constexpr (KH > 0) {
+        float xv[KH * KW * CI];
+        bool ok[KH * KW];
+#pragma unroll
+        for (int ky = 0; ky < KH; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < KW; ++kx) {
+                const int iy = oy * g.sh - g.pt + ky, ix = ox * g.sw - g.pl + kx;
+                ok[ky * KW + kx] = iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
+                const int cy = min(max(iy, 0), g.Hin - 1), cx = min(max(ix, 0), g.Win - 1);
+                const float* px = img + ((size_t)cy * g.Win + cx) * CI;
+#pragma unroll
+                for (int ci = 0; ci < CI; ++ci) xv[(ky * KW + kx) * CI + ci] = px[ci];
+            }
+#pragma unroll
+        for (int t = 0; t < KH * KW; ++t)
+            if (ok[t]) {
+#pragma unroll
+                for (int ci = 0; ci < CI; ++ci) fma32(xv[t * CI + ci], t * CI + ci);
+            }
+    } else {
+        for (int ky = 0; ky < g.kh; ++ky) {
+            const int iy = oy * g.sh - g.pt + ky;
+            if (iy < 0 || iy >= g.Hin) continue;
+            for (int kx = 0; kx < g.kw; ++kx) {
+                const int ix = ox * g.sw - g.pl + kx;
+                if (ix < 0 || ix >= g.Win) continue;
+                const float* px = img + ((size_t)iy * g.Win + ix) * g.Cin;
+                for (int ci = 0; ci < g.Cin; ++ci) fma32(px[ci], (ky * g.kw + kx) * g.Cin + ci);
             }
         }
     }
     float* o = out + ((size_t)n * g.Hout * g.Wout + P) * g.Cout;
-    const float4 y = make_float4(gact(acc.x, act, alpha), gact(acc.y, act, alpha), gact(acc.z, act, alpha),
-                                 gact(acc.w, act, alpha));
-    if ((g.Cout & 3) == 0 && cq + 4 <= g.Cout) {
-        *reinterpret_cast<float4*>(o + cq) = y;
+    if ((g.Cout & 3) == 0 && c0 + 32 <= g.Cout) {
+#pragma unroll
+        for (int c = 0; c < 32; c += 4)
+            *reinterpret_cast<float4*>(o + c0 + c) = make_float4(gact(acc[c], act, alpha), gact(acc[c + 1], act, alpha),
+                                                                 gact(acc[c + 2], act, alpha),
+                                                                 gact(acc[c + 3], act, alpha));
     } else {
-        if (cq < g.Cout) o[cq] = y.x;
-        if (cq + 1 < g.Cout) o[cq + 1] = y.y;
-        if (cq + 2 < g.Cout) o[cq + 2] = y.z;
-        if (cq + 3 < g.Cout) o[cq + 3] = y.w;
+#pragma unroll
+        for (int c = 0; c < 32; ++c)
+            if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], act, alpha);
     }
 }
 

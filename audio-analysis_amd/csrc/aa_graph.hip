@@ -801,8 +801,16 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                 hipLaunchKernelGGL(gmatvec, dim3((N.C + 3) / 4, n), dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
                                    out, Cin, N.C, act, d.alpha);
             } else if (d.kh * d.kw * Cin <= GF32_KMAX) {
-                hipLaunchKernelGGL(gconv_f32_lds, dim3((N.H * N.W + 31) / 32, (N.C + 31) / 32, n), dim3(256), 0, st,
-                                   a, (const float*)N.d_w, N.d_b, out, N.g, act, d.alpha);
+                const dim3 grid((N.H * N.W + 255) / 256, (N.C + 31) / 32, n);
+                if (d.kh == 3 && d.kw == 3 && Cin == 3)  // an RGB-style stem
+                    hipLaunchKernelGGL((gconv_f32_lds<3, 3, 3>), grid, dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
+                                       out, N.g, act, d.alpha);
+                else if (d.kh == 3 && d.kw == 3 && Cin == 1)
+                    hipLaunchKernelGGL((gconv_f32_lds<3, 3, 1>), grid, dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
+                                       out, N.g, act, d.alpha);
+                else
+                    hipLaunchKernelGGL((gconv_f32_lds<>), grid, dim3(256), 0, st, a, (const float*)N.d_w, N.d_b, out,
+                                       N.g, act, d.alpha);
             } else {
                 hipLaunchKernelGGL(gconv_f32, dim3((N.H * N.W + 255) / 256, (N.C + 7) / 8, n), dim3(256), 0, st, a,
                                    (const float*)N.d_w, N.d_b, out, N.g, act, d.alpha);
