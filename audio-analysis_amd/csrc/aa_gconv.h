@@ -71,13 +71,13 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
                                                  const float* __restrict__ bias, float* __restrict__ out,
                                                  ConvGeom g, int cout_pad, int act, float alpha,
                                                  const float* __restrict__ in_scale, const float* __restrict__ res,
-                                                 int scale_hw = 0) {
+                                                 int scale_hw = 0, int cslice = 0, float* __restrict__ part = nullptr) {
     static_assert(WM * WN == 4, "four waves");
     constexpr int BM = WM * MF * 16, BN = WN * NF * 16, AI = BM / 64;
     constexpr int ROW = KC * 32 + 16;  // bf16 per LDS row (+32 B: conflict-free ds_read_b128 runs)
     __shared__ __attribute__((aligned(16))) uint16_t Ah[BM * ROW], Al[BM * ROW];
     __shared__ __attribute__((aligned(16))) uint16_t Bh[BN * ROW], Bl[BN * ROW];
-    const int n = blockIdx.z;
+    const int n = part ? 0 : blockIdx.z;  // (split K: z is the slice)
     const int pix0 = blockIdx.x * BM, ch0 = blockIdx.y * BN;
     const int HWo = g.Hout * g.Wout;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -100,7 +100,11 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
     const bool bload = r < BN;
     const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
     const int ncc = g.cin_pad / 32;
-    const int ngs = ncc / KC;  // K steps per tap
+    // split K (part != nullptr, flattened pointwise convs): blockIdx.z = slice
+    // of cslice chunks, raw sums to part[slice][pixel][Cout] (gsplit_reduce
+    // adds the slices in order, then bias, residual and activation)
+    const int cbase = part ? (int)blockIdx.z * cslice : 0;
+    const int ngs = (part ? cslice : ncc) / KC;  // K steps per tap
     const int nsteps = g.kh * g.kw * ngs;
     gf32x4 acc[NF][MF];
 #pragma unroll
@@ -125,7 +129,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             const float* scl = sclp[it];
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
-                const int c0 = (gs * KC + k) * 32 + 8 * q;
+                const int c0 = (cbase + gs * KC + k) * 32 + 8 * q;
                 if (inside && vec && c0 + 8 <= g.Cin) {
                     const float4 a = *reinterpret_cast<const float4*>(px + c0);
                     const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
@@ -149,7 +153,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
         if (bload) {
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
-                const uint16_t* wrow = wpk + (((size_t)(tap * ncc + gs * KC + k) * cout_pad) + ch0 + r) * 64;
+                const uint16_t* wrow = wpk + (((size_t)(tap * ncc + cbase + gs * KC + k) * cout_pad) + ch0 + r) * 64;
                 wh[k] = *reinterpret_cast<const uint4*>(wrow + 8 * q);
                 wl[k] = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
             }
@@ -205,6 +209,24 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
         }
     }
     // D[channel][pixel]: lane holds channels 4 (lane >> 4) .. + 3 of pixel lane & 15
+    if (part) {
+#pragma unroll
+        for (int j = 0; j < MF; ++j) {
+            const int Pj = pix0 + wm * MF * 16 + j * 16 + (lane & 15);
+            if (Pj >= HWo) continue;
+            float* o = part + ((size_t)blockIdx.z * HWo + Pj) * g.Cout;
+#pragma unroll
+            for (int i = 0; i < NF; ++i) {
+                const int c = ch0 + wn * NF * 16 + i * 16 + 4 * (lane >> 4);
+                if (c + 4 <= g.Cout && (g.Cout & 3) == 0) {
+                    *reinterpret_cast<float4*>(o + c) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+                } else {
+                    for (int e = 0; e < 4 && c + e < g.Cout; ++e) o[c + e] = acc[i][j][e];
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < MF; ++j) {
         const int Pj = pix0 + wm * MF * 16 + j * 16 + (lane & 15);
@@ -226,6 +248,39 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             } else {
                 for (int e = 0; e < 4 && c + e < g.Cout; ++e) o[c + e] = y[e];
             }
+        }
+    }
+}
+
+// the split-K slices of a pointwise conv added in slice order, then the
+// epilogue of gconv_x3t (bias, residual, activation); total = pixels x Cout
+static __global__ __launch_bounds__(256) void gsplit_reduce(const float* __restrict__ part, int nslice, size_t total,
+                                                     int Cout, const float* __restrict__ bias,
+                                                     const float* __restrict__ res, float* __restrict__ out, int act,
+                                                     float alpha) {
+    const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i >= total) return;
+    if ((Cout & 3) == 0) {
+        float4 a = *reinterpret_cast<const float4*>(part + i);
+        for (int s = 1; s < nslice; ++s) {
+            const float4 b = *reinterpret_cast<const float4*>(part + (size_t)s * total + i);
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
+        const int c = (int)(i % Cout);
+        float z[4] = {a.x + bias[c], a.y + bias[c + 1], a.z + bias[c + 2], a.w + bias[c + 3]};
+        if (res) {
+            const float4 r = *reinterpret_cast<const float4*>(res + i);
+            z[0] += r.x; z[1] += r.y; z[2] += r.z; z[3] += r.w;
+        }
+        *reinterpret_cast<float4*>(out + i) =
+            make_float4(gact(z[0], act, alpha), gact(z[1], act, alpha), gact(z[2], act, alpha), gact(z[3], act, alpha));
+    } else {
+        for (size_t k = i; k < i + 4 && k < total; ++k) {
+            float a = part[k];
+            for (int s = 1; s < nslice; ++s) a += part[(size_t)s * total + k];
+            float z = a + bias[(int)(k % Cout)];
+            if (res) z += res[k];
+            out[k] = gact(z, act, alpha);
         }
     }
 }

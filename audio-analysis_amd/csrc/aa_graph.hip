@@ -21,6 +21,7 @@
 #include <array>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 
 #include "aa_common.h"
 #include "aa_gconv.h"
@@ -322,6 +323,7 @@ struct GNode {
     int H = 0, W = 0, C = 0;  // output shape
     int mfma = 0;             // conv on gconv_x3t
     int bn = 64;              // its tile's output channels (16, 32, 64)
+    int split = 1, cslice = 0;  // pointwise conv on a small map: K split into `split` slices of cslice chunks
     ConvGeom g{};
     int cout_pad = 0;
     void* d_w = nullptr;
@@ -346,16 +348,35 @@ struct Graph {
     int in_h = 0, in_w = 0, in_c = 0;
     std::vector<GNode> nodes;
     size_t per_win = 0;  // workspace f32 elements per window
+    size_t part_off = 0; // split-K partial sums (per window, after the node buffers)
     int L = 0;
     int sigmoid_out = 0;
     // HIP events around node launches (aa_graph_set_timing / aa_graph_time_stage):
     // time_stage -1 every node, >= 0 that node only, -2 none
     int time_stage = -2;
     StageTimer timer;
+    // the forward's launches captured into HIP graphs, one per (input,
+    // batch, workspace, outputs, stream): a graph model issues one launch per
+    // node (~180 for an EfficientNetV2-B0), which from the host costs about
+    // as much as the kernels take on the device; a replay is one launch
+    struct Captured {
+        const float* x;
+        int n;
+        void* ws;
+        float* logits;
+        float* probs;
+        hipStream_t st;
+        hipGraphExec_t exec;
+    };
+    std::vector<Captured> captured;
+    std::vector<Captured> seen;  // keys met once (captured the second time: a caller
+                                 // that allocates its outputs per call never pays a capture)
+    std::mutex cap_mu;
 };
 
 static void free_graph(Graph* g) {
     if (!g) return;
+    for (auto& c : g->captured) (void)hipGraphExecDestroy(c.exec);
     g->timer.release();
     for (auto& nd : g->nodes) {
         (void)hipFree(nd.d_w);
@@ -537,6 +558,19 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                 }
                 N.flops = 2.0 * N.H * N.W * K * N.C;
                 N.bytes = 4.0 * (H * W * C + N.H * N.W * N.C);
+                // a pointwise conv over >= 384 channels on a small map (<= 128
+                // pixels per window) is a short grid of long K loops: split K
+                // over blocks (shape-only choice: the sums do not depend on n)
+                if (N.mfma && ntap == 1 && d.sh == 1 && d.sw == 1 && d.pt == 0 && d.pl == 0 && N.H * N.W <= 128 &&
+                    getenv("AA_GRAPH_NOSPLIT") == nullptr) {
+                    const int ncc = N.g.cin_pad / 32;
+                    for (int cs : {6, 7, 4, 5, 8, 9})
+                        if (ncc >= 12 && ncc % cs == 0) {
+                            N.split = ncc / cs;
+                            N.cslice = cs;
+                            break;
+                        }
+                }
                 snprintf(nm, sizeof nm, "%s_%dx%d_s%d_%d_%d", N.mfma ? "conv_gx3" : N.matvec ? "matvec" : "conv_gf32",
                          d.kh, d.kw, d.sh, C, N.C);
                 break;
@@ -680,7 +714,11 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
             if (it != live.end()) live.erase(it);
         }
     }
-    G->per_win = (peak + 63) / 64 * 64;
+    G->part_off = (peak + 63) / 64 * 64;
+    size_t part = 0;
+    for (const GNode& N : G->nodes)
+        if (N.split > 1 && !N.skip) part = std::max(part, (size_t)N.split * N.H * N.W * N.C);
+    G->per_win = G->part_off + (part + 63) / 64 * 64;
     const GNode& O = G->nodes[last];
     G->L = O.H * O.W * O.C;
     G->sigmoid_out = O.d.act == AA_GACT_SIGMOID;
@@ -782,7 +820,21 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     hipLaunchKernelGGL((gconv_x3t<2, 2, 4, 2>), dim3((HWo + 127) / 128, N.cout_pad / 64, nz), dim3(256),
                                        0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
                                        res, scale_hw);
-                else {
+                else if (N.split > 1 && nz == 1) {
+                    // split K: slices of cslice chunks on blockIdx.z, then the ordered sum
+                    float* part = ws + G.part_off * (size_t)n;
+                    const dim3 grid((HWo + 63) / 64, N.cout_pad / 64, N.split);
+                    if (N.cslice % 2 == 0 && kc_max() >= 2)
+                        hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 2>), grid, dim3(256), 0, st, a, (const uint16_t*)N.d_w,
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, N.cslice, part);
+                    else
+                        hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 1>), grid, dim3(256), 0, st, a, (const uint16_t*)N.d_w,
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, N.cslice, part);
+                    AA_LAUNCH_CHECK();
+                    const size_t total = (size_t)HWo * N.C;
+                    hipLaunchKernelGGL(gsplit_reduce, dim3((unsigned)((total / 4 + 255) / 256 + 1)), dim3(256), 0, st, part,
+                                       N.split, total, N.C, N.d_b, res, out, act, d.alpha);
+                } else {
                     // 64 x 64 tiles, KC 32-channel chunks per K step (the same
                     // products summed in the same order whatever KC is)
                     const int ncc = N.g.cin_pad / 32, kmax = kc_max();
@@ -921,6 +973,33 @@ extern "C" size_t aa_graph_workspace_bytes(const void* graph, int32_t max_batch)
     return align_up(G->per_win * 4 * (size_t)std::min<int32_t>(max_batch, 32768), 256);
 }
 
+// the forward's launches for n windows (<= 32768) on stream st
+static int graph_enqueue(Graph* G, const float* x, int32_t n, float* logits, float* probs, float* ws,
+                         hipStream_t st) {
+    G->timer.mask = 0xFFFFFFFFu;  // the node filter is time_stage (graphs exceed 32 stages)
+    for (size_t i = 0; i < G->nodes.size(); ++i) {
+        if (G->nodes[i].skip || G->nodes[i].nolaunch) continue;
+        const bool timed = G->time_stage == -1 || G->time_stage == (int)i;
+        hipEvent_t e0 = nullptr;
+        if (timed) {
+            const int rc = G->timer.begin(0, st, &e0);
+            if (rc != AA_OK) return rc;
+        }
+        const int rc = graph_run_node(*G, G->nodes[i], x, ws, n, st);
+        if (rc != AA_OK) return rc;
+        if (timed) {
+            const int rc2 = G->timer.end((int)i, st, e0);
+            if (rc2 != AA_OK) return rc2;
+        }
+    }
+    const GNode& O = G->nodes.back();
+    const size_t total = (size_t)G->L * n;
+    hipLaunchKernelGGL(gfinal, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ws + O.off * (size_t)n, logits,
+                       probs, total, G->sigmoid_out);
+    AA_LAUNCH_CHECK();
+    return AA_OK;
+}
+
 extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* logits, float* probs, void* workspace,
                                 size_t workspace_bytes, void* stream) {
     Graph* G = static_cast<Graph*>(graph);
@@ -931,32 +1010,59 @@ extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* l
     AA_CHECK(workspace && workspace_bytes >= aa_graph_workspace_bytes(G, nc0), AA_ERR_WORKSPACE,
              "aa_graph_forward: workspace %zu < %zu", workspace_bytes, aa_graph_workspace_bytes(G, nc0));
     hipStream_t st = static_cast<hipStream_t>(stream);
+    float* ws = static_cast<float*>(workspace);
     const size_t in_per = (size_t)G->in_h * G->in_w * G->in_c;
+    static const bool no_capture = getenv("AA_GRAPH_NOCAPTURE") != nullptr;  // (A/B knob)
+    // replay a captured forward (not while timing nodes: the events would be
+    // baked into the capture; not on the legacy null stream, which cannot capture)
+    if (n <= CHUNK && G->time_stage == -2 && st != nullptr && !no_capture) {
+        std::lock_guard<std::mutex> lk(G->cap_mu);
+        auto same = [&](const Graph::Captured& c) {
+            return c.x == x && c.n == n && c.ws == workspace && c.logits == logits && c.probs == probs && c.st == st;
+        };
+        for (const auto& c : G->captured)
+            if (same(c)) {
+                AA_HIP(hipGraphLaunch(c.exec, st));
+                return AA_OK;
+            }
+        bool again = false;
+        for (auto it = G->seen.begin(); it != G->seen.end(); ++it)
+            if (same(*it)) {
+                again = true;
+                G->seen.erase(it);
+                break;
+            }
+        if (!again) {
+            if (G->seen.size() >= 16) G->seen.erase(G->seen.begin());
+            G->seen.push_back(Graph::Captured{x, n, workspace, logits, probs, st, nullptr});
+            return graph_enqueue(G, x, n, logits, probs, ws, st);
+        }
+        hipGraph_t hg = nullptr;
+        AA_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        const int rc = graph_enqueue(G, x, n, logits, probs, ws, st);
+        const hipError_t ec = hipStreamEndCapture(st, &hg);
+        if (rc != AA_OK) {
+            if (hg) (void)hipGraphDestroy(hg);
+            return rc;
+        }
+        AA_HIP(ec);
+        hipGraphExec_t exec = nullptr;
+        const hipError_t ei = hipGraphInstantiate(&exec, hg, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(hg);
+        AA_HIP(ei);
+        if (G->captured.size() >= 16) {  // bounded: the oldest goes
+            (void)hipGraphExecDestroy(G->captured.front().exec);
+            G->captured.erase(G->captured.begin());
+        }
+        G->captured.push_back(Graph::Captured{x, n, workspace, logits, probs, st, exec});
+        AA_HIP(hipGraphLaunch(exec, st));
+        return AA_OK;
+    }
     for (int32_t c0 = 0; c0 < n; c0 += CHUNK) {
         const int32_t nc = std::min(CHUNK, n - c0);
-        float* ws = static_cast<float*>(workspace);
-        G->timer.mask = 0xFFFFFFFFu;  // the node filter is time_stage (graphs exceed 32 stages)
-        for (size_t i = 0; i < G->nodes.size(); ++i) {
-            if (G->nodes[i].skip || G->nodes[i].nolaunch) continue;
-            const bool timed = G->time_stage == -1 || G->time_stage == (int)i;
-            hipEvent_t e0 = nullptr;
-            if (timed) {
-                const int rc = G->timer.begin(0, st, &e0);
-                if (rc != AA_OK) return rc;
-            }
-            const int rc = graph_run_node(*G, G->nodes[i], x + (size_t)c0 * in_per, ws, nc, st);
-            if (rc != AA_OK) return rc;
-            if (timed) {
-                const int rc2 = G->timer.end((int)i, st, e0);
-                if (rc2 != AA_OK) return rc2;
-            }
-        }
-        const GNode& O = G->nodes.back();
-        const size_t total = (size_t)G->L * nc;
-        hipLaunchKernelGGL(gfinal, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ws + O.off * (size_t)nc,
-                           logits + (size_t)c0 * G->L, probs ? probs + (size_t)c0 * G->L : nullptr, total,
-                           G->sigmoid_out);
-        AA_LAUNCH_CHECK();
+        const int rc = graph_enqueue(G, x + (size_t)c0 * in_per, nc, logits + (size_t)c0 * G->L,
+                                     probs ? probs + (size_t)c0 * G->L : nullptr, ws, st);
+        if (rc != AA_OK) return rc;
     }
     return AA_OK;
 }

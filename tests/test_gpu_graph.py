@@ -72,3 +72,36 @@ def test_graph_model_large_batch_is_batch_invariant(gpu, tmp_path):
     a = m.forward(xt)[0].cpu().numpy()
     b = np.concatenate([m.forward(xt[i:i + 7])[0].cpu().numpy() for i in range(0, 40, 7)])
     assert np.array_equal(a, b)
+
+
+def test_graph_capture_replay_matches_direct_launches(gpu, tmp_path):
+    """aa_graph_forward replays a captured HIP graph of its launches (one per
+    input / batch / workspace / output / stream); with node timing on it
+    launches node by node.  Both give the same logits, and a replay after the
+    input changed sees the new input."""
+    from aa_amd.model import Model
+    p = make_graph(tmp_path / "v2", "effnetv2", in_channels=3, T=160, seed=7)
+    rng = np.random.default_rng(5)
+    x = np.repeat(calibration_input(4, 160, 160, True, rng), 3, axis=3)
+    m = Model(p, x.shape[1:])
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        xt = torch.from_numpy(x).cuda()
+        lg = torch.empty((4, m.n_labels), dtype=torch.float32, device=xt.device)
+        pr = torch.empty_like(lg)
+        ws = m._workspace(4)
+        run = lambda: m.forward(xt, lg, pr, workspace=ws)[0].cpu().numpy()
+        a = run()      # node by node (first sight of these buffers)
+        b = run()      # captured and launched
+        b2 = run()     # replayed
+        m.set_timing(True)
+        c = run()      # node by node
+        m.set_timing(False)
+        xt.copy_(torch.from_numpy(np.repeat(calibration_input(4, 160, 160, True, rng), 3, axis=3)).cuda())
+        d = run()      # replayed on the new input
+        m.set_timing(True)
+        e = run()
+        m.set_timing(False)
+    torch.cuda.synchronize()
+    assert np.array_equal(a, b) and np.array_equal(a, b2) and np.array_equal(a, c)
+    assert np.array_equal(d, e) and not np.array_equal(a, d)
