@@ -309,6 +309,23 @@ __global__ __launch_bounds__(256) void gpow(const float* __restrict__ in, float*
     if (i < total) out[i] = powf(in[i], e);
 }
 
+// [n][K] x W[K][Cout] + bias for short K: one thread per (window, output),
+// lanes along the outputs (coalesced weight rows), the K products summed in
+// order
+__global__ __launch_bounds__(256) void gmatvec_t(const float* __restrict__ in, const float* __restrict__ w,
+                                                 const float* __restrict__ bias, float* __restrict__ out, int K,
+                                                 int Cout, int act, float alpha) {
+    const int o = blockIdx.x * 256 + threadIdx.x;
+    const int n = blockIdx.y;
+    if (o >= Cout) return;
+    const float* x = in + (size_t)n * K;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < K; ++k) acc = fmaf(x[k], w[(size_t)k * Cout + o], acc);  // (loads 8 ahead, one ordered chain)
+    if (bias) acc += bias[o];
+    out[(size_t)n * Cout + o] = gact(acc, act, alpha);
+}
+
 __global__ __launch_bounds__(256) void gfinal(const float* __restrict__ x, float* __restrict__ logits,
                                               float* __restrict__ probs, size_t total, int sigmoid) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -548,10 +565,15 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                     for (int o = 0; o < N.C; ++o) bias[o] = b ? b[o] : 0.f;
                     if ((rc = gupload((void**)&N.d_b, bias.data(), bias.size() * 4)) != AA_OK) return rc;
                 } else {
+                    // [Cout][K]; a matrix-vector product with K <= 64 keeps the
+                    // Keras [K][Cout] order (gmatvec_t: one thread per output)
+                    if (N.matvec && K <= 64) N.matvec = 2;
                     std::vector<float> w_ohwc((size_t)N.C * K);
                     for (int o = 0; o < N.C; ++o)
                         for (int kk = 0; kk < K; ++kk) w_ohwc[(size_t)o * K + kk] = k[(size_t)kk * N.C + o];
-                    if ((rc = gupload(&N.d_w, w_ohwc.data(), w_ohwc.size() * 4)) != AA_OK) return rc;
+                    if ((rc = N.matvec == 2 ? gupload(&N.d_w, k, (size_t)K * N.C * 4)
+                                            : gupload(&N.d_w, w_ohwc.data(), w_ohwc.size() * 4)) != AA_OK)
+                        return rc;
                     std::vector<float> bias(N.C, 0.f);
                     for (int o = 0; o < N.C; ++o) bias[o] = b ? b[o] : 0.f;
                     if ((rc = gupload((void**)&N.d_b, bias.data(), bias.size() * 4)) != AA_OK) return rc;
@@ -849,6 +871,9 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     else AA_GX(1);
 #undef AA_GX
                 }
+            } else if (N.matvec == 2) {
+                hipLaunchKernelGGL(gmatvec_t, dim3((N.C + 255) / 256, n), dim3(256), 0, st, a, (const float*)N.d_w,
+                                   N.d_b, out, Cin, N.C, act, d.alpha);
             } else if (N.matvec) {
                 hipLaunchKernelGGL(gmatvec, dim3((N.C + 3) / 4, n), dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
                                    out, Cin, N.C, act, d.alpha);
