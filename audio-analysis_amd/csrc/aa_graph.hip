@@ -813,7 +813,18 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     const size_t lds = (size_t)((TH - 1) * d.sh + d.kh) * ((TW - 1) * d.sw + d.kw) * GX_ROW * 4;
                     if (lds > 65536) BM = 0;
                 }
-                if (BM) {
+                // (A/B knob AA_GRAPH_Q=1: measured slower -- 3x3 32->128 161 -> 197 us,
+                // 48->192 118 -> 148 us: two waves per SIMD wait out a barrier per tap)
+                static const bool useq = getenv("AA_GRAPH_Q") != nullptr;
+                if (!BM && useq && N.bn == 64 && d.kh * d.kw > 1 && d.kh <= 3 && d.kw <= 3 && d.sh == 1 &&
+                    d.sw == 1) {
+                    // stride 1 at 64 channels per block: patch + two-slot weight ring
+                    const int tiles_w = (N.W + 15) / 16, tiles_h = (N.H + 7) / 8;
+                    const size_t lds = ((size_t)(7 + d.kh) * (15 + d.kw) * 2 + 4 * 64) * GX_ROW * 2;
+                    const dim3 grid((unsigned)(tiles_w * tiles_h), N.cout_pad / 64, n);
+                    hipLaunchKernelGGL((gconv_x3q<4, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w, N.d_b,
+                                       out, g, N.cout_pad, act, d.alpha, tiles_w, scl, res);
+                } else if (BM) {
                     const int TH = BM / TW;
                     const int tiles_w = (N.W + TW - 1) / TW, tiles_h = (N.H + TH - 1) / TH;
                     const size_t lds = (size_t)((TH - 1) * d.sh + d.kh) * ((TW - 1) * d.sw + d.kw) * GX_ROW * 4;
