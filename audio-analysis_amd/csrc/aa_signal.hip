@@ -73,6 +73,8 @@ struct SnPlan {
     StageTimer timer;          // HIP events around the launches of the stages in timer.mask
     bool select_reg = false;   // row medians by sn_select_reg (AA_SN_SELECT=reg; A/B knob) or sn_select
     bool stft_r8 = false;      // the transform by sn_stft64r8 (AA_SN_STFT=r8; A/B knob) or sn_stft64
+    bool colmed_bs = false;    // column medians by bit-serial search (AA_SN_COLMED=bs; A/B knob: 52 us against
+                               // the LDS-histogram radix select's 44) or radix select
     int diag = 0;              // AA_SN_DIAG: ablation bits of sn_select_reg (tools only; results then invalid)
 };
 
@@ -648,13 +650,60 @@ __device__ __forceinline__ unsigned wave_median_2049(const unsigned (&v)[33], un
     return prefix;
 }
 
+// The same median by a bit-serial search with no LDS (A/B variant, measured
+// slower: VALU-bound at ~27 bits x 70 ops per frame): from the bits below the
+// frame's common min / max prefix down, keep a candidate bit when fewer than
+// rank + 1 values lie below the candidate.  A count is 33 compare-and-adds per
+// lane and a DPP reduction (popcounting the 33 ballots instead kept the one
+// scalar unit a CU shares busy: 52 us against the histograms' 44); the
+// histogram atomics and their bank conflicts are gone.  Values outside the frame (v[32] of lanes
+// other than 0) are 0xFFFFFFFF: never below a candidate.  The result is the
+// exact (rank)-th smallest pattern, as wave_median_2049's.
+__device__ __forceinline__ unsigned wave_median_2049_bs(const unsigned (&v)[33], int lane) {
+    unsigned mn = v[0], mx = v[0];
+#pragma unroll
+    for (int i = 1; i < 33; ++i) {
+        if (i == 32 && lane != 0) break;
+        mn = min(mn, v[i]);
+        mx = max(mx, v[i]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    mn = __builtin_amdgcn_readfirstlane(mn);
+    mx = __builtin_amdgcn_readfirstlane(mx);
+    if (mn == mx) return mn;
+    const int hb = 31 - __clz(mn ^ mx);
+    unsigned ans = hb == 31 ? 0u : (mn & (0xFFFFFFFFu << (hb + 1)));
+    const unsigned rank = kSnBins / 2;
+#pragma unroll 1
+    for (int b = hb; b >= 0; --b) {
+        const unsigned cand = ans | (1u << b);
+        unsigned c = 0;  // the lane's values below the candidate (compare + carry-add each)
+#pragma unroll
+        for (int i = 0; i < 33; ++i) c += v[i] < cand ? 1u : 0u;
+        // the wave's sum: within rows of 16 lanes by DPP, then the four row sums
+        c += (unsigned)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+        c += (unsigned)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+        c += (unsigned)__builtin_amdgcn_update_dpp(0, (int)c, 0x124, 0xF, 0xF, false);  // row_ror:4
+        c += (unsigned)__builtin_amdgcn_update_dpp(0, (int)c, 0x128, 0xF, 0xF, false);  // row_ror:8
+        const unsigned cnt = __builtin_amdgcn_readlane(c, 0) + __builtin_amdgcn_readlane(c, 16) +
+                             __builtin_amdgcn_readlane(c, 32) + __builtin_amdgcn_readlane(c, 48);
+        if (cnt <= rank) ans = cand;  // (wave-uniform)
+    }
+    return ans;
+}
+
 // sn_colmed: one wave per frame, the frame's S row (2049 floats, just
 // written by sn_stft64: L2 / Infinity-Cache resident) into registers, its
 // median over bins into colmed[f].  Four frames per 256-thread block, 4 KiB
 // of histograms per wave.
+template <bool BS>
 __global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, int ld, int n_frames,
                                                  unsigned* __restrict__ colmed) {
-    __shared__ unsigned hists[4][4 * kSnHist];
+    __shared__ unsigned hists[BS ? 1 : 4][BS ? 1 : 4 * kSnHist];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.x * 4 + wave;
     if (f >= n_frames) return;  // wave-uniform; no block barrier below
@@ -662,8 +711,14 @@ __global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, in
     unsigned v[33];
 #pragma unroll
     for (int i = 0; i < 32; ++i) v[i] = row[lane + 64 * i];
-    v[32] = lane == 0 ? row[2048] : 0u;
-    const unsigned med = wave_median_2049(v, hists[wave], lane);
+    unsigned med;
+    if constexpr (BS) {
+        v[32] = lane == 0 ? row[2048] : 0xFFFFFFFFu;
+        med = wave_median_2049_bs(v, lane);
+    } else {
+        v[32] = lane == 0 ? row[2048] : 0u;
+        med = wave_median_2049(v, hists[wave], lane);
+    }
     if (lane == 0) colmed[f] = med;
 }
 
@@ -1535,7 +1590,10 @@ static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const i
         if (rc != AA_OK) return rc;
         hipEvent_t e1;
         if ((rc = p->timer.begin(SN_STAGE_COLMED, st, &e1)) != AA_OK) return rc;
-        hipLaunchKernelGGL(sn_colmed, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
+        if (p->colmed_bs)
+            hipLaunchKernelGGL(sn_colmed<true>, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
+        else
+            hipLaunchKernelGGL(sn_colmed<false>, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
         AA_LAUNCH_CHECK();
         if ((rc = p->timer.end(SN_STAGE_COLMED, st, e1)) != AA_OK) return rc;
         const int words = (F + 63) / 64, ldt = words * 64;
@@ -1610,6 +1668,7 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
     if (const char* e = std::getenv("AA_SN_SELECT")) p->select_reg = std::strcmp(e, "reg") == 0;
     if (const char* e = std::getenv("AA_SN_DIAG")) p->diag = std::atoi(e);
     if (const char* e = std::getenv("AA_SN_STFT")) p->stft_r8 = std::strcmp(e, "r8") == 0;
+    if (const char* e = std::getenv("AA_SN_COLMED")) p->colmed_bs = std::strcmp(e, "bs") == 0;
     // sn_stft64's tables, rounded from long double
     auto wexp = [](long long e, long long m) {  // exp(-2 pi i e / m)
         const long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)(e % m) / (long double)m;

@@ -107,6 +107,21 @@ def test_spectrogram_variants_bit_exact(gpu, monkeypatch, variant, n, seed):
         assert stats.tolist() == ref_stats.tolist()
 
 
+@pytest.mark.parametrize("colmed", ["bs", "hist"])
+def test_column_median_variants(gpu, monkeypatch, colmed):
+    """Both column-median kernels (radix select with LDS histograms, the
+    default; bit-serial search, AA_SN_COLMED=bs) give the oracle's mask."""
+    monkeypatch.setenv("AA_SN_COLMED", colmed)
+    x = _clip(60.0, 38)
+    det = _det(gpu)
+    F = det.n_frames(len(x))
+    mask_dev = torch.empty((2049, det.words(F)), dtype=torch.int64, device=gpu)
+    stats = det.components(torch.from_numpy(x).to(gpu), mask_out=mask_dev)
+    _, ref_mask, ref_stats = so.signal_noise(x, SR, HOP)
+    assert int((_unpack(mask_dev.cpu().numpy(), F) != ref_mask).sum()) == 0
+    assert stats.tolist() == ref_stats.tolist()
+
+
 def _assert_s_equal(got, want):
     d = got.view(np.uint32) != want.view(np.uint32)
     ulps = np.abs(got.view(np.int32)[d].astype(np.int64) - want.view(np.int32)[d].astype(np.int64))
