@@ -73,6 +73,8 @@ struct SnPlan {
     StageTimer timer;          // HIP events around the launches of the stages in timer.mask
     bool select_reg = false;   // row medians by sn_select_reg (AA_SN_SELECT=reg; A/B knob) or sn_select
     bool stft_r8 = false;      // the transform by sn_stft64r8 (AA_SN_STFT=r8; A/B knob) or sn_stft64
+    bool colmed_fused = false; // column medians inside sn_stft64 (AA_SN_COLMED=fused; A/B knob: 188 us per
+                               // clip against 98 + 44 as two launches) or their own launch
     bool colmed_bs = false;    // column medians by bit-serial search (AA_SN_COLMED=bs; A/B knob: 52 us against
                                // the LDS-histogram radix select's 44) or radix select
     int diag = 0;              // AA_SN_DIAG: ablation bits of sn_select_reg (tools only; results then invalid)
@@ -292,10 +294,17 @@ static_assert(16 * kS64R1 <= kS64Buf && (kS64Mag + 2049) * 4 <= kS64Buf * 16, "s
 // window (halved) as pairs (w[2n], w[2n + 1]); tw1: W256^(n2 k1) [k1 - 1][n2];
 // tw3: W2048^(n3 j) [n3 - 1][j]; twS: W4096^t (thread 0: W4096^128), the
 // split's per-thread base.
+__device__ unsigned wave_median_2049(const unsigned (&v)[33], unsigned* hists, int lane);
+
+// colmed (may be null; A/B variant AA_SN_COLMED=fused): the frame's median
+// over bins, by wave 0 from the LDS copy of the magnitudes while wave 1 waits
+// at the frame's last barrier.  Measured 188 us per clip against 98 + 44 us as
+// two launches: the select holds the block -- and its 36 KiB of LDS -- far
+// longer than the transform, and 4 blocks per CU leave nothing to fill in.
 __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) void sn_stft64(
     const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const double2* __restrict__ win2,
     const double2* __restrict__ tw1, const double2* __restrict__ tw3, const double2* __restrict__ twS,
-    float* __restrict__ S, int ld, unsigned* __restrict__ gmax) {
+    float* __restrict__ S, int ld, unsigned* __restrict__ gmax, unsigned* __restrict__ colmed = nullptr) {
     __shared__ double2 buf[kS64Buf];
     const int t = threadIdx.x;
     const bool z = t == 0;
@@ -447,6 +456,16 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
             const float m = mag[2048];
             srow[2048] = m;
             wmax = max(wmax, __float_as_uint(m));
+        }
+        if (colmed && t < 64) {
+            unsigned vv[33];
+#pragma unroll
+            for (int i = 0; i < 32; ++i) vv[i] = __float_as_uint(mag[t + 64 * i]);
+            vv[32] = z ? __float_as_uint(mag[2048]) : 0u;
+            // histograms after the magnitudes (floats 64 .. 2112 of the buffer)
+            unsigned* hists = reinterpret_cast<unsigned*>(buf) + 2176;
+            const unsigned med = wave_median_2049(vv, hists, t);
+            if (z) colmed[fi] = med;
         }
         __syncthreads();  // the buffer is rewritten by the next frame
     }
@@ -1540,7 +1559,7 @@ static int sn_components(SnPlan& p, const SnWs& ws, const SnBatch& nb, bool with
 // sn_stft64 over one recording: persistent blocks (4 per CU, the LDS limit),
 // a multiple of 8 so every XCD owns an equal share of the blocks
 static int sn_launch_stft(SnPlan& p, const float* pcm, int64_t n, int F, float* S, int ld, unsigned* gmax,
-                          hipStream_t st) {
+                          hipStream_t st, unsigned* colmed = nullptr) {
     int grid = std::min(F, 256 * 4);
     grid = (grid + 7) & ~7;
     const double2* tab = p.d_tab;
@@ -1552,7 +1571,7 @@ static int sn_launch_stft(SnPlan& p, const float* pcm, int64_t n, int F, float* 
                            tab + kR8Tw1, tab + kR8Tw2, tab + kR8Tw3, tab + kR8TwS, S, ld, gmax);
     else
         hipLaunchKernelGGL(sn_stft64, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
-                           tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax);
+                           tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax, colmed);
     AA_LAUNCH_CHECK();
     return p.timer.end(SN_STAGE_STFT, st, e0);
 }
@@ -1586,16 +1605,21 @@ static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const i
         unsigned* colmed = sn_at(ws.colmed, ws.pf, k);
         float* c3 = sn_at(ws.c3, ws.pf, k);
         unsigned long long* M0 = sn_at(ws.M0, ws.pf, k);
-        int rc = sn_launch_stft(*p, lens[k] ? pcm + offs[k] : pcm, lens[k], F, ws.S, kSnLd, gmax, st);
+        // column medians inside sn_stft64 (default) or as their own launch
+        const bool fused = p->colmed_fused && !p->stft_r8 && !p->colmed_bs;
+        int rc = sn_launch_stft(*p, lens[k] ? pcm + offs[k] : pcm, lens[k], F, ws.S, kSnLd, gmax, st,
+                                fused ? colmed : nullptr);
         if (rc != AA_OK) return rc;
-        hipEvent_t e1;
-        if ((rc = p->timer.begin(SN_STAGE_COLMED, st, &e1)) != AA_OK) return rc;
-        if (p->colmed_bs)
-            hipLaunchKernelGGL(sn_colmed<true>, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
-        else
-            hipLaunchKernelGGL(sn_colmed<false>, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
-        AA_LAUNCH_CHECK();
-        if ((rc = p->timer.end(SN_STAGE_COLMED, st, e1)) != AA_OK) return rc;
+        if (!fused) {
+            hipEvent_t e1;
+            if ((rc = p->timer.begin(SN_STAGE_COLMED, st, &e1)) != AA_OK) return rc;
+            if (p->colmed_bs)
+                hipLaunchKernelGGL(sn_colmed<true>, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
+            else
+                hipLaunchKernelGGL(sn_colmed<false>, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
+            AA_LAUNCH_CHECK();
+            if ((rc = p->timer.end(SN_STAGE_COLMED, st, e1)) != AA_OK) return rc;
+        }
         const int words = (F + 63) / 64, ldt = words * 64;
         hipEvent_t e0;
         if ((rc = p->timer.begin(SN_STAGE_TRANSPOSE, st, &e0)) != AA_OK) return rc;
@@ -1668,7 +1692,10 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
     if (const char* e = std::getenv("AA_SN_SELECT")) p->select_reg = std::strcmp(e, "reg") == 0;
     if (const char* e = std::getenv("AA_SN_DIAG")) p->diag = std::atoi(e);
     if (const char* e = std::getenv("AA_SN_STFT")) p->stft_r8 = std::strcmp(e, "r8") == 0;
-    if (const char* e = std::getenv("AA_SN_COLMED")) p->colmed_bs = std::strcmp(e, "bs") == 0;
+    if (const char* e = std::getenv("AA_SN_COLMED")) {
+        p->colmed_bs = std::strcmp(e, "bs") == 0;
+        p->colmed_fused = std::strcmp(e, "fused") == 0;
+    }
     // sn_stft64's tables, rounded from long double
     auto wexp = [](long long e, long long m) {  // exp(-2 pi i e / m)
         const long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)(e % m) / (long double)m;

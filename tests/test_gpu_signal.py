@@ -107,10 +107,11 @@ def test_spectrogram_variants_bit_exact(gpu, monkeypatch, variant, n, seed):
         assert stats.tolist() == ref_stats.tolist()
 
 
-@pytest.mark.parametrize("colmed", ["bs", "hist"])
+@pytest.mark.parametrize("colmed", ["fused", "sep", "bs"])
 def test_column_median_variants(gpu, monkeypatch, colmed):
-    """Both column-median kernels (radix select with LDS histograms, the
-    default; bit-serial search, AA_SN_COLMED=bs) give the oracle's mask."""
+    """Every column-median form -- radix select as its own launch (the
+    default), the same select inside the STFT kernel (AA_SN_COLMED=fused), the
+    bit-serial search (AA_SN_COLMED=bs) -- gives the oracle's mask."""
     monkeypatch.setenv("AA_SN_COLMED", colmed)
     x = _clip(60.0, 38)
     det = _det(gpu)
