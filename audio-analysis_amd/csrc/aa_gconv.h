@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
                                                  const float* __restrict__ in_scale, const float* __restrict__ res,
                                                  int scale_hw = 0, int cslice = 0, float* __restrict__ part = nullptr) {
     static_assert(WM * WN == 4, "four waves");
-    constexpr int BM = WM * MF * 16, BN = WN * NF * 16, AI = BM / 64;
+    constexpr int BM = WM * MF * 16, BN = WN * NF * 16, AI = BM / 64, BI = (BN + 63) / 64;
     constexpr int ROW = KC * 32 + 16;  // bf16 per LDS row (+32 B: conflict-free ds_read_b128 runs)
     __shared__ __attribute__((aligned(16))) uint16_t Ah[BM * ROW], Al[BM * ROW];
     __shared__ __attribute__((aligned(16))) uint16_t Bh[BN * ROW], Bl[BN * ROW];
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
                    : scale_hw > 0 ? in_scale + (size_t)((pv[it] ? P : 0) / scale_hw) * g.Cin
                                   : in_scale + (size_t)n * g.Cin;
     }
-    const bool bload = r < BN;
+    // weight rows r + 64 ib (ib < BI) of the block's BN
     const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
     const int ncc = g.cin_pad / 32;
     // split K (part != nullptr, flattened pointwise convs): blockIdx.z = slice
@@ -113,9 +113,11 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
         for (int j = 0; j < MF; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
     const bool vec = (g.Cin & 7) == 0;
     float v[AI][KC][8];
-    uint4 wh[KC], wl[KC];
+    uint4 wh[BI][KC], wl[BI][KC];
 #pragma unroll
-    for (int k = 0; k < KC; ++k) wh[k] = wl[k] = make_uint4(0, 0, 0, 0);
+    for (int ib = 0; ib < BI; ++ib)
+#pragma unroll
+        for (int k = 0; k < KC; ++k) wh[ib][k] = wl[ib][k] = make_uint4(0, 0, 0, 0);
     // step s = (tap, chunks KC gs .. KC gs + KC - 1): this thread's 8 channels
     // of AI pixels per chunk and its 8 hi + 8 lo weights per chunk
     auto load = [&](int s) {
@@ -150,12 +152,15 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
                 }
             }
         }
-        if (bload) {
+#pragma unroll
+        for (int ib = 0; ib < BI; ++ib) {
+            if (r + 64 * ib >= BN) continue;
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
-                const uint16_t* wrow = wpk + (((size_t)(tap * ncc + cbase + gs * KC + k) * cout_pad) + ch0 + r) * 64;
-                wh[k] = *reinterpret_cast<const uint4*>(wrow + 8 * q);
-                wl[k] = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
+                const uint16_t* wrow =
+                    wpk + (((size_t)(tap * ncc + cbase + gs * KC + k) * cout_pad) + ch0 + r + 64 * ib) * 64;
+                wh[ib][k] = *reinterpret_cast<const uint4*>(wrow + 8 * q);
+                wl[ib][k] = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
             }
         }
     };
@@ -179,11 +184,13 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
                 *reinterpret_cast<gbf16x8*>(Ah + (r + 64 * it) * ROW + 32 * k + 8 * q) = h[it][k];
                 *reinterpret_cast<gbf16x8*>(Al + (r + 64 * it) * ROW + 32 * k + 8 * q) = l[it][k];
             }
-        if (bload) {
+#pragma unroll
+        for (int ib = 0; ib < BI; ++ib) {
+            if (r + 64 * ib >= BN) continue;
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
-                *reinterpret_cast<uint4*>(Bh + r * ROW + 32 * k + 8 * q) = wh[k];
-                *reinterpret_cast<uint4*>(Bl + r * ROW + 32 * k + 8 * q) = wl[k];
+                *reinterpret_cast<uint4*>(Bh + (r + 64 * ib) * ROW + 32 * k + 8 * q) = wh[ib][k];
+                *reinterpret_cast<uint4*>(Bl + (r + 64 * ib) * ROW + 32 * k + 8 * q) = wl[ib][k];
             }
         }
         __syncthreads();

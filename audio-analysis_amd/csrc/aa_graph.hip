@@ -767,6 +767,13 @@ static int kc_max() {
     return k;
 }
 
+// 64 x 128 tiles for short-K pointwise convs with C_out a multiple of 128
+// (A/B knob AA_GRAPH_NOWIDEN: 42.3k -> 43.2k audio-s/s on the EfficientNetV2 graph)
+static bool wide_n() {
+    static const bool w = getenv("AA_GRAPH_NOWIDEN") == nullptr;
+    return w;
+}
+
 static int graph_run_node(const Graph& G, const GNode& N, const float* x, float* ws, int n, hipStream_t st) {
     const aa_node& d = N.d;
     auto buf = [&](int k) -> const float* {
@@ -847,6 +854,11 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                                        res, scale_hw);
                 else if (N.bn == 32)
                     hipLaunchKernelGGL((gconv_x3t<4, 1, 2, 2>), dim3((HWo + 127) / 128, N.cout_pad / 32, nz), dim3(256),
+                                       0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
+                                       res, scale_hw);
+                else if (wide_n() && d.kh * d.kw == 1 && N.C >= 128 && N.g.cin_pad <= 256 && N.cout_pad % 128 == 0)
+                    // 64 x 128 tiles: half the re-reads of the pixel tile
+                    hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 4>), dim3((HWo + 63) / 64, N.cout_pad / 128, nz), dim3(256),
                                        0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
                                        res, scale_hw);
                 else if (wide_tile(d.kh * d.kw > 1))
