@@ -583,7 +583,11 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                 // a pointwise conv over >= 384 channels on a small map (<= 128
                 // pixels per window) is a short grid of long K loops: split K
                 // over blocks (shape-only choice: the sums do not depend on n)
-                if (N.mfma && ntap == 1 && d.sh == 1 && d.sw == 1 && d.pt == 0 && d.pl == 0 && N.H * N.W <= 128 &&
+                static const int split_hw = [] {  // (A/B knob AA_GRAPH_SPLITHW)
+                    const char* e = getenv("AA_GRAPH_SPLITHW");
+                    return e ? std::atoi(e) : 128;
+                }();
+                if (N.mfma && ntap == 1 && d.sh == 1 && d.sw == 1 && d.pt == 0 && d.pl == 0 && N.H * N.W <= split_hw &&
                     getenv("AA_GRAPH_NOSPLIT") == nullptr) {
                     const int ncc = N.g.cin_pad / 32;
                     for (int cs : {6, 7, 4, 5, 8, 9})
