@@ -456,14 +456,16 @@ static inline int gconv_bn(int cout) { return cout <= 16 ? 16 : cout <= 32 ? 32 
 // barrier.  TH = BM / TW; patch PH x PW = ((TH - 1) sh + kh) x ((TW - 1) sw +
 // kw) pixels, dynamic LDS.  Accumulation runs chunk-major (all taps of chunk
 // 0, then chunk 1, ...).
-template <int WM, int WN, int MF, int NF>
+// TWC > 0: the tile width at compile time (divisions by it become shifts)
+template <int WM, int WN, int MF, int NF, int TWC = 0>
 __global__ __launch_bounds__(256) void gconv_x3p(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
                                                  const float* __restrict__ bias, float* __restrict__ out,
-                                                 ConvGeom g, int cout_pad, int act, float alpha, int TW, int tiles_w,
+                                                 ConvGeom g, int cout_pad, int act, float alpha, int TWr, int tiles_w,
                                                  const float* __restrict__ in_scale, const float* __restrict__ res) {
     static_assert(WM * WN == 4, "four waves");
     constexpr int BM = WM * MF * 16, BN = WN * NF * 16;
     extern __shared__ __attribute__((aligned(16))) uint16_t gsm[];
+    const int TW = TWC ? TWC : TWr;
     const int TH = BM / TW;
     const int PH = (TH - 1) * g.sh + g.kh, PW = (TW - 1) * g.sw + g.kw, NP = PH * PW;
     uint16_t* Ph = gsm;
@@ -524,41 +526,56 @@ __global__ __launch_bounds__(256) void gconv_x3p(const float* __restrict__ in, c
     for (int cc = 0; cc < ncc; ++cc) {
         load_b(cc, b0h, b0l);  // tap 0 of this chunk: in flight during the staging
         if (cc > 0) __syncthreads();  // every wave is done with the previous chunk's patch
-        // ---- stage the chunk: item = (patch pixel, 8-channel quad) ----
-        for (int it = t; it < NP * 4; it += 256) {
+        // ---- stage the chunk: item = (patch pixel, 8-channel quad); every
+        // item's loads issued before any is split (a patch of <= 341 pixels,
+        // the 64 KiB cap, is <= 6 items per thread), the patch coordinates by
+        // a float reciprocal (exact: (pix + 1/2) / PW stays >= 1/128 from an
+        // integer for PW <= 64) ----
+        constexpr int STG = 6;
+        const float inv_pw = 1.f / (float)PW;
+        float v[STG][8];
+        int pixs[STG];
+#pragma unroll
+        for (int u = 0; u < STG; ++u) {
+            const int it = t + 256 * u;
             const int pix = it >> 2, q = it & 3;
-            const int R = pix / PW, C = pix - (pix / PW) * PW;
+            pixs[u] = it < NP * 4 ? pix : -1;
+            const int R = (int)(((float)pix + 0.5f) * inv_pw), C = pix - R * PW;
             const int iy = iy0 + R, ix = ix0 + C;
-            const bool inside = iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
+            const bool inside = it < NP * 4 && iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
             const int c0 = cc * 32 + 8 * q;
             const float* px = img + ((size_t)(inside ? iy : 0) * g.Win + (inside ? ix : 0)) * g.Cin;
-            float v[8];
             if (inside && vec && c0 + 8 <= g.Cin) {
                 const float4 a = *reinterpret_cast<const float4*>(px + c0);
                 const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
-                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-                v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+                v[u][0] = a.x; v[u][1] = a.y; v[u][2] = a.z; v[u][3] = a.w;
+                v[u][4] = b.x; v[u][5] = b.y; v[u][6] = b.z; v[u][7] = b.w;
                 if (scl) {
                     const float4 sa = *reinterpret_cast<const float4*>(scl + c0);
                     const float4 sb = *reinterpret_cast<const float4*>(scl + c0 + 4);
-                    v[0] *= sa.x; v[1] *= sa.y; v[2] *= sa.z; v[3] *= sa.w;
-                    v[4] *= sb.x; v[5] *= sb.y; v[6] *= sb.z; v[7] *= sb.w;
+                    v[u][0] *= sa.x; v[u][1] *= sa.y; v[u][2] *= sa.z; v[u][3] *= sa.w;
+                    v[u][4] *= sb.x; v[u][5] *= sb.y; v[u][6] *= sb.z; v[u][7] *= sb.w;
                 }
             } else {
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const bool ok = inside && c0 + e < g.Cin;
-                    v[e] = ok ? (scl ? px[c0 + e] * scl[c0 + e] : px[c0 + e]) : 0.f;
+                    v[u][e] = ok ? (scl ? px[c0 + e] * scl[c0 + e] : px[c0 + e]) : 0.f;
                 }
             }
+        }
+#pragma unroll
+        for (int u = 0; u < STG; ++u) {
+            if (pixs[u] < 0) continue;
+            const int q = (t + 256 * u) & 3;
             gbf16x8 h, l;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                h[e] = (__bf16)v[e];
-                l[e] = (__bf16)(v[e] - (float)h[e]);
+                h[e] = (__bf16)v[u][e];
+                l[e] = (__bf16)(v[u][e] - (float)h[e]);
             }
-            *reinterpret_cast<gbf16x8*>(Ph + pix * GX_ROW + 8 * q) = h;
-            *reinterpret_cast<gbf16x8*>(Pl + pix * GX_ROW + 8 * q) = l;
+            *reinterpret_cast<gbf16x8*>(Ph + pixs[u] * GX_ROW + 8 * q) = h;
+            *reinterpret_cast<gbf16x8*>(Pl + pixs[u] * GX_ROW + 8 * q) = l;
         }
         __syncthreads();
         // ---- the chunk's taps, two per iteration (B slots alternate) ----
@@ -703,6 +720,61 @@ __global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restrict__ i
             }
         }
     }
+    float* o = out + ((size_t)n * g.Hout * g.Wout + P) * g.Cout;
+    if ((g.Cout & 3) == 0 && c0 + 32 <= g.Cout) {
+#pragma unroll
+        for (int c = 0; c < 32; c += 4)
+            *reinterpret_cast<float4*>(o + c0 + c) = make_float4(gact(acc[c], act, alpha), gact(acc[c + 1], act, alpha),
+                                                                 gact(acc[c + 2], act, alpha),
+                                                                 gact(acc[c + 3], act, alpha));
+    } else {
+#pragma unroll
+        for (int c = 0; c < 32; ++c)
+            if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], act, alpha);
+    }
+}
+
+// gconv_f32_s: the same conv for a compile-time KH x KW x CI (a 3-channel
+// stem) with the weights in the scalar data path: ws = [C_out / 32][K][32]
+// (zero-padded), read at wave-uniform addresses, so each FMA takes its weight
+// from an SGPR -- no LDS staging, no LDS reads (gconv_f32_lds spends a
+// ds_read_b128 per 4 FMAs).  The same chain per output as gconv_f32.
+template <int KH, int KW, int CI>
+__global__ __launch_bounds__(256) void gconv_f32_s(const float* __restrict__ in, const float* __restrict__ ws,
+                                                   const float* __restrict__ bias, float* __restrict__ out,
+                                                   ConvGeom g, int act, float alpha) {
+    constexpr int K = KH * KW * CI;
+    const int n = blockIdx.z;
+    const int c0 = blockIdx.y * 32;
+    const float* wq = ws + (size_t)blockIdx.y * K * 32;
+    const int P = blockIdx.x * 256 + threadIdx.x;
+    if (P >= g.Hout * g.Wout) return;
+    const int oy = P / g.Wout, ox = P - (P / g.Wout) * g.Wout;
+    const float* img = in + (size_t)n * g.Hin * g.Win * CI;
+    float xv[K];
+    bool ok[KH * KW];
+#pragma unroll
+    for (int ky = 0; ky < KH; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < KW; ++kx) {
+            const int iy = oy * g.sh - g.pt + ky, ix = ox * g.sw - g.pl + kx;
+            ok[ky * KW + kx] = iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
+            const int cy = min(max(iy, 0), g.Hin - 1), cx = min(max(ix, 0), g.Win - 1);
+            const float* px = img + ((size_t)cy * g.Win + cx) * CI;
+#pragma unroll
+            for (int ci = 0; ci < CI; ++ci) xv[(ky * KW + kx) * CI + ci] = px[ci];
+        }
+    float acc[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) acc[c] = c0 + c < g.Cout ? bias[c0 + c] : 0.f;
+#pragma unroll
+    for (int t = 0; t < KH * KW; ++t)
+        if (ok[t]) {
+#pragma unroll
+            for (int ci = 0; ci < CI; ++ci)
+#pragma unroll
+                for (int c = 0; c < 32; ++c) acc[c] = fmaf(wq[(t * CI + ci) * 32 + c], xv[t * CI + ci], acc[c]);
+        }
     float* o = out + ((size_t)n * g.Hout * g.Wout + P) * g.Cout;
     if ((g.Cout & 3) == 0 && c0 + 32 <= g.Cout) {
 #pragma unroll

@@ -346,6 +346,7 @@ struct GNode {
     void* d_w = nullptr;
     float* d_b = nullptr;
     float* d_b2 = nullptr;    // affine shift
+    float* d_ws = nullptr;    // f32 stem: weights [C_out / 32][K][32] for the scalar path (gconv_f32_s)
     size_t off = 0;           // workspace offset (f32 elements per window)
     // fusions (graph_build): a skipped node launches nothing; a conv may read
     // a squeeze-and-excite scale [n][Cin] (the Multiply it replaces) and add a
@@ -399,6 +400,7 @@ static void free_graph(Graph* g) {
         (void)hipFree(nd.d_w);
         (void)hipFree(nd.d_b);
         (void)hipFree(nd.d_b2);
+        (void)hipFree(nd.d_ws);
     }
     delete g;
 }
@@ -574,6 +576,14 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                     if ((rc = N.matvec == 2 ? gupload(&N.d_w, k, (size_t)K * N.C * 4)
                                             : gupload(&N.d_w, w_ohwc.data(), w_ohwc.size() * 4)) != AA_OK)
                         return rc;
+                    if (d.kh == 3 && d.kw == 3 && C == 3) {  // the scalar-path stem layout
+                        const int ng = (N.C + 31) / 32;
+                        std::vector<float> wsl((size_t)ng * K * 32, 0.f);
+                        for (int o = 0; o < N.C; ++o)
+                            for (int kk = 0; kk < K; ++kk)
+                                wsl[((size_t)(o / 32) * K + kk) * 32 + o % 32] = k[(size_t)kk * N.C + o];
+                        if ((rc = gupload((void**)&N.d_ws, wsl.data(), wsl.size() * 4)) != AA_OK) return rc;
+                    }
                     std::vector<float> bias(N.C, 0.f);
                     for (int o = 0; o < N.C; ++o) bias[o] = b ? b[o] : 0.f;
                     if ((rc = gupload((void**)&N.d_b, bias.data(), bias.size() * 4)) != AA_OK) return rc;
@@ -841,8 +851,9 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     const size_t lds = (size_t)((TH - 1) * d.sh + d.kh) * ((TW - 1) * d.sw + d.kw) * GX_ROW * 4;
                     const dim3 grid((unsigned)(tiles_w * tiles_h), N.cout_pad / N.bn, n);
                     if (N.bn == 16)
-                        hipLaunchKernelGGL((gconv_x3p<4, 1, 4, 1>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
-                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res);
+                        hipLaunchKernelGGL((gconv_x3p<4, 1, 4, 1, 16>), grid, dim3(256), lds, st, a,
+                                           (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w,
+                                           scl, res);
                     else if (N.bn == 32)
                         hipLaunchKernelGGL((gconv_x3p<4, 1, 2, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
                                            N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res);
@@ -906,7 +917,11 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                                    out, Cin, N.C, act, d.alpha);
             } else if (d.kh * d.kw * Cin <= GF32_KMAX) {
                 const dim3 grid((N.H * N.W + 255) / 256, (N.C + 31) / 32, n);
-                if (d.kh == 3 && d.kw == 3 && Cin == 3)  // an RGB-style stem
+                static const bool nosgpr = getenv("AA_GRAPH_NOSGPR") != nullptr;  // (A/B knob)
+                if (N.d_ws && !nosgpr)  // an RGB-style stem, weights through the scalar cache
+                    hipLaunchKernelGGL((gconv_f32_s<3, 3, 3>), grid, dim3(256), 0, st, a, (const float*)N.d_ws, N.d_b,
+                                       out, N.g, act, d.alpha);
+                else if (d.kh == 3 && d.kw == 3 && Cin == 3)
                     hipLaunchKernelGGL((gconv_f32_lds<3, 3, 3>), grid, dim3(256), 0, st, a, (const float*)N.d_w, N.d_b,
                                        out, N.g, act, d.alpha);
                 else if (d.kh == 3 && d.kw == 3 && Cin == 1)
