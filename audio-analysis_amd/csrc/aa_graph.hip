@@ -1104,19 +1104,25 @@ extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* l
             G->seen.push_back(Graph::Captured{x, n, workspace, logits, probs, st, nullptr});
             return graph_enqueue(G, x, n, logits, probs, ws, st);
         }
+        // capture; if the stream cannot be captured (the runtime refuses, or the
+        // caller's stream is itself capturing), launch node by node instead
         hipGraph_t hg = nullptr;
-        AA_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            (void)hipGetLastError();
+            return graph_enqueue(G, x, n, logits, probs, ws, st);
+        }
         const int rc = graph_enqueue(G, x, n, logits, probs, ws, st);
         const hipError_t ec = hipStreamEndCapture(st, &hg);
-        if (rc != AA_OK) {
-            if (hg) (void)hipGraphDestroy(hg);
-            return rc;
-        }
-        AA_HIP(ec);
         hipGraphExec_t exec = nullptr;
-        const hipError_t ei = hipGraphInstantiate(&exec, hg, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(hg);
-        AA_HIP(ei);
+        const hipError_t ei = (rc == AA_OK && ec == hipSuccess) ? hipGraphInstantiate(&exec, hg, nullptr, nullptr, 0)
+                                                                : hipErrorUnknown;
+        if (hg) (void)hipGraphDestroy(hg);
+        if (rc != AA_OK) return rc;  // a launch-configuration error: report it
+        if (ei != hipSuccess) {
+            (void)hipGetLastError();
+            // (nothing ran during the capture attempt)
+            return graph_enqueue(G, x, n, logits, probs, ws, st);
+        }
         if (G->captured.size() >= 16) {  // bounded: the oldest goes
             (void)hipGraphExecDestroy(G->captured.front().exec);
             G->captured.erase(G->captured.begin());
