@@ -78,6 +78,8 @@ struct SnPlan {
     bool colmed_bs = false;    // column medians by bit-serial search (AA_SN_COLMED=bs; A/B knob: 52 us against
                                // the LDS-histogram radix select's 44) or radix select
     int diag = 0;              // AA_SN_DIAG: ablation bits of sn_select_reg (tools only; results then invalid)
+    int stft_blocks = 1024;    // sn_stft64 grid (AA_SN_STFT_BLOCKS; A/B knob): 1024 = 4 resident blocks per
+                               // CU, persistent; more blocks leave the frame balance to the dispatcher
 };
 
 __device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
@@ -1560,7 +1562,7 @@ static int sn_components(SnPlan& p, const SnWs& ws, const SnBatch& nb, bool with
 // a multiple of 8 so every XCD owns an equal share of the blocks
 static int sn_launch_stft(SnPlan& p, const float* pcm, int64_t n, int F, float* S, int ld, unsigned* gmax,
                           hipStream_t st, unsigned* colmed = nullptr) {
-    int grid = std::min(F, 256 * 4);
+    int grid = std::min(F, p.stft_blocks);
     grid = (grid + 7) & ~7;
     const double2* tab = p.d_tab;
     hipEvent_t e0;
@@ -1692,6 +1694,7 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
     if (const char* e = std::getenv("AA_SN_SELECT")) p->select_reg = std::strcmp(e, "reg") == 0;
     if (const char* e = std::getenv("AA_SN_DIAG")) p->diag = std::atoi(e);
     if (const char* e = std::getenv("AA_SN_STFT")) p->stft_r8 = std::strcmp(e, "r8") == 0;
+    if (const char* e = std::getenv("AA_SN_STFT_BLOCKS")) p->stft_blocks = std::max(8, std::atoi(e));
     if (const char* e = std::getenv("AA_SN_COLMED")) {
         p->colmed_bs = std::strcmp(e, "bs") == 0;
         p->colmed_fused = std::strcmp(e, "fused") == 0;
