@@ -47,6 +47,29 @@ typedef __attribute__((ext_vector_type(4))) float gf32x4;
 
 constexpr int GX_ROW = 48;  // bf16 per LDS row: 32 + 16 B of padding (96 B)
 
+// The block's (x, y, z) tile coordinates.  xord = 0: the launch grid's.
+// xord = 1, XCD-aware order (as x3_block in aa_conv_x3.h): workgroup L (x
+// fastest) is dispatched to XCD L % 8, so XCD x is given the contiguous
+// logical range [x per, (x + 1) per) of an order with y (the channel blocks
+// of a pixel tile) fastest, then x, then z: a tile's pixels -- and its
+// neighbours' halo rows -- are read into one L2 once instead of once per
+// channel block on every XCD.  Each block's arithmetic is unchanged
+// (bit-identical results).
+__device__ __forceinline__ void xcd_order(int xord, int& bx, int& by, int& bz) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    bz = blockIdx.z;
+    if (!xord) return;
+    const int X = gridDim.x, Y = gridDim.y;
+    const int total = X * Y * (int)gridDim.z, per = total >> 3;
+    const int L = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+    const int lg = L < (per << 3) ? (L & 7) * per + (L >> 3) : L;
+    by = lg % Y;
+    const int rr = lg / Y;
+    bx = rr % X;
+    bz = rr / X;
+}
+
 // weights: [tap][cin_pad / 32][cout_pad][64] bf16, per row 32 hi then 32 lo.
 // Tile: BM = WM MF 16 output pixels x BN = WN NF 16 output channels, the four
 // waves WM x WN over it, each MF x NF fragments (64 x 64 by default; narrow
@@ -71,14 +94,17 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
                                                  const float* __restrict__ bias, float* __restrict__ out,
                                                  ConvGeom g, int cout_pad, int act, float alpha,
                                                  const float* __restrict__ in_scale, const float* __restrict__ res,
-                                                 int scale_hw = 0, int cslice = 0, float* __restrict__ part = nullptr) {
+                                                 int scale_hw = 0, int cslice = 0, float* __restrict__ part = nullptr,
+                                                 int xord = 0) {
     static_assert(WM * WN == 4, "four waves");
     constexpr int BM = WM * MF * 16, BN = WN * NF * 16, AI = BM / 64, BI = (BN + 63) / 64;
     constexpr int ROW = KC * 32 + 16;  // bf16 per LDS row (+32 B: conflict-free ds_read_b128 runs)
     __shared__ __attribute__((aligned(16))) uint16_t Ah[BM * ROW], Al[BM * ROW];
     __shared__ __attribute__((aligned(16))) uint16_t Bh[BN * ROW], Bl[BN * ROW];
-    const int n = part ? 0 : blockIdx.z;  // (split K: z is the slice)
-    const int pix0 = blockIdx.x * BM, ch0 = blockIdx.y * BN;
+    int bx, by, bz;
+    xcd_order(xord, bx, by, bz);
+    const int n = part ? 0 : bz;  // (split K: z is the slice)
+    const int pix0 = bx * BM, ch0 = by * BN;
     const int HWo = g.Hout * g.Wout;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave % WM, wn = wave / WM;
@@ -103,7 +129,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
     // split K (part != nullptr, flattened pointwise convs): blockIdx.z = slice
     // of cslice chunks, raw sums to part[slice][pixel][Cout] (gsplit_reduce
     // adds the slices in order, then bias, residual and activation)
-    const int cbase = part ? (int)blockIdx.z * cslice : 0;
+    const int cbase = part ? bz * cslice : 0;
     const int ngs = (part ? cslice : ncc) / KC;  // K steps per tap
     const int nsteps = g.kh * g.kw * ngs;
     gf32x4 acc[NF][MF];
@@ -221,7 +247,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
         for (int j = 0; j < MF; ++j) {
             const int Pj = pix0 + wm * MF * 16 + j * 16 + (lane & 15);
             if (Pj >= HWo) continue;
-            float* o = part + ((size_t)blockIdx.z * HWo + Pj) * g.Cout;
+            float* o = part + ((size_t)bz * HWo + Pj) * g.Cout;
 #pragma unroll
             for (int i = 0; i < NF; ++i) {
                 const int c = ch0 + wn * NF * 16 + i * 16 + 4 * (lane >> 4);
@@ -461,19 +487,22 @@ template <int WM, int WN, int MF, int NF, int TWC = 0>
 __global__ __launch_bounds__(256) void gconv_x3p(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
                                                  const float* __restrict__ bias, float* __restrict__ out,
                                                  ConvGeom g, int cout_pad, int act, float alpha, int TWr, int tiles_w,
-                                                 const float* __restrict__ in_scale, const float* __restrict__ res) {
+                                                 const float* __restrict__ in_scale, const float* __restrict__ res,
+                                                 int xord = 0) {
     static_assert(WM * WN == 4, "four waves");
     constexpr int BM = WM * MF * 16, BN = WN * NF * 16;
     extern __shared__ __attribute__((aligned(16))) uint16_t gsm[];
+    int bx, by, bz;
+    xcd_order(xord, bx, by, bz);
     const int TW = TWC ? TWC : TWr;
     const int TH = BM / TW;
     const int PH = (TH - 1) * g.sh + g.kh, PW = (TW - 1) * g.sw + g.kw, NP = PH * PW;
     uint16_t* Ph = gsm;
     uint16_t* Pl = gsm + NP * GX_ROW;
-    const int n = blockIdx.z;
-    const int ty = blockIdx.x / tiles_w, tx = blockIdx.x - (blockIdx.x / tiles_w) * tiles_w;
+    const int n = bz;
+    const int ty = bx / tiles_w, tx = bx - (bx / tiles_w) * tiles_w;
     const int oy0 = ty * TH, ox0 = tx * TW;
-    const int ch0 = blockIdx.y * BN;
+    const int ch0 = by * BN;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave % WM, wn = wave / WM;
     const int iy0 = oy0 * g.sh - g.pt, ix0 = ox0 * g.sw - g.pl;

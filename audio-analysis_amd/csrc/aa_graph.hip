@@ -787,6 +787,27 @@ static bool wide_n() {
     static const bool w = getenv("AA_GRAPH_NOWIDEN") == nullptr;
     return w;
 }
+// 64 x 128 tiles for kernels larger than 1x1 too (A/B knob AA_GRAPH_NOWIDEN3
+// turns it off: 3x3 32->128 160 -> 147 us alone, 139 us with the XCD order,
+// profiles/r04/graph_ab_xcd.txt)
+static bool wide_n3() {
+    static const bool w = getenv("AA_GRAPH_NOWIDEN3") == nullptr;
+    return w;
+}
+
+// channel quads per block of the depthwise conv + pool (A/B knob AA_GRAPH_DWQ:
+// 16 = 64 channels x 32 pixel stripes per 512-thread block, 8 = 32 channels
+// per 256-thread block; the per-channel stripe sums, and so the results, are
+// the same either way.  8: 45.0k -> 45.4k audio-s/s, stage sum unchanged --
+// the smaller blocks pack beside the other stream's kernels,
+// profiles/r04/graph_ab_dwq.txt)
+static int dw_q() {
+    static const int q = [] {
+        const char* e = getenv("AA_GRAPH_DWQ");
+        return e && std::atoi(e) == 16 ? 16 : 8;
+    }();
+    return q;
+}
 
 static int graph_run_node(const Graph& G, const GNode& N, const float* x, float* ws, int n, hipStream_t st) {
     const aa_node& d = N.d;
@@ -816,6 +837,12 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     nz = 1;
                     scale_hw = N.H * N.W;
                 }
+                // XCD-aware block order (aa_gconv.h xcd_order; AA_GRAPH_XCD=0 turns it off:
+                // stage sum 3016 -> 2923 us, profiles/r04/graph_ab_xcd.txt)
+                static const int xo = [] {
+                    const char* e = getenv("AA_GRAPH_XCD");
+                    return e ? atoi(e) : 1;
+                }();
                 const float* scl = N.scale_src >= 0 ? buf(N.scale_src) : nullptr;
                 const float* res = N.res_src >= 0 ? buf(N.res_src) : nullptr;
                 const int HWo = g.Hout * g.Wout;
@@ -827,8 +854,10 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                 // stall the short tap loop: gconv_x3t keeps those.)
                 int BM = 0, TW = 0;
                 static const bool nopatch = getenv("AA_GRAPH_NOPATCH") != nullptr;  // (A/B knob)
+                // (A/B knob AA_GRAPH_P128: 128-pixel tiles, 8 x 16, for more blocks per CU)
+                static const bool p128 = getenv("AA_GRAPH_P128") != nullptr;
                 if (d.kh * d.kw > 1 && N.bn == 16 && !nopatch) {
-                    BM = 256;
+                    BM = p128 ? 128 : 256;
                     TW = BM == 64 ? 8 : 16;
                     const int TH = BM / TW;
                     const size_t lds = (size_t)((TH - 1) * d.sh + d.kh) * ((TW - 1) * d.sw + d.kw) * GX_ROW * 4;
@@ -850,46 +879,50 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     const int tiles_w = (N.W + TW - 1) / TW, tiles_h = (N.H + TH - 1) / TH;
                     const size_t lds = (size_t)((TH - 1) * d.sh + d.kh) * ((TW - 1) * d.sw + d.kw) * GX_ROW * 4;
                     const dim3 grid((unsigned)(tiles_w * tiles_h), N.cout_pad / N.bn, n);
-                    if (N.bn == 16)
+                    if (N.bn == 16 && BM == 128)
+                        hipLaunchKernelGGL((gconv_x3p<4, 1, 2, 1, 16>), grid, dim3(256), lds, st, a,
+                                           (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w,
+                                           scl, res, xo);
+                    else if (N.bn == 16)
                         hipLaunchKernelGGL((gconv_x3p<4, 1, 4, 1, 16>), grid, dim3(256), lds, st, a,
                                            (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w,
-                                           scl, res);
+                                           scl, res, xo);
                     else if (N.bn == 32)
                         hipLaunchKernelGGL((gconv_x3p<4, 1, 2, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
-                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res);
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res, xo);
                     else if (BM == 128)
                         hipLaunchKernelGGL((gconv_x3p<2, 2, 4, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
-                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res);
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res, xo);
                     else
                         hipLaunchKernelGGL((gconv_x3p<2, 2, 2, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
-                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res);
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res, xo);
                 } else if (N.bn == 16)
                     hipLaunchKernelGGL((gconv_x3t<4, 1, 4, 1>), dim3((HWo + 255) / 256, N.cout_pad / 16, nz), dim3(256),
                                        0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res, scale_hw);
+                                       res, scale_hw, 0, nullptr, xo);
                 else if (N.bn == 32)
                     hipLaunchKernelGGL((gconv_x3t<4, 1, 2, 2>), dim3((HWo + 127) / 128, N.cout_pad / 32, nz), dim3(256),
                                        0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res, scale_hw);
-                else if (wide_n() && d.kh * d.kw == 1 && N.C >= 128 && N.g.cin_pad <= 256 && N.cout_pad % 128 == 0)
+                                       res, scale_hw, 0, nullptr, xo);
+                else if (wide_n() && (d.kh * d.kw == 1 || wide_n3()) && N.C >= 128 && N.g.cin_pad <= 256 && N.cout_pad % 128 == 0)
                     // 64 x 128 tiles: half the re-reads of the pixel tile
                     hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 4>), dim3((HWo + 63) / 64, N.cout_pad / 128, nz), dim3(256),
                                        0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res, scale_hw);
+                                       res, scale_hw, 0, nullptr, xo);
                 else if (wide_tile(d.kh * d.kw > 1))
                     hipLaunchKernelGGL((gconv_x3t<2, 2, 4, 2>), dim3((HWo + 127) / 128, N.cout_pad / 64, nz), dim3(256),
                                        0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res, scale_hw);
+                                       res, scale_hw, 0, nullptr, xo);
                 else if (N.split > 1 && nz == 1) {
                     // split K: slices of cslice chunks on blockIdx.z, then the ordered sum
                     float* part = ws + G.part_off * (size_t)n;
                     const dim3 grid((HWo + 63) / 64, N.cout_pad / 64, N.split);
                     if (N.cslice % 2 == 0 && kc_max() >= 2)
                         hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 2>), grid, dim3(256), 0, st, a, (const uint16_t*)N.d_w,
-                                           N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, N.cslice, part);
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, N.cslice, part, xo);
                     else
                         hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 1>), grid, dim3(256), 0, st, a, (const uint16_t*)N.d_w,
-                                           N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, N.cslice, part);
+                                           N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, N.cslice, part, xo);
                     AA_LAUNCH_CHECK();
                     const size_t total = (size_t)HWo * N.C;
                     hipLaunchKernelGGL(gsplit_reduce, dim3((unsigned)((total / 4 + 255) / 256 + 1)), dim3(256), 0, st, part,
@@ -902,7 +935,7 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                                    : ncc % 2 == 0 && kmax >= 2 ? 2 : 1;
 #define AA_GX(K_)                                                                                                   \
     hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, K_>), dim3((HWo + 63) / 64, N.cout_pad / 64, nz), dim3(256), 0, st, a, \
-                       (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw)
+                       (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, 0, nullptr, xo)
                     if (KC == 4) AA_GX(4);
                     else if (KC == 3) AA_GX(3);
                     else if (KC == 2) AA_GX(2);
@@ -940,12 +973,16 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                 const GNode& P = G.nodes[N.pool_into];
                 float* pooled = ws + P.off * (size_t)n;
                 if ((Cin & 3) == 0) {
-#define AA_DWP(KS)                                                                                             \
-    hipLaunchKernelGGL((gdwconv_pool4<16, KS>), dim3((Cin + 63) / 64, n), dim3(16 * GP4_STRIPES), 0, st, a,     \
-                       (const float*)N.d_w, N.d_b, out, pooled, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw, d.pt, \
-                       d.pl, act, d.alpha, P.d.act, P.d.alpha)
-                    if (d.kh == 3 && d.kw == 3) AA_DWP(3);
-                    else AA_DWP(0);
+#define AA_DWP(Q, KS)                                                                                          \
+    hipLaunchKernelGGL((gdwconv_pool4<Q, KS>), dim3((Cin + 4 * Q - 1) / (4 * Q), n), dim3(Q * GP4_STRIPES), 0, st, \
+                       a, (const float*)N.d_w, N.d_b, out, pooled, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw,  \
+                       d.pt, d.pl, act, d.alpha, P.d.act, P.d.alpha)
+                    const bool k3 = d.kh == 3 && d.kw == 3;
+                    if (dw_q() == 8) {
+                        if (k3) AA_DWP(8, 3);
+                        else AA_DWP(8, 0);
+                    } else if (k3) AA_DWP(16, 3);
+                    else AA_DWP(16, 0);
 #undef AA_DWP
                 } else {
                     hipLaunchKernelGGL(gdwconv_pool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a,
