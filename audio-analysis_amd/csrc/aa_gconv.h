@@ -24,12 +24,28 @@ namespace aa {
 
 enum GAct { GACT_NONE = 0, GACT_RELU = 1, GACT_LEAKY = 2, GACT_SIGMOID = 3, GACT_SWISH = 4 };
 
+// The logistic of sigmoid / swish as v_exp_f32 (2^x) and v_rcp_f32, each
+// within 1 ulp: 3 VALU instead of expf's range reduction and the IEEE
+// division's scale / fixup sequence (~25), which made the epilogues of the
+// graph's expand convs VALU-bound (112 -> 672: 21 VALU per MFMA).  Keras'
+// own logistic (Eigen's rational approximation on the CPU) is no closer to
+// the exact value than this.  Large -v: 2^x = inf, rcp(inf) = 0.
+#ifndef AA_GACT_FAST
+#define AA_GACT_FAST 1
+#endif
+__device__ __forceinline__ float glogistic(float v) {
+#if AA_GACT_FAST
+    return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(v * -1.44269504088896341f));
+#else
+    return 1.f / (1.f + expf(-v));
+#endif
+}
 __device__ __forceinline__ float gact(float v, int act, float alpha) {
     switch (act) {
         case GACT_RELU: return fmaxf(v, 0.f);
         case GACT_LEAKY: return v >= 0.f ? v : v * alpha;
-        case GACT_SIGMOID: return 1.f / (1.f + expf(-v));
-        case GACT_SWISH: return v * (1.f / (1.f + expf(-v)));
+        case GACT_SIGMOID: return glogistic(v);
+        case GACT_SWISH: return v * glogistic(v);
         default: return v;
     }
 }
@@ -146,9 +162,18 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
         for (int k = 0; k < KC; ++k) wh[ib][k] = wl[ib][k] = make_uint4(0, 0, 0, 0);
     // step s = (tap, chunks KC gs .. KC gs + KC - 1): this thread's 8 channels
     // of AI pixels per chunk and its 8 hi + 8 lo weights per chunk
-    auto load = [&](int s) {
-        const int tap = s / ngs, gs = s - (s / ngs) * ngs;
-        const int ky = tap / g.kw, kx = tap - (tap / g.kw) * g.kw;
+    // the coordinates (kernel row, column, chunk group) of the next step to
+    // load, stepped on by one per load (no integer divisions per step)
+    int l_ky = 0, l_kx = 0, l_gs = 0;
+    auto load = [&]() {
+        const int ky = l_ky, kx = l_kx, gs = l_gs, tap = ky * g.kw + kx;
+        if (++l_gs == ngs) {
+            l_gs = 0;
+            if (++l_kx == g.kw) {
+                l_kx = 0;
+                ++l_ky;
+            }
+        }
 #pragma unroll
         for (int it = 0; it < AI; ++it) {
             const int iy = oy[it] * g.sh - g.pt + ky, ix = ox[it] * g.sw - g.pl + kx;
@@ -190,7 +215,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             }
         }
     };
-    load(0);
+    load();
     for (int s = 0; s < nsteps; ++s) {
         gbf16x8 h[AI][KC], l[AI][KC];
 #pragma unroll
@@ -220,7 +245,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             }
         }
         __syncthreads();
-        if (s + 1 < nsteps) load(s + 1);
+        if (s + 1 < nsteps) load();
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
             const int ko = 32 * k + 8 * (lane >> 4);
@@ -260,6 +285,18 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
         }
         return;
     }
+    float bv[NF][4];  // the lane's channels' biases, the same for every pixel fragment
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const int c = ch0 + wn * NF * 16 + i * 16 + 4 * (lane >> 4);
+        if (c + 4 <= g.Cout && (g.Cout & 3) == 0) {
+            const float4 b4 = *reinterpret_cast<const float4*>(bias + c);
+            bv[i][0] = b4.x; bv[i][1] = b4.y; bv[i][2] = b4.z; bv[i][3] = b4.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bv[i][e] = c + e < g.Cout ? bias[c + e] : 0.f;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < MF; ++j) {
         const int Pj = pix0 + wm * MF * 16 + j * 16 + (lane & 15);
@@ -272,7 +309,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             float y[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                float z = acc[i][j][e] + (c + e < g.Cout ? bias[c + e] : 0.f);
+                float z = acc[i][j][e] + bv[i][e];
                 if (rp && c + e < g.Cout) z += rp[c + e];
                 y[e] = gact(z, act, alpha);
             }

@@ -204,8 +204,10 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
             for (int t = 0; t < NW; ++t) wr[t] = *reinterpret_cast<const float4*>(w + t * C + c);
         }
         const int KH = KS ? KS : kh, KW = KS ? KS : kw;
+        // the pixel's (row, column), stepped on by the stripe count (no
+        // integer division per pixel)
+        int oy = s / Wout, ox = s - (s / Wout) * Wout;
         for (int P = s; P < HW; P += GP4_STRIPES) {
-            const int oy = P / Wout, ox = P - (P / Wout) * Wout;
             float4 acc = b;
 #pragma unroll
             for (int ky = 0; ky < KH; ++ky) {
@@ -229,6 +231,11 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
                                          gact(acc.w, act, alpha));
             *reinterpret_cast<float4*>(o + (size_t)P * C) = y;
             m.x += y.x; m.y += y.y; m.z += y.z; m.w += y.w;
+            ox += GP4_STRIPES;
+            while (ox >= Wout) {
+                ox -= Wout;
+                ++oy;
+            }
         }
     }
     part[s][4 * cq] = m.x; part[s][4 * cq + 1] = m.y; part[s][4 * cq + 2] = m.z; part[s][4 * cq + 3] = m.w;
