@@ -10,8 +10,8 @@
 // (zero outside the image), splits them into bf16 hi / lo in LDS next to the
 // step's pre-split weight slice, and each wave (2 x 2 over the tile) runs
 // 2 x 2 fragments x 3 MFMAs (hi*hi + lo*hi + hi*lo, f32 accumulation, as
-// conv_x3).  LDS rows are 96 B (32 bf16 + 16 B), which makes the 16-lane
-// ds_read_b128 fragment reads conflict-free.  Fused epilogue: bias,
+// conv_x3).  LDS rows are 96 B (32 bf16 + 16 B; per KC chunk 64 B more).
+// Fused epilogue: bias,
 // activation, NHWC f32 store (4 channels per lane).
 //
 // gconv_f32: the same geometry in exact f32 FMA chains (VALU), for C_in < 16
@@ -61,7 +61,16 @@ struct ConvGeom {
 typedef __attribute__((ext_vector_type(8))) __bf16 gbf16x8;
 typedef __attribute__((ext_vector_type(4))) float gf32x4;
 
-constexpr int GX_ROW = 48;  // bf16 per LDS row: 32 + 16 B of padding (96 B)
+// LDS rows of the patch-staged convs (gconv_x3p / gconv_x3q): 32 bf16 +
+// GX_PAD.  8 (80 B rows, an odd multiple of 16 B, so the 16 rows of a
+// fragment read sit on distinct banks) instead of round 4's 16 (96 B): the
+// 3x3 32->16 patch kernel 125 -> 107 us -- the smaller patch (52 KiB) also
+// fits three blocks per CU instead of two (profiles/r04/graph_ab_pad.txt).
+#ifndef AA_GX_PAD
+#define AA_GX_PAD 8
+#endif
+constexpr int GX_PAD = AA_GX_PAD;
+constexpr int GX_ROW = 32 + GX_PAD;  // bf16 per LDS row (80 B)
 
 // The block's (x, y, z) tile coordinates.  xord = 0: the launch grid's.
 // xord = 1, XCD-aware order (as x3_block in aa_conv_x3.h): workgroup L (x
@@ -114,7 +123,10 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
                                                  int xord = 0) {
     static_assert(WM * WN == 4, "four waves");
     constexpr int BM = WM * MF * 16, BN = WN * NF * 16, AI = BM / 64, BI = (BN + 63) / 64;
-    constexpr int ROW = KC * 32 + 16;  // bf16 per LDS row (+32 B: conflict-free ds_read_b128 runs)
+    // bf16 per LDS row: +32 B (the odd-multiple-of-16-B stride of GX_ROW
+    // measured slower here: 3x3 48->192 96 -> 102 us, 16->64 81 -> 85 us,
+    // 32->128 unchanged; profiles/r04/graph_ab_pad.txt)
+    constexpr int ROW = KC * 32 + 16;
     __shared__ __attribute__((aligned(16))) uint16_t Ah[BM * ROW], Al[BM * ROW];
     __shared__ __attribute__((aligned(16))) uint16_t Bh[BN * ROW], Bl[BN * ROW];
     int bx, by, bz;
@@ -571,11 +583,15 @@ __global__ __launch_bounds__(256) void gconv_x3p(const float* __restrict__ in, c
             l[i] = *reinterpret_cast<const gbf16x8*>(wrow + 32);
         }
     };
+    int tky = 0, tkx = 0;  // the tap's kernel row / column, stepped on per tap (no divisions)
     auto tap_step = [&](int tap, int cc, const gbf16x8 (&h)[NF], const gbf16x8 (&l)[NF], gbf16x8 (&nh)[NF],
                         gbf16x8 (&nl)[NF]) {
         if (tap + 1 < ntap) load_b((tap + 1) * ncc + cc, nh, nl);
-        const int ky = tap / g.kw, kx = tap - (tap / g.kw) * g.kw;
-        const int toff = ky * PW + kx;
+        const int toff = tky * PW + tkx;
+        if (++tkx == g.kw) {
+            tkx = 0;
+            ++tky;
+        }
 #pragma unroll
         for (int j = 0; j < MF; ++j) {
             const int xr = (pb[j] + toff) * GX_ROW + ko;
@@ -645,6 +661,7 @@ __global__ __launch_bounds__(256) void gconv_x3p(const float* __restrict__ in, c
         }
         __syncthreads();
         // ---- the chunk's taps, two per iteration (B slots alternate) ----
+        tky = tkx = 0;
         for (int tap = 0; tap < ntap; tap += 2) {
             tap_step(tap, cc, b0h, b0l, b1h, b1l);
             if (tap + 1 < ntap) tap_step(tap + 1, cc, b1h, b1l, b0h, b0l);
