@@ -240,7 +240,10 @@ class StageTiming:
         (graphs: one stage, or every one)."""
         if self._timing_prefix == "aa_graph" and on and stages is not None:
             st = list(stages)
-            check(lib().aa_graph_time_stage(self._h, int(st[0]) if len(st) == 1 else -1), "aa_graph_time_stage")
+            if len(st) != 1:
+                raise ValueError("graph models time one node or every node (stages=None), "
+                                 f"not a subset of {len(st)}")
+            check(lib().aa_graph_time_stage(self._h, int(st[0])), "aa_graph_time_stage")
             return
         mask = 0
         if on:

@@ -519,6 +519,16 @@ static __global__ __launch_bounds__(256) void gsplit_reduce(const float* __restr
     }
 }
 
+// gconv_x3p stages a chunk as (pixel, 8-channel quad) items, GX_P_STG per
+// thread of its 256: patches of more than GX_P_STG * 64 pixels would leave
+// pixels unwritten, so the host checks gconv_x3p_fits (patch pixels and the
+// 64 KiB LDS cap) before it picks that kernel.
+constexpr int GX_P_STG = 6;
+static inline bool gconv_x3p_fits(int ph, int pw) {
+    const long np = (long)ph * pw;
+    return np * 4 <= (long)GX_P_STG * 256 && np * GX_ROW * 4 <= 65536;
+}
+
 // tile of a layer with C_out output channels: BN = 16, 32 or 64
 static inline int gconv_bn(int cout) { return cout <= 16 ? 16 : cout <= 32 ? 32 : 64; }
 
@@ -609,11 +619,12 @@ __global__ __launch_bounds__(256) void gconv_x3p(const float* __restrict__ in, c
         load_b(cc, b0h, b0l);  // tap 0 of this chunk: in flight during the staging
         if (cc > 0) __syncthreads();  // every wave is done with the previous chunk's patch
         // ---- stage the chunk: item = (patch pixel, 8-channel quad); every
-        // item's loads issued before any is split (a patch of <= 341 pixels,
-        // the 64 KiB cap, is <= 6 items per thread), the patch coordinates by
+        // item's loads issued before any is split (GX_P_STG items per thread:
+        // the host launches this kernel only for patches of <= GX_P_STG * 64
+        // pixels, gconv_x3p_fits), the patch coordinates by
         // a float reciprocal (exact: (pix + 1/2) / PW stays >= 1/128 from an
         // integer for PW <= 64) ----
-        constexpr int STG = 6;
+        constexpr int STG = GX_P_STG;
         const float inv_pw = 1.f / (float)PW;
         float v[STG][8];
         int pixs[STG];

@@ -392,6 +392,7 @@ struct Graph {
         float* probs;
         hipStream_t st;
         hipGraphExec_t exec;
+        hipEvent_t done;  // recorded after every launch of exec: it may still run when evicted
     };
     std::vector<Captured> captured;
     std::vector<Captured> seen;  // keys met once (captured the second time: a caller
@@ -399,9 +400,23 @@ struct Graph {
     std::mutex cap_mu;
 };
 
+constexpr size_t AA_GRAPH_CAPTURES = 16;  // captured forwards kept per graph
+
+// an instantiated forward that may still be executing from its last launch:
+// wait for that launch before the executable goes
+static void release_captured(Graph::Captured& c) {
+    if (c.done) {
+        (void)hipEventSynchronize(c.done);
+        (void)hipEventDestroy(c.done);
+    }
+    if (c.exec) (void)hipGraphExecDestroy(c.exec);
+    c.done = nullptr;
+    c.exec = nullptr;
+}
+
 static void free_graph(Graph* g) {
     if (!g) return;
-    for (auto& c : g->captured) (void)hipGraphExecDestroy(c.exec);
+    for (auto& c : g->captured) release_captured(c);
     g->timer.release();
     for (auto& nd : g->nodes) {
         (void)hipFree(nd.d_w);
@@ -867,8 +882,9 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     BM = p128 ? 128 : 256;
                     TW = BM == 64 ? 8 : 16;
                     const int TH = BM / TW;
-                    const size_t lds = (size_t)((TH - 1) * d.sh + d.kh) * ((TW - 1) * d.sw + d.kw) * GX_ROW * 4;
-                    if (lds > 65536) BM = 0;
+                    // every patch pixel staged (GX_P_STG items per thread) and the
+                    // patch within 64 KiB; otherwise gconv_x3t
+                    if (!gconv_x3p_fits((TH - 1) * d.sh + d.kh, (TW - 1) * d.sw + d.kw)) BM = 0;
                 }
                 // (A/B knob AA_GRAPH_Q=1: measured slower -- 3x3 32->128 161 -> 197 us,
                 // 48->192 118 -> 148 us: two waves per SIMD wait out a barrier per tap)
@@ -1134,6 +1150,7 @@ extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* l
         for (const auto& c : G->captured)
             if (same(c)) {
                 AA_HIP(hipGraphLaunch(c.exec, st));
+                AA_HIP(hipEventRecord(c.done, st));
                 return AA_OK;
             }
         bool again = false;
@@ -1144,8 +1161,8 @@ extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* l
                 break;
             }
         if (!again) {
-            if (G->seen.size() >= 16) G->seen.erase(G->seen.begin());
-            G->seen.push_back(Graph::Captured{x, n, workspace, logits, probs, st, nullptr});
+            if (G->seen.size() >= AA_GRAPH_CAPTURES) G->seen.erase(G->seen.begin());
+            G->seen.push_back(Graph::Captured{x, n, workspace, logits, probs, st, nullptr, nullptr});
             return graph_enqueue(G, x, n, logits, probs, ws, st);
         }
         // capture; if the stream cannot be captured (the runtime refuses, or the
@@ -1167,12 +1184,19 @@ extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* l
             // (nothing ran during the capture attempt)
             return graph_enqueue(G, x, n, logits, probs, ws, st);
         }
-        if (G->captured.size() >= 16) {  // bounded: the oldest goes
-            (void)hipGraphExecDestroy(G->captured.front().exec);
+        hipEvent_t done = nullptr;
+        if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipGraphExecDestroy(exec);
+            return graph_enqueue(G, x, n, logits, probs, ws, st);
+        }
+        if (G->captured.size() >= AA_GRAPH_CAPTURES) {  // bounded: the oldest goes
+            release_captured(G->captured.front());
             G->captured.erase(G->captured.begin());
         }
-        G->captured.push_back(Graph::Captured{x, n, workspace, logits, probs, st, exec});
+        G->captured.push_back(Graph::Captured{x, n, workspace, logits, probs, st, exec, done});
         AA_HIP(hipGraphLaunch(exec, st));
+        AA_HIP(hipEventRecord(done, st));
         return AA_OK;
     }
     for (int32_t c0 = 0; c0 < n; c0 += CHUNK) {

@@ -1607,7 +1607,8 @@ static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const i
         unsigned* colmed = sn_at(ws.colmed, ws.pf, k);
         float* c3 = sn_at(ws.c3, ws.pf, k);
         unsigned long long* M0 = sn_at(ws.M0, ws.pf, k);
-        // column medians inside sn_stft64 (default) or as their own launch
+        // column medians as their own sn_colmed launch (default), or inside
+        // sn_stft64 with AA_SN_COLMED=fused
         const bool fused = p->colmed_fused && !p->stft_r8 && !p->colmed_bs;
         int rc = sn_launch_stft(*p, lens[k] ? pcm + offs[k] : pcm, lens[k], F, ws.S, kSnLd, gmax, st,
                                 fused ? colmed : nullptr);

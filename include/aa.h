@@ -330,7 +330,7 @@ int aa_sn_run_batch(void* plan, const float* pcm, const int64_t* offsets, const 
  * = frame f's 2049 bins.  No workspace. */
 int aa_sn_spectrogram(void* plan, const float* pcm, int64_t n_samples, float* out, int64_t ld, void* stream);
 /* Launch stages of aa_sn_run / aa_sn_run_batch (0 sn_stft64, 1 sn_transpose,
- * 2 sn_select, 3 sn_morph, 4 the component launches) and their timing, the
+ * 2 sn_select, 3 sn_morph, 4 the component launches, 5 sn_colmed) and their timing, the
  * aa_fe_stage_* contract; an item is one STFT frame of one recording. */
 int aa_sn_n_stages(const void* plan);
 int aa_sn_stage_info(const void* plan, int32_t stage, char* name, int32_t name_len, double* flops_per_item,

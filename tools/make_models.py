@@ -411,7 +411,7 @@ def _graph_weights(arch, in_ch, rng):
 
 
 def make_graph(out_dir, kind="effnet", name=None, seed=1, in_channels=1, n_mels=160, T=226, labels=None,
-               meta_overrides=None, calib=None):
+               meta_overrides=None, calib=None, arch=None):
     """A graph model (graph_arch) with seeded weights, BatchNormalization
     statistics calibrated layer by layer on dB-like inputs (float64, through
     the oracle's graph semantics) and centred logits; writes
@@ -420,12 +420,13 @@ def make_graph(out_dir, kind="effnet", name=None, seed=1, in_channels=1, n_mels=
     the model will see) replaces the synthetic dB-like calibration input: a
     deep network whose statistics were taken on another input distribution
     amplifies its activations layer after layer (logits in the thousands),
-    which no trained network does."""
+    which no trained network does.  ``arch`` (a graph_arch-style layer list
+    ending in a Dense) replaces the named ``kind``."""
     import torch
     from safetensors.numpy import save_file
     from oracle.cnn_oracle import _forward_graph
     labels = list(labels or LABELS)
-    arch = graph_arch(kind, len(labels))
+    arch = arch if arch is not None else graph_arch(kind, len(labels))
     rng = np.random.default_rng(seed)
     tensors = _graph_weights(arch, in_channels, rng)
     # (BatchNorm statistics are per channel: a deep network calibrates on a
