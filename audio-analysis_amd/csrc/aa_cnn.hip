@@ -1121,7 +1121,8 @@ struct Stage {
     int lm_f16 = 0;       // fused_first: the model input is float16
     int in_split = 0;     // split-bf16: input / output in the grouped-split layout (aa_conv_x3.h)
     int out_split = 0;
-    int wg = 0;           // split-bf16 Winograd F(2,3)-along-W kernel (aa_conv_wg.h) and its weight packing
+    int wg = 0;           // split-bf16 Winograd F(wg, 3)-along-W kernel (aa_conv_wg.h, wg = WO) and its weight packing
+    int wg_npass = 1;     // its staging passes (planes per pass = (wg + 2) / wg_npass)
     int cin_pad = 0;      // ST_GCONV: C_in rounded up to 32
     int tail = 0;         // ST_HEAD, split-bf16: computes the previous conv stage itself (aa_conv_tail.h)
     void* d_tw = nullptr;  // tail: head weights packed per wave / label fragment, hi then lo
@@ -1202,10 +1203,11 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
     X(1, 3, 128, 1, 2, 2, 3, 2, 7, 12, 1, 1, 0)
 #endif
 
-// conv_wg (split-bf16, Winograd F(2,3) along W) instantiations: (kh, C_in,
+// conv_wg (split-bf16, Winograd F(WO,3) along W) instantiations: (kh, C_in,
 // pool) of kernel-width-3 convs -> waves (WM x WN), fragments per wave (MF x
-// NF, each with 4 accumulator sets), output tile TH x TW (TW even), pinned
-// waves per SIMD (0: free).  Preferred over conv_x3 where a row exists (the
+// NF, each with WO + 2 accumulator sets), output tile TH x TW (TW a multiple
+// of WO), pinned waves per SIMD (0: free), outputs per group WO, staging
+// passes NPASS.  Preferred over conv_x3 where a row exists (the
 // fused first-layer stage always runs conv_x3).  In-pipeline A/B (tools/ab.sh,
 // same box): the 9x3 layer 187 -> 160 us, step 180k -> 193k audio-s/s; the
 // small 3x3 / 1x3 layers lose on it (their transform-heavy staging outweighs
@@ -1213,15 +1215,28 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
 #ifdef AA_WG_ALT
 #define AA_WG_CFGS(X) AA_WG_ALT(X)
 #else
-#define AA_WG_CFGS(X) X(9, 64, 3, 2, 2, 4, 2, 39, 6, 2)
+// F(6,3) for the 9x3 layer (in-pipeline A/B, 3 rounds on one box: 9x3 131 ->
+// 122 us, step 260k -> 264k; F(4,3) on 39x12 tiles 140 us, F(3,3) spills):
+// 8 planes of the 39 x 6 tile's single column group, 4 waves of 16 output
+// channels each, 96 accumulator VGPRs
+#define AA_WG_CFGS(X) X(9, 64, 3, 1, 4, 3, 1, 39, 6, 2, 6, 1)
 #endif
 
 static int wg_bn(int kh, int kw, int cin, int pool) {
-#define AA_WBN(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC) \
+#define AA_WBN(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS) \
     if (kw == 3 && kh == KH && cin == CIN && pool == POOL) return WN * NF * 16;
     AA_WG_CFGS(AA_WBN)
 #undef AA_WBN
     return 0;
+}
+// (WO, NPASS) of the Winograd instantiation serving a stage
+static void wg_form(int kh, int cin, int pool, int* wo, int* npass) {
+#define AA_WFORM(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS) \
+    if (kh == KH && cin == CIN && pool == POOL) { *wo = WO; *npass = NPASS; return; }
+    AA_WG_CFGS(AA_WFORM)
+#undef AA_WFORM
+    *wo = 0;
+    *npass = 1;
 }
 
 template <typename T>
@@ -1273,14 +1288,14 @@ static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream
     return AA_OK;
 }
 
-template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int OCC, bool IN_SPLIT,
-          bool OUT_SPLIT>
+template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int OCC, int WO, int NPASS,
+          bool IN_SPLIT, bool OUT_SPLIT>
 static int launch_wg(const Stage& s, const void* in, void* out, int n, hipStream_t st) {
-    auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IN_SPLIT, OUT_SPLIT>;
+    auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IN_SPLIT, OUT_SPLIT, 0, WO, NPASS>;
     constexpr int BN = WN * NF * 16;
     AA_CHECK((double)s.Hin * s.Win * s.cin * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
              "conv %s: one window's activations exceed 2 GiB", s.name.c_str());
-    const size_t lds = wg_lds_bytes<KH, BN, TH, TW>();
+    const size_t lds = wg_lds_bytes<KH, BN, TH, TW, WO, NPASS>();
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
     AA_DYN_LDS(k, lds);
     const int tiles_h = (s.Hout * POOL + TH - 1) / TH;
@@ -1401,13 +1416,13 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
     }
     if constexpr (is_split<T>()) {
         if (s.wg) {
-#define AA_LAUNCHW(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC)                                                   \
+#define AA_LAUNCHW(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS)                                       \
             if (s.kh == KH && s.cin == CIN && s.pool == POOL) {                                                   \
                 if (s.in_split)                                                                                   \
-                    return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, true, true>(s, in, out, n, st) \
-                                       : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, true, false>(s, in, out, n, st); \
-                return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, false, true>(s, in, out, n, st) \
-                                   : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, false, false>(s, in, out, n, st); \
+                    return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, true, true>(s, in, out, n, st) \
+                                       : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, true, false>(s, in, out, n, st); \
+                return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, false, true>(s, in, out, n, st) \
+                                   : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, false, false>(s, in, out, n, st); \
             }
             AA_WG_CFGS(AA_LAUNCHW)
 #undef AA_LAUNCHW
@@ -1711,7 +1726,9 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             C = s.cout;
             continue;
         }
-        s.wg = precision == AA_PREC_BF16X3 && s.kind == ST_MFMA && wg_bn(s.kh, s.kw, s.cin, s.pool) > 0;
+        s.wg = 0;
+        if (precision == AA_PREC_BF16X3 && s.kind == ST_MFMA && wg_bn(s.kh, s.kw, s.cin, s.pool) > 0)
+            wg_form(s.kh, s.cin, s.pool, &s.wg, &s.wg_npass);
         const bool rowmajor = s.kind == ST_SMALL || s.kind == ST_GENERIC;  // f32 [cout][K]
         s.cout_pad = rowmajor ? s.cout : (s.cout + bn_tile - 1) / bn_tile * bn_tile;
         // pack weights with the BN scale folded in: conv_small / generic
@@ -1791,11 +1808,14 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             std::vector<uint16_t> h(2 * wpk.size(), 0);
             const int ng = s.cin / 32;
             if (s.wg) {
-                // conv_wg steps (group g, row kh, e) in order ((g * kh + kh) * 4 + e), each
-                // [cout_pad][8 units] as above, holding the transformed weights
-                // v0 = w0, v1 = (w0 + w1 + w2) / 2, v2 = (w0 - w1 + w2) / 2, v3 = w2
-                // (w_kw = the folded kernel at (kh, kw)), computed in double
-                h.assign((size_t)ng * s.kh * 4 * s.cout_pad * 64 * 2 + 1024, 0);
+                // conv_wg steps (group g, pass p, row kh, plane slot el) in order
+                // ((g * npass + p) * kh + kh) * pps + el, each [cout_pad][8 units] as
+                // above, holding the transformed weights v_e = sum_k G[e][k] w_k of
+                // plane e = p * pps + el (w_kw = the folded kernel at (kh, kw);
+                // F(2,3): v0 = w0, v1 = (w0 + w1 + w2) / 2, v2 = (w0 - w1 + w2) / 2,
+                // v3 = w2), computed in double
+                const int A = s.wg + 2, np = s.wg_npass, pps = A / np;
+                h.assign((size_t)ng * s.kh * A * s.cout_pad * 64 * 2 + 1024, 0);
                 for (int g = 0; g < ng; ++g)
                     for (int kh = 0; kh < s.kh; ++kh)
                         for (int o = 0; o < s.cout_pad; ++o)
@@ -1803,10 +1823,11 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
                                 double w3[3];
                                 for (int kw = 0; kw < 3; ++kw)
                                     w3[kw] = o < s.cout ? (double)kern[((size_t)(kh * 3 + kw) * s.cin + 32 * g + c) * s.cout + o] * scale[o] : 0.0;
-                                const double v[4] = {w3[0], 0.5 * (w3[0] + w3[1] + w3[2]), 0.5 * (w3[0] - w3[1] + w3[2]), w3[2]};
-                                for (int e = 0; e < 4; ++e) {
-                                    const size_t row = ((size_t)((g * s.kh + kh) * 4 + e) * s.cout_pad + o) * 64;
-                                    const float w = (float)v[e];
+                                for (int e = 0; e < A; ++e) {
+                                    const double v = wg_g(s.wg, e, 0) * w3[0] + wg_g(s.wg, e, 1) * w3[1] + wg_g(s.wg, e, 2) * w3[2];
+                                    const int p = e / pps, el = e % pps;
+                                    const size_t row = ((size_t)(((g * np + p) * s.kh + kh) * pps + el) * s.cout_pad + o) * 64;
+                                    const float w = (float)v;
                                     const uint16_t hi = f2bf(w);
                                     const int u = c / 8;
                                     h[row + ((u + o) & 7) * 8 + c % 8] = hi;

@@ -1,66 +1,143 @@
-// Split-bf16 convolution with a Winograd F(2,3) transform along W
+// Split-bf16 convolution with a Winograd F(WO, 3) transform along W
 // (AA_PREC_BF16X3, kernel width 3), included by aa_cnn.hip after
 // aa_conv_x3.h (shares bf_hi/bf_lo, the grouped-split layout and x3_store).
 //
 // A kernel-width-3 conv computes, per output row, y_k = sum_t g_t d_{k+t}
-// along W.  F(2,3) produces two adjacent outputs from four inputs with four
-// products instead of six:
-//   u0 = d0 - d2   u1 = d1 + d2   u2 = d2 - d1   u3 = d1 - d3
-//   v0 = g0        v1 = (g0 + g1 + g2) / 2       v2 = (g0 - g1 + g2) / 2   v3 = g2
-//   m_e = u_e v_e  (summed over C_in and the KH rows)
-//   y0 = m0 + m1 + m2      y1 = m1 - m2 - m3
-// so the conv becomes four independent implicit GEMMs (one per e) over the
-// output column PAIRS, K = KH x C_in each: 2/3 of the direct MFMA work.  The
-// input transform runs at staging (f32 arithmetic, then the bf16 hi / lo
-// split of u); the weights are transformed on the host in double and split
-// there; the output transform runs in the epilogue on the f32 accumulators.
+// along W.  F(WO, 3) produces WO adjacent outputs from A = WO + 2 inputs with
+// A products instead of 3 WO:
+//   u = B^T d (A x A),   v = G g (A x 3),   m_e = u_e v_e,   y = A^T m (WO x A)
+// (m_e summed over C_in and the KH rows), so the conv becomes A independent
+// implicit GEMMs (one per plane e) over the output column GROUPS of WO, K =
+// KH x C_in each: A / (3 WO) of the direct MFMA work -- 2/3 for F(2, 3), 1/2
+// for F(4, 3), 4/9 for F(6, 3).  The input transform runs at staging (f32
+// arithmetic, then the bf16 hi / lo split of u); the weights are transformed
+// on the host in double and split there; the output transform runs in the
+// epilogue on the f32 accumulators.  F(2, 3) is the form of rounds 2-4
+// (u0 = d0 - d2, u1 = d1 + d2, u2 = d2 - d1, u3 = d1 - d3; v0 = g0, v1 =
+// (g0 + g1 + g2) / 2, v2 = (g0 - g1 + g2) / 2, v3 = g2; y0 = m0 + m1 + m2,
+// y1 = m1 - m2 - m3); F(4, 3) and F(6, 3) take the interpolation points
+// {0, +-1, +-2} and {0, +-1, +-2, +-1/2} (and infinity).  The larger
+// transforms amplify rounding, but split-bf16 keeps ~17 bits: emulated on the
+// CPU (tools/wino_study.py), model1's max |delta logit| on the bench's 64
+// windows stays 1.6-1.9e-4 for the 9x3 layer direct, F(2,3), F(4,3) or
+// F(6,3) -- the other layers' rounding dominates.
 //
-// LDS: four planes (e) of the transformed patch, (TH + KH - 1) rows x TW/2
-// pairs, 128 B per pair-pixel (32-channel group, hi then lo), with the
-// rotation swizzle of aa_conv_x3.h on the plane's linear pair index v.  A
-// fragment's 16 lanes read 16 consecutive tile pairs p, and at tap kh the
-// pair index is v = p + kh * TW/2: consecutive for every tap with no row
-// wrap at all (the pair planes have no halo along W), so the ds_read_b128
-// lane groups are conflict-free.  Weights come per step (group g, row kh,
-// e) as [cout_pad][8 units] with aa_conv_x3.h's swizzle, loaded per wave
-// straight from global (L2) one step ahead -- waves meet only at the
-// barriers around each group's staging.
+// LDS: the A planes of the transformed patch, (TH + KH - 1) rows x TW / WO
+// groups, 128 B per group-pixel (32-channel group, hi then lo), with the
+// rotation swizzle of aa_conv_x3.h on the plane's linear group index v; staged
+// NPASS planes-sets at a time (A / NPASS planes each) to bound the LDS.  A
+// fragment's 16 lanes read 16 consecutive tile groups p, and at tap kh the
+// group index is v = p + kh * TW/WO: consecutive for every tap with no row
+// wrap (the planes have no halo along W), so the ds_read_b128 lane groups
+// are conflict-free.  Weights come per step (group g, pass, row kh, plane) as
+// [cout_pad][8 units] with aa_conv_x3.h's swizzle, loaded per wave straight
+// from global (L2) one step ahead -- waves meet only at the barriers around
+// each staging.
 #pragma once
+
+#include <type_traits>
 
 namespace aa {
 
-template <int KH, int TH, int TW>
-__host__ __device__ constexpr size_t wg_patch_bytes() {
-    return (size_t)4 * (TH + KH - 1) * (TW / 2) * 128;
+// transform coefficients (exact in f32): B^T [A][A], A^T [WO][A]
+__host__ __device__ constexpr float wg_bt(int wo, int e, int t) {
+    constexpr float b2[4][4] = {{1, 0, -1, 0}, {0, 1, 1, 0}, {0, -1, 1, 0}, {0, 1, 0, -1}};
+    constexpr float b3[5][5] = {{2, -1, -2, 1, 0}, {0, -2, -1, 1, 0}, {0, 2, -3, 1, 0}, {0, -1, 0, 1, 0},
+                                {0, 2, -1, -2, 1}};
+    constexpr float b4[6][6] = {{4, 0, -5, 0, 1, 0},  {0, -4, -4, 1, 1, 0}, {0, 4, -4, -1, 1, 0},
+                                {0, -2, -1, 2, 1, 0}, {0, 2, -1, -2, 1, 0}, {0, 4, 0, -5, 0, 1}};
+    constexpr float b6[8][8] = {{-1, 0, 5.25f, 0, -5.25f, 0, 1, 0},         {0, 1, 1, -4.25f, -4.25f, 1, 1, 0},
+                                {0, -1, 1, 4.25f, -4.25f, -1, 1, 0},        {0, 0.5f, 0.25f, -2.5f, -1.25f, 2, 1, 0},
+                                {0, -0.5f, 0.25f, 2.5f, -1.25f, -2, 1, 0},  {0, 2, 4, -2.5f, -5, 0.5f, 1, 0},
+                                {0, -2, 4, 2.5f, -5, -0.5f, 1, 0},          {0, -1, 0, 5.25f, 0, -5.25f, 0, 1}};
+    return wo == 2 ? b2[e][t] : wo == 3 ? b3[e][t] : wo == 4 ? b4[e][t] : b6[e][t];
+}
+__host__ __device__ constexpr float wg_at(int wo, int k, int e) {
+    constexpr float a2[2][4] = {{1, 1, 1, 0}, {0, 1, -1, -1}};
+    constexpr float a3[3][5] = {{1, 1, 1, 1, 0}, {0, 1, -1, 2, 0}, {0, 1, 1, 4, 1}};
+    constexpr float a4[4][6] = {{1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -2, 0}, {0, 1, 1, 4, 4, 0}, {0, 1, -1, 8, -8, 1}};
+    constexpr float a6[6][8] = {{1, 1, 1, 1, 1, 1, 1, 0},
+                                {0, 1, -1, 2, -2, 0.5f, -0.5f, 0},
+                                {0, 1, 1, 4, 4, 0.25f, 0.25f, 0},
+                                {0, 1, -1, 8, -8, 0.125f, -0.125f, 0},
+                                {0, 1, 1, 16, 16, 0.0625f, 0.0625f, 0},
+                                {0, 1, -1, 32, -32, 0.03125f, -0.03125f, 1}};
+    return wo == 2 ? a2[k][e] : wo == 3 ? a3[k][e] : wo == 4 ? a4[k][e] : a6[k][e];
+}
+// G [A][3] (host, double): v_e = sum_k G[e][k] g_k
+static inline double wg_g(int wo, int e, int k) {
+    static const double g2[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    static const double g3[5][3] = {{0.5, 0, 0},
+                                    {-0.5, -0.5, -0.5},
+                                    {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                    {1.0 / 6, 1.0 / 3, 2.0 / 3},
+                                    {0, 0, 1}};
+    static const double g4[6][3] = {{0.25, 0, 0},
+                                    {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                                    {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                    {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                                    {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                                    {0, 0, 1}};
+    static const double g6[8][3] = {{-1, 0, 0},
+                                    {-2.0 / 9, -2.0 / 9, -2.0 / 9},
+                                    {-2.0 / 9, 2.0 / 9, -2.0 / 9},
+                                    {1.0 / 90, 1.0 / 45, 2.0 / 45},
+                                    {1.0 / 90, -1.0 / 45, 2.0 / 45},
+                                    {32.0 / 45, 16.0 / 45, 8.0 / 45},
+                                    {32.0 / 45, -16.0 / 45, 8.0 / 45},
+                                    {0, 0, 1}};
+    return wo == 2 ? g2[e][k] : wo == 3 ? g3[e][k] : wo == 4 ? g4[e][k] : g6[e][k];
 }
 
-template <int KH, int BN, int TH, int TW>
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename Fn>
+__device__ __forceinline__ void wg_static_for(Fn&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        wg_static_for<B + 1, E>(f);
+    }
+}
+
+template <int KH, int TH, int TW, int WO, int NPASS>
+__host__ __device__ constexpr size_t wg_patch_bytes() {
+    return (size_t)((WO + 2) / NPASS) * (TH + KH - 1) * (TW / WO) * 128;
+}
+
+template <int KH, int BN, int TH, int TW, int WO, int NPASS>
 constexpr size_t wg_lds_bytes() {
-    const size_t main = wg_patch_bytes<KH, TH, TW>();
+    const size_t main = wg_patch_bytes<KH, TH, TW, WO, NPASS>();
     const size_t epi = (size_t)TH * TW * BN * 4;
     return main > epi ? main : epi;
 }
 
+// epilogue pixel swizzle shift (x3_eoff): the WO outputs of a group land in
+// distinct 16-B slots across a store's 8 lanes when WO >> PSH is odd
+constexpr int wg_psh(int wo) { return wo == 4 ? 2 : wo == 3 ? 0 : 1; }
+
 // DIAG (tools/conv_bench_x3.hip only): bit 0 skips the staging, bit 1 the MFMA steps
 template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int OCC = 0,
-          bool IN_SPLIT = false, bool OUT_SPLIT = false, int DIAG = 0>
+          bool IN_SPLIT = false, bool OUT_SPLIT = false, int DIAG = 0, int WO = 2, int NPASS = 1>
 __global__ __launch_bounds__(WM * WN * 64)
 __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, OCC ? OCC : 8)))
 void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restrict__ wt,
              const float* __restrict__ bias, float* __restrict__ out, int Hout, int Wout, int cout_store,
              int tiles_w, int act, float alpha) {
     typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-    static_assert(TW % 2 == 0 && TH % POOL == 0 && TW % POOL == 0, "pair- and pool-aligned tile");
-    constexpr int NP = TW / 2;  // output column pairs per tile row
-    constexpr int TP = TH * NP;  // pair-pixels per tile
+    constexpr int A = WO + 2;                 // planes
+    constexpr int PPS = A / NPASS;            // planes per staging pass
+    static_assert(WO >= 2 && WO <= 6 && WO != 5, "F(2|3|4|6, 3)");
+    static_assert(A % NPASS == 0, "whole passes");
+    static_assert(TW % WO == 0 && TH % POOL == 0 && TW % POOL == 0, "group- and pool-aligned tile");
+    constexpr int NP = TW / WO;  // output column groups per tile row
+    constexpr int TP = TH * NP;  // group-pixels per tile
     static_assert(TP <= WM * MF * 16, "tile covered by the waves' fragments");
     static_assert(CIN % 32 == 0, "C_in multiple of 32");
     constexpr int NTHR = WM * WN * 64;
     constexpr int BN = WN * NF * 16;
     constexpr int PH = TH + KH - 1;
-    constexpr int PV = PH * NP;  // pair-pixels per plane
+    constexpr int PV = PH * NP;  // group-pixels per plane
     constexpr int NG = CIN / 32;
-    constexpr int NSTEP = NG * KH * 4;  // (group, kh, e)
+    constexpr int NSTEP = NG * NPASS * KH * PPS;  // (group, pass, kh, plane of the pass)
     constexpr int SLICE = BN * 64;      // bf16 elements of one step's slice
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* patch = smem;
@@ -91,9 +168,9 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     const size_t step_stride = (size_t)gridDim.y * SLICE;
     const __amdgpu_buffer_rsrc_t wrs = x3_wrsrc(wt);
 
-    f32x4 acc[4][MF][NF];
+    f32x4 acc[A][MF][NF];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+    for (int e = 0; e < A; ++e)
 #pragma unroll
         for (int i = 0; i < MF; ++i)
 #pragma unroll
@@ -111,13 +188,14 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             b.l[j] = x3_wload(wrs, bofs[j] ^ 64, soff);
         }
     };
-    // one step: plane e at row offset kh, B of this step in `cur`, the next
-    // step's B loaded into `nxt` under this step's MFMAs; A fragments just
-    // in time, two in flight
-    auto step = [&](BSet& cur, BSet& nxt, int s, int kh, auto ec) {
+    // one step: plane e (slot el of the staged pass) at row offset kh, B of
+    // this step in `cur`, the next step's B loaded into `nxt` under this
+    // step's MFMAs; A fragments just in time, two in flight
+    auto step = [&](BSet& cur, BSet& nxt, int s, int kh, auto ec, auto elc) {
         constexpr int e = decltype(ec)::value;
+        constexpr int el = decltype(elc)::value;
         if (s + 1 < NSTEP) read_b(nxt, s + 1);
-        const int pofs = e * PV * 128 + kh * NP * 128, tv = kh * NP;
+        const int pofs = el * PV * 128 + kh * NP * 128, tv = kh * NP;
         bf16x8 h2[2], l2[2];
         auto rd = [&](int i, int k) {
             const int a = pofs + abase[i] + (((aph[i] + tv) & 7) << 4);
@@ -148,7 +226,6 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         const int pix = gh * Win + gw;
         if constexpr (IN_SPLIT) {
             const int o = pix * (CIN * 4) + g * 128 + cq * 8;
-            typedef __attribute__((ext_vector_type(2))) int i32x2;
             const bf16x4 h = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(ars, o, wbase, 0));
             const bf16x4 l = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(ars, o + 64, wbase, 0));
             return make_float4((float)h[0] + (float)l[0], (float)h[1] + (float)l[1], (float)h[2] + (float)l[2],
@@ -160,47 +237,88 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     };
 
     read_b(B0, 0);  // its latency hides behind the first staging
-    for (int g = 0; g < NG; ++g) {
-        if (g > 0) __syncthreads();  // every wave is done with group g-1's planes
-        // ---- stage group g: per (pair-pixel v, channel quad cq) the four
-        // input columns 2 jp .. 2 jp + 3, transformed, split, into the planes ----
-        constexpr int ITEMS = (DIAG & 1) ? 0 : PV * 8;
-        for (int idx = threadIdx.x; idx < ITEMS; idx += NTHR) {
-            const int v = idx >> 3, cq = idx & 7;
-            const int R = v / NP, jp = v - (v / NP) * NP;
-            const int gh = min(oh0 + R, Hin - 1);
-            float4 d[4];
+    wg_static_for<0, NG>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        wg_static_for<0, NPASS>([&](auto pc) {
+            constexpr int pass = decltype(pc)::value;
+            if (g > 0 || pass > 0) __syncthreads();  // every wave is done with the previous planes
+            // ---- stage (group g, pass): per (group-pixel v, channel quad cq) the
+            // A input columns WO jp .. WO jp + A - 1, transformed, split, into
+            // the pass's planes ----
+            constexpr int ITEMS = (DIAG & 1) ? 0 : PV * 8;
+            for (int idx = threadIdx.x; idx < ITEMS; idx += NTHR) {
+                const int v = idx >> 3, cq = idx & 7;
+                const int R = v / NP, jp = v - (v / NP) * NP;
+                const int gh = min(oh0 + R, Hin - 1);
+                float4 d[A];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) d[c] = load4(gh, min(ow0 + 2 * jp + c, Win - 1), g, cq);
-            float4 u[4];
-            u[0] = make_float4(d[0].x - d[2].x, d[0].y - d[2].y, d[0].z - d[2].z, d[0].w - d[2].w);
-            u[1] = make_float4(d[1].x + d[2].x, d[1].y + d[2].y, d[1].z + d[2].z, d[1].w + d[2].w);
-            u[2] = make_float4(d[2].x - d[1].x, d[2].y - d[1].y, d[2].z - d[1].z, d[2].w - d[1].w);
-            u[3] = make_float4(d[1].x - d[3].x, d[1].y - d[3].y, d[1].z - d[3].z, d[1].w - d[3].w);
-            const int unit = (((cq >> 1) + v) & 7) << 4;
+                for (int c = 0; c < A; ++c) d[c] = load4(gh, min(ow0 + WO * jp + c, Win - 1), g, cq);
+                const int unit = (((cq >> 1) + v) & 7) << 4;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                uint32_t h0, l0, h1, l1;
-                split2(u[e].x, u[e].y, h0, l0);
-                split2(u[e].z, u[e].w, h1, l1);
-                const int a = (e * PV + v) * 128 + unit + (cq & 1) * 8;
-                *reinterpret_cast<uint2*>(patch + a) = make_uint2(h0, h1);
-                *reinterpret_cast<uint2*>(patch + (a ^ 64)) = make_uint2(l0, l1);
+                for (int el = 0; el < PPS; ++el) {
+                    constexpr int e0 = pass * PPS;
+                    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int t = 0; t < A; ++t) {
+                        const float b = wg_bt(WO, e0 + el, t);
+                        if (b == 0.f) continue;
+                        if (b == 1.f) {
+                            u.x += d[t].x; u.y += d[t].y; u.z += d[t].z; u.w += d[t].w;
+                        } else if (b == -1.f) {
+                            u.x -= d[t].x; u.y -= d[t].y; u.z -= d[t].z; u.w -= d[t].w;
+                        } else {
+                            u.x = fmaf(b, d[t].x, u.x); u.y = fmaf(b, d[t].y, u.y);
+                            u.z = fmaf(b, d[t].z, u.z); u.w = fmaf(b, d[t].w, u.w);
+                        }
+                    }
+                    uint32_t h0, l0, h1, l1;
+                    split2(u.x, u.y, h0, l0);
+                    split2(u.z, u.w, h1, l1);
+                    const int a = (el * PV + v) * 128 + unit + (cq & 1) * 8;
+                    *reinterpret_cast<uint2*>(patch + a) = make_uint2(h0, h1);
+                    *reinterpret_cast<uint2*>(patch + (a ^ 64)) = make_uint2(l0, l1);
+                }
             }
-        }
-        __syncthreads();
-        for (int kh = 0; kh < ((DIAG & 2) ? 0 : KH); ++kh) {
-            const int s0 = (g * KH + kh) * 4;
-            step(B0, B1, s0, kh, std::integral_constant<int, 0>{});
-            step(B1, B0, s0 + 1, kh, std::integral_constant<int, 1>{});
-            step(B0, B1, s0 + 2, kh, std::integral_constant<int, 2>{});
-            step(B1, B0, s0 + 3, kh, std::integral_constant<int, 3>{});
-        }
-    }
+            __syncthreads();
+            if constexpr ((DIAG & 2) == 0) {
+                if constexpr (PPS % 2 == 0) {
+                    // an even count of steps per row: the B sets alternate the same way every row
+                    for (int kh = 0; kh < KH; ++kh) {
+                        const int s0 = ((g * NPASS + pass) * KH + kh) * PPS;
+                        wg_static_for<0, PPS>([&](auto elc) {
+                            constexpr int el = decltype(elc)::value;
+                            constexpr std::integral_constant<int, pass * PPS + el> ec{};
+                            if constexpr ((el & 1) == 0)
+                                step(B0, B1, s0 + el, kh, ec, elc);
+                            else
+                                step(B1, B0, s0 + el, kh, ec, elc);
+                        });
+                    }
+                } else {
+                    // odd: rows unrolled, the B set by the step's parity in the pass
+                    // (KH * PPS steps per pass: even KH keeps passes aligned)
+                    constexpr int sb = (g * NPASS + pass) * KH * PPS;
+                    wg_static_for<0, KH * PPS>([&](auto sc) {
+                        constexpr int si = decltype(sc)::value;
+                        constexpr int kh = si / PPS, el = si % PPS;
+                        constexpr std::integral_constant<int, pass * PPS + el> ec{};
+                        constexpr std::integral_constant<int, el> elc{};
+                        // global step parity: the B set a step reads was loaded by the previous step
+                        if constexpr ((sb + si) % 2 == 0)
+                            step(B0, B1, sb + si, kh, ec, elc);
+                        else
+                            step(B1, B0, sb + si, kh, ec, elc);
+                    });
+                }
+            }
+        });
+    });
     __syncthreads();  // planes no longer needed: the f32 tile reuses LDS
 
     // ---- epilogue: output transform into the f32 tile (x3_store's swizzled
-    // layout, PSH = 1: a store's 8 lanes hold every other pixel) ----
+    // layout: a store's 8 lanes hold pixels WO apart, PSH keeps their units in
+    // distinct 16-B slots) ----
+    constexpr int PSH = wg_psh(WO);
     float* E = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
@@ -210,17 +328,26 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
             const int p = (wm * MF + i) * 16 + (lane & 15);
             if (p < TP) {
                 const int r = p / NP, jp = p - (p / NP) * NP;
-                const f32x4 y0 = acc[0][i][j] + acc[1][i][j] + acc[2][i][j];
-                const f32x4 y1 = acc[1][i][j] - acc[2][i][j] - acc[3][i][j];
-                const int px = r * TW + 2 * jp;
-                *reinterpret_cast<float4*>(E + x3_eoff<BN, 1>(px, u)) = make_float4(y0[0], y0[1], y0[2], y0[3]);
-                *reinterpret_cast<float4*>(E + x3_eoff<BN, 1>(px + 1, u)) = make_float4(y1[0], y1[1], y1[2], y1[3]);
+                const int px = r * TW + WO * jp;
+#pragma unroll
+                for (int k = 0; k < WO; ++k) {
+                    f32x4 y = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int e = 0; e < A; ++e) {
+                        const float c = wg_at(WO, k, e);
+                        if (c == 0.f) continue;
+                        if (c == 1.f) y += acc[e][i][j];
+                        else if (c == -1.f) y -= acc[e][i][j];
+                        else y += c * acc[e][i][j];
+                    }
+                    *reinterpret_cast<float4*>(E + x3_eoff<BN, PSH>(px + k, u)) = make_float4(y[0], y[1], y[2], y[3]);
+                }
             }
         }
     }
     __syncthreads();
-    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, false, 1>(E, bias, out, n, cb, oh0, ow0, Hout, Wout, cout_store, act,
-                                                         alpha);
+    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, false, PSH>(E, bias, out, n, cb, oh0, ow0, Hout, Wout, cout_store,
+                                                           act, alpha);
 }
 
 }  // namespace aa
