@@ -1207,7 +1207,7 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
 // pool) of kernel-width-3 convs -> waves (WM x WN), fragments per wave (MF x
 // NF, each with WO + 2 accumulator sets), output tile TH x TW (TW a multiple
 // of WO), pinned waves per SIMD (0: free), outputs per group WO, staging
-// passes NPASS.  Preferred over conv_x3 where a row exists (the
+// passes NPASS, B fragment sets in flight BD.  Preferred over conv_x3 where a row exists (the
 // fused first-layer stage always runs conv_x3).  In-pipeline A/B (tools/ab.sh,
 // same box): the 9x3 layer 187 -> 160 us, step 180k -> 193k audio-s/s; the
 // small 3x3 / 1x3 layers lose on it (their transform-heavy staging outweighs
@@ -1219,11 +1219,11 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
 // 122 us, step 260k -> 264k; F(4,3) on 39x12 tiles 140 us, F(3,3) spills):
 // 8 planes of the 39 x 6 tile's single column group, 4 waves of 16 output
 // channels each, 96 accumulator VGPRs
-#define AA_WG_CFGS(X) X(9, 64, 3, 1, 4, 3, 1, 39, 6, 2, 6, 1)
+#define AA_WG_CFGS(X) X(9, 64, 3, 1, 4, 3, 1, 39, 6, 0, 6, 1, 2)
 #endif
 
 static int wg_bn(int kh, int kw, int cin, int pool) {
-#define AA_WBN(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS) \
+#define AA_WBN(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS, BD) \
     if (kw == 3 && kh == KH && cin == CIN && pool == POOL) return WN * NF * 16;
     AA_WG_CFGS(AA_WBN)
 #undef AA_WBN
@@ -1231,7 +1231,7 @@ static int wg_bn(int kh, int kw, int cin, int pool) {
 }
 // (WO, NPASS) of the Winograd instantiation serving a stage
 static void wg_form(int kh, int cin, int pool, int* wo, int* npass) {
-#define AA_WFORM(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS) \
+#define AA_WFORM(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS, BD) \
     if (kh == KH && cin == CIN && pool == POOL) { *wo = WO; *npass = NPASS; return; }
     AA_WG_CFGS(AA_WFORM)
 #undef AA_WFORM
@@ -1289,9 +1289,9 @@ static int launch_x3(const Stage& s, const void* in, void* out, int n, hipStream
 }
 
 template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int OCC, int WO, int NPASS,
-          bool IN_SPLIT, bool OUT_SPLIT>
+          int BD, bool IN_SPLIT, bool OUT_SPLIT>
 static int launch_wg(const Stage& s, const void* in, void* out, int n, hipStream_t st) {
-    auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IN_SPLIT, OUT_SPLIT, 0, WO, NPASS>;
+    auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IN_SPLIT, OUT_SPLIT, 0, WO, NPASS, BD>;
     constexpr int BN = WN * NF * 16;
     AA_CHECK((double)s.Hin * s.Win * s.cin * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
              "conv %s: one window's activations exceed 2 GiB", s.name.c_str());
@@ -1416,13 +1416,13 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
     }
     if constexpr (is_split<T>()) {
         if (s.wg) {
-#define AA_LAUNCHW(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS)                                       \
+#define AA_LAUNCHW(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS, BD)                                       \
             if (s.kh == KH && s.cin == CIN && s.pool == POOL) {                                                   \
                 if (s.in_split)                                                                                   \
-                    return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, true, true>(s, in, out, n, st) \
-                                       : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, true, false>(s, in, out, n, st); \
-                return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, false, true>(s, in, out, n, st) \
-                                   : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, false, false>(s, in, out, n, st); \
+                    return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, BD, true, true>(s, in, out, n, st) \
+                                       : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, BD, true, false>(s, in, out, n, st); \
+                return s.out_split ? launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, BD, false, true>(s, in, out, n, st) \
+                                   : launch_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, WO, NPASS, BD, false, false>(s, in, out, n, st); \
             }
             AA_WG_CFGS(AA_LAUNCHW)
 #undef AA_LAUNCHW
@@ -1902,6 +1902,10 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             Stage& b = m->st[k + 1];
             if (a.skipped || a.kind != ST_MFMA || b.kind != ST_MFMA || b.fused_first) continue;
             if (a.cout % 32 != 0 || b.cin != a.cout) continue;
+            // a Winograd consumer transforms f32 values before it splits them: it
+            // reads plain f32 (one 16-B load per 4 channels, not two 8-B loads and
+            // a hi + lo sum); the split layout only pays for global_load_lds staging
+            if (b.wg && !getenv("AA_WG_SPLIT_IN")) continue;
             a.out_split = 1;
             b.in_split = 1;
         }

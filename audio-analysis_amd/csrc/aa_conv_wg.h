@@ -116,7 +116,7 @@ constexpr int wg_psh(int wo) { return wo == 4 ? 2 : wo == 3 ? 0 : 1; }
 
 // DIAG (tools/conv_bench_x3.hip only): bit 0 skips the staging, bit 1 the MFMA steps
 template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int OCC = 0,
-          bool IN_SPLIT = false, bool OUT_SPLIT = false, int DIAG = 0, int WO = 2, int NPASS = 1>
+          bool IN_SPLIT = false, bool OUT_SPLIT = false, int DIAG = 0, int WO = 2, int NPASS = 1, int BD = 2>
 __global__ __launch_bounds__(WM * WN * 64)
 __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, OCC ? OCC : 8)))
 void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restrict__ wt,
@@ -127,6 +127,10 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     constexpr int PPS = A / NPASS;            // planes per staging pass
     static_assert(WO >= 2 && WO <= 6 && WO != 5, "F(2|3|4|6, 3)");
     static_assert(A % NPASS == 0, "whole passes");
+    // BD: B fragment sets in flight (the next BD - 1 steps' weights load under
+    // this step's MFMAs); a runtime row loop needs the set of a step fixed by
+    // its plane slot
+    static_assert(BD >= 2 && ((A / NPASS) % 2 != 0 || (A / NPASS) % BD == 0), "B ring depth divides the pass");
     static_assert(TW % WO == 0 && TH % POOL == 0 && TW % POOL == 0, "group- and pool-aligned tile");
     constexpr int NP = TW / WO;  // output column groups per tile row
     constexpr int TP = TH * NP;  // group-pixels per tile
@@ -179,7 +183,7 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     struct BSet {
         bf16x8 h[NF], l[NF];
     };
-    BSet B0, B1;
+    BSet Bq[BD];
     auto read_b = [&](BSet& b, int s) {
         const int soff = __builtin_amdgcn_readfirstlane((int)((cb * SLICE + s * step_stride) * 2));
 #pragma unroll
@@ -191,10 +195,13 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     // one step: plane e (slot el of the staged pass) at row offset kh, B of
     // this step in `cur`, the next step's B loaded into `nxt` under this
     // step's MFMAs; A fragments just in time, two in flight
-    auto step = [&](BSet& cur, BSet& nxt, int s, int kh, auto ec, auto elc) {
+    // bc: the step's B set (s % BD, known at compile time)
+    auto step = [&](auto bc, int s, int kh, auto ec, auto elc) {
         constexpr int e = decltype(ec)::value;
         constexpr int el = decltype(elc)::value;
-        if (s + 1 < NSTEP) read_b(nxt, s + 1);
+        constexpr int b = decltype(bc)::value;
+        BSet& cur = Bq[b];
+        if (s + BD - 1 < NSTEP) read_b(Bq[(b + BD - 1) % BD], s + BD - 1);
         const int pofs = el * PV * 128 + kh * NP * 128, tv = kh * NP;
         bf16x8 h2[2], l2[2];
         auto rd = [&](int i, int k) {
@@ -236,7 +243,9 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         }
     };
 
-    read_b(B0, 0);  // its latency hides behind the first staging
+#pragma unroll
+    for (int k = 0; k < BD - 1; ++k)
+        if (k < NSTEP) read_b(Bq[k], k);  // their latency hides behind the first staging
     wg_static_for<0, NG>([&](auto gc) {
         constexpr int g = decltype(gc)::value;
         wg_static_for<0, NPASS>([&](auto pc) {
@@ -254,12 +263,39 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
 #pragma unroll
                 for (int c = 0; c < A; ++c) d[c] = load4(gh, min(ow0 + WO * jp + c, Win - 1), g, cq);
                 const int unit = (((cq >> 1) + v) & 7) << 4;
+                // F(6, 3): the factored input transform (shared partial sums,
+                // 26 operations per channel instead of the 44 non-zeros of B^T)
+                float4 u6[WO == 6 ? 8 : 1];
+                if constexpr (WO == 6) {
+                    auto f = [&](auto get, auto put) {
+                        const float d0 = get(d[0]), d1 = get(d[1]), d2 = get(d[2]), d3 = get(d[3]);
+                        const float d4 = get(d[4]), d5 = get(d[5]), d6 = get(d[6]), d7 = get(d[7]);
+                        put(0, fmaf(5.25f, d2 - d4, d6 - d0));
+                        put(7, fmaf(5.25f, d3 - d5, d7 - d1));
+                        const float a12 = fmaf(-4.25f, d4, d2 + d6), b12 = fmaf(-4.25f, d3, d1 + d5);
+                        put(1, a12 + b12);
+                        put(2, a12 - b12);
+                        const float a34 = fmaf(-1.25f, d4, fmaf(0.25f, d2, d6));
+                        const float b34 = fmaf(2.f, d5, fmaf(-2.5f, d3, 0.5f * d1));
+                        put(3, a34 + b34);
+                        put(4, a34 - b34);
+                        const float a56 = fmaf(-5.f, d4, fmaf(4.f, d2, d6));
+                        const float b56 = fmaf(0.5f, d5, fmaf(-2.5f, d3, 2.f * d1));
+                        put(5, a56 + b56);
+                        put(6, a56 - b56);
+                    };
+                    f([](const float4& x) { return x.x; }, [&](int e, float y) { u6[e].x = y; });
+                    f([](const float4& x) { return x.y; }, [&](int e, float y) { u6[e].y = y; });
+                    f([](const float4& x) { return x.z; }, [&](int e, float y) { u6[e].z = y; });
+                    f([](const float4& x) { return x.w; }, [&](int e, float y) { u6[e].w = y; });
+                }
 #pragma unroll
                 for (int el = 0; el < PPS; ++el) {
                     constexpr int e0 = pass * PPS;
                     float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if constexpr (WO == 6) u = u6[e0 + el];
 #pragma unroll
-                    for (int t = 0; t < A; ++t) {
+                    for (int t = 0; t < (WO == 6 ? 0 : A); ++t) {
                         const float b = wg_bt(WO, e0 + el, t);
                         if (b == 0.f) continue;
                         if (b == 1.f) {
@@ -288,10 +324,8 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                         wg_static_for<0, PPS>([&](auto elc) {
                             constexpr int el = decltype(elc)::value;
                             constexpr std::integral_constant<int, pass * PPS + el> ec{};
-                            if constexpr ((el & 1) == 0)
-                                step(B0, B1, s0 + el, kh, ec, elc);
-                            else
-                                step(B1, B0, s0 + el, kh, ec, elc);
+                            // s0 is a multiple of PPS, hence of BD: the set is el % BD
+                            step(std::integral_constant<int, el % BD>{}, s0 + el, kh, ec, elc);
                         });
                     }
                 } else {
@@ -303,11 +337,8 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                         constexpr int kh = si / PPS, el = si % PPS;
                         constexpr std::integral_constant<int, pass * PPS + el> ec{};
                         constexpr std::integral_constant<int, el> elc{};
-                        // global step parity: the B set a step reads was loaded by the previous step
-                        if constexpr ((sb + si) % 2 == 0)
-                            step(B0, B1, sb + si, kh, ec, elc);
-                        else
-                            step(B1, B0, sb + si, kh, ec, elc);
+                        // the B set a step reads was loaded BD - 1 steps before
+                        step(std::integral_constant<int, (sb + si) % BD>{}, sb + si, kh, ec, elc);
                     });
                 }
             }

@@ -73,6 +73,8 @@ struct SnPlan {
     StageTimer timer;          // HIP events around the launches of the stages in timer.mask
     bool select_reg = false;   // row medians by sn_select_reg (AA_SN_SELECT=reg; A/B knob) or sn_select
     bool stft_r8 = false;      // the transform by sn_stft64r8 (AA_SN_STFT=r8; A/B knob) or sn_stft64
+    bool tw_chain = true;      // sn_stft64's twiddle ladders from 7 table values (AA_SN_TW=table: all 22;
+                               // 99 -> 94.5 us per 60 s clip, S bit-identical on the tests' clips)
     bool colmed_fused = false; // column medians inside sn_stft64 (AA_SN_COLMED=fused; A/B knob: 188 us per
                                // clip against 98 + 44 as two launches) or their own launch
     bool colmed_bs = false;    // column medians by bit-serial search (AA_SN_COLMED=bs; A/B knob: 52 us against
@@ -303,6 +305,12 @@ __device__ unsigned wave_median_2049(const unsigned (&v)[33], unsigned* hists, i
 // at the frame's last barrier.  Measured 188 us per clip against 98 + 44 us as
 // two launches: the select holds the block -- and its 36 KiB of LDS -- far
 // longer than the transform, and 4 blocks per CU leave nothing to fill in.
+// TWC (default; AA_SN_TW=table for all table values): per frame only W^1, W^2, W^4 (W^8) of each twiddle
+// ladder come from the tables (L2); the other powers are their products in
+// f64 (<= 3 roundings of 2^-53: the f32 magnitudes can move only on rounding
+// ties, as between any two f64 FFT factorisations), so 7 instead of 22 table
+// loads of 16 B per thread and frame
+template <bool TWC>
 __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) void sn_stft64(
     const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const double2* __restrict__ win2,
     const double2* __restrict__ tw1, const double2* __restrict__ tw3, const double2* __restrict__ twS,
@@ -358,9 +366,26 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
             }
         }
         // ---- 1. DFT-16 over n1, twiddle, rows k1 ----
-        ddft16(v);
+        if constexpr (TWC) {
+            double2 w[16];
+            w[1] = tw1[0 * 16 + i1];
+            w[2] = tw1[1 * 16 + i1];
+            w[4] = tw1[3 * 16 + i1];
+            w[8] = tw1[7 * 16 + i1];
+            ddft16(v);
+            w[3] = dmul(w[2], w[1]);
+            w[5] = dmul(w[4], w[1]);
+            w[6] = dmul(w[4], w[2]);
+            w[7] = dmul(w[4], w[3]);
 #pragma unroll
-        for (int k1 = 1; k1 < 16; ++k1) v[dp16(k1)] = dmul(v[dp16(k1)], tw1[(k1 - 1) * 16 + i1]);
+            for (int k = 9; k < 16; ++k) w[k] = dmul(w[8], w[k - 8]);
+#pragma unroll
+            for (int k1 = 1; k1 < 16; ++k1) v[dp16(k1)] = dmul(v[dp16(k1)], w[k1]);
+        } else {
+            ddft16(v);
+#pragma unroll
+            for (int k1 = 1; k1 < 16; ++k1) v[dp16(k1)] = dmul(v[dp16(k1)], tw1[(k1 - 1) * 16 + i1]);
+        }
 #pragma unroll
         for (int k1 = 0; k1 < 16; ++k1) buf[k1 * kS64R1 + t] = v[dp16(k1)];
         __syncthreads();
@@ -383,9 +408,19 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
         // W16^n = (cos, -sin)(2 pi n / 16), n < 8
         constexpr double kW16r[8] = {1.0, kCos8, kRt2, kSin8, 0.0, -kSin8, -kRt2, -kCos8};
         constexpr double kW16i[8] = {0.0, -kSin8, -kRt2, -kCos8, -1.0, -kCos8, -kRt2, -kSin8};
+        double2 w3c[8];
+        if constexpr (TWC) {
+            w3c[1] = tw3[0 * kS64T + i3];
+            w3c[2] = tw3[1 * kS64T + i3];
+            w3c[4] = tw3[3 * kS64T + i3];
+            w3c[3] = dmul(w3c[2], w3c[1]);
+            w3c[5] = dmul(w3c[4], w3c[1]);
+            w3c[6] = dmul(w3c[4], w3c[2]);
+            w3c[7] = dmul(w3c[4], w3c[3]);
+        }
 #pragma unroll
         for (int n3 = 1; n3 < 8; ++n3) {
-            const double2 w = tw3[(n3 - 1) * kS64T + i3];  // W2048^(n3 j)
+            const double2 w = TWC ? w3c[n3] : tw3[(n3 - 1) * kS64T + i3];  // W2048^(n3 j)
             // thread 0's second column (128) takes W16^n3 = W8^n3 conj(W16^n3):
             // the same shift by one bin, times conj(W16^n3)
             const double2 b2 = z ? make_double2(kW16r[n3], kW16i[n3]) : w;
@@ -1571,8 +1606,11 @@ static int sn_launch_stft(SnPlan& p, const float* pcm, int64_t n, int F, float* 
     if (p.stft_r8)
         hipLaunchKernelGGL(sn_stft64r8, dim3(grid), dim3(kR8T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
                            tab + kR8Tw1, tab + kR8Tw2, tab + kR8Tw3, tab + kR8TwS, S, ld, gmax);
+    else if (p.tw_chain)
+        hipLaunchKernelGGL(sn_stft64<true>, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
+                           tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax, colmed);
     else
-        hipLaunchKernelGGL(sn_stft64, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
+        hipLaunchKernelGGL(sn_stft64<false>, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
                            tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax, colmed);
     AA_LAUNCH_CHECK();
     return p.timer.end(SN_STAGE_STFT, st, e0);
@@ -1695,6 +1733,7 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
     if (const char* e = std::getenv("AA_SN_SELECT")) p->select_reg = std::strcmp(e, "reg") == 0;
     if (const char* e = std::getenv("AA_SN_DIAG")) p->diag = std::atoi(e);
     if (const char* e = std::getenv("AA_SN_STFT")) p->stft_r8 = std::strcmp(e, "r8") == 0;
+    if (const char* e = std::getenv("AA_SN_TW")) p->tw_chain = std::strcmp(e, "table") != 0;
     if (const char* e = std::getenv("AA_SN_STFT_BLOCKS")) p->stft_blocks = std::max(8, std::atoi(e));
     if (const char* e = std::getenv("AA_SN_COLMED")) {
         p->colmed_bs = std::strcmp(e, "bs") == 0;

@@ -693,6 +693,21 @@ def main_step(args, world, rank, dev, emit=True):
                 e["cold_over_warm"] = round(el_w / el, 4)
             if mode.startswith("pool"):
                 e["note"] = f"{pairs} resident clip pairs in rotation (inside the Infinity Cache)"
+            if mode.startswith("fp8"):
+                # configs[4]'s kernels against their own bounds: events around
+                # every launch of 5 serial steps (untimed for the value above)
+                pl, ln = s2.pipeline, s2.lanes
+                s2.pipeline, s2.lanes = False, None
+                for o in (s2.fe, s2.model):
+                    o.set_timing(True)
+                for _ in range(5):
+                    s2()
+                torch.cuda.synchronize()
+                for o in (s2.fe, s2.model):
+                    o.set_timing(False)
+                s2.pipeline, s2.lanes = pl, ln
+                rows, dom = stage_table([(s2.fe, 5 * s2.n_win, "window"), (s2.model, 5 * s2.n_win, "window")], prec)
+                e["roofline"] = dict(dom, timed_on="HIP events around every launch of 5 serial steps", stages=rows)
             if mode != "cold" and not mode.startswith("pool") and ref is not None:
                 s2.k, s2.issued = 0, -1
                 s2()

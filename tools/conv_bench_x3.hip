@@ -51,12 +51,12 @@ static void time_one(const char* tag, int n, int Hin, int Win, int cout, const v
 }
 
 template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int OCC, bool IS, bool OS,
-          int DIAG = 0>
+          int DIAG = 0, int WO = 2, int NPASS = 1>
 static void time_wg(const char* tag, int n, int Hin, int Win, int cout, const void* in, const void* w, const float* b,
                     void* out, int iters) {
-    auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IS, OS, DIAG>;
+    auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IS, OS, DIAG, WO, NPASS>;
     constexpr int BN = WN * NF * 16;
-    const size_t lds = wg_lds_bytes<KH, BN, TH, TW>();
+    const size_t lds = wg_lds_bytes<KH, BN, TH, TW, WO, NPASS>();
     if (lds > 160 * 1024) { printf("%s LDS %zu: skip\n", tag, lds); return; }
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     const int Hc = Hin - KH + 1, Wc = Win - 3 + 1;
@@ -79,8 +79,8 @@ static void time_wg(const char* tag, int n, int Hin, int Win, int cout, const vo
     (void)hipEventElapsedTime(&ms, e0, e1);
     const float us = 1e3f * ms / iters;
     const double fl = 2.0 * n * Hc * Wc * KH * 3 * CIN * cout;
-    printf("%-6s wg d%d %dx3 cin %3d WM%d WN%d MF%d NF%d %2dx%2d occ%d LDS %6zu grid %6d  %7.1f us  %6.1f TF (%.3f of 833)\n",
-           tag, DIAG, KH, CIN, WM, WN, MF, NF, TH, TW, OCC, lds, grid.x * grid.y * grid.z, us, fl / us * 1e-6,
+    printf("%-6s wg%d d%d %dx3 cin %3d WM%d WN%d MF%d NF%d %2dx%2d occ%d LDS %6zu grid %6d  %7.1f us  %6.1f TF (%.3f of 833)\n",
+           tag, WO, DIAG, KH, CIN, WM, WN, MF, NF, TH, TW, OCC, lds, grid.x * grid.y * grid.z, us, fl / us * 1e-6,
            fl / us * 1e-6 / 833.3);
 }
 
@@ -166,6 +166,15 @@ int main(int argc, char** argv) {
         FS(0) S3(4, 2, 3, 2, 10, 18, true, false, 4) S4(2, 2, 3, 2, 12, 8, true, true, 0)
         W5(2, 2, 4, 2, 39, 6, 2, 0) S6(2, 2, 3, 2, 7, 12, true, true, 0)
         FS(2) FS(64) FS(4) FS(128) FS(16) FS(512) FS(576) FS(0)
+        return 0;
+    }
+    if (which == 30) {  // Winograd 9x3: F(2,3) (round 4) vs F(6,3) (round 5), ablations (1 no staging, 2 no MFMA)
+#define W5O(WM, WN, MF, NF, TH, TW, O, D, WO) time_wg<9, 64, WM, WN, MF, NF, 3, TH, TW, O, true, true, D, WO>("c5", n, 48, 70, 128, in, w, b, out, it);
+        W5O(2, 2, 4, 2, 39, 6, 2, 0, 2) W5O(1, 4, 3, 1, 39, 6, 2, 0, 6)
+        W5O(2, 2, 4, 2, 39, 6, 2, 1, 2) W5O(1, 4, 3, 1, 39, 6, 2, 1, 6)
+        W5O(2, 2, 4, 2, 39, 6, 2, 2, 2) W5O(1, 4, 3, 1, 39, 6, 2, 2, 6)
+        W5O(2, 2, 4, 2, 39, 6, 2, 3, 2) W5O(1, 4, 3, 1, 39, 6, 2, 3, 6)
+        W5O(1, 4, 3, 1, 39, 6, 0, 0, 6) W5O(1, 4, 3, 1, 39, 6, 3, 0, 6)
         return 0;
     }
     if (which == 21) {  // the shipped fused kernel, three timings (variant A/B across builds)
