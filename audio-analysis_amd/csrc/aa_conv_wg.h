@@ -316,6 +316,7 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                 }
             }
             __syncthreads();
+            if constexpr (AA_WG_PRIO > 0) __builtin_amdgcn_s_setprio(AA_WG_PRIO);  // (A/B knob, as AA_X3_PRIO)
             if constexpr ((DIAG & 2) == 0) {
                 if constexpr (PPS % 2 == 0) {
                     // an even count of steps per row: the B sets alternate the same way every row
@@ -342,6 +343,7 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
                     });
                 }
             }
+            if constexpr (AA_WG_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         });
     });
     __syncthreads();  // planes no longer needed: the f32 tile reuses LDS

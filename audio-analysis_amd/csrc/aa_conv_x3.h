@@ -72,6 +72,16 @@ constexpr int X3_CG = 32;  // channels per staged group
 #ifndef AA_PIN_X3
 #define AA_PIN_X3 3
 #endif
+// MFMA steps at issue priority 1 (s_setprio) in conv_x3 and conv_wg: in-pipeline
+// A/B, 3 rounds on one box, step 259.2k -> 261.6k audio-s/s (both) -- the
+// other batch's front end and the co-resident blocks' staging VALU fill the
+// slots the matrix pipe leaves instead of delaying its issue
+#ifndef AA_X3_PRIO
+#define AA_X3_PRIO 1
+#endif
+#ifndef AA_WG_PRIO
+#define AA_WG_PRIO 1
+#endif
 #ifndef AA_PIN_WG
 #define AA_PIN_WG 3
 #endif
@@ -790,11 +800,16 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         // are discarded by the epilogue
         const bool wave_idle = oh0 + (wm * MF * 16) / TW >= Hout * POOL;
         if constexpr (DIAG & 4096) ts[1] = __builtin_amdgcn_s_memtime();
+        // AA_X3_PRIO (A/B knob): the wave's MFMA steps at a raised issue
+        // priority, so waves of co-resident blocks still staging (VALU) fill
+        // the slots the matrix pipe leaves instead of delaying its issue
+        if constexpr (AA_X3_PRIO > 0) __builtin_amdgcn_s_setprio(AA_X3_PRIO);
 #pragma unroll
         for (int t = 0; t < ((DIAG & 2) || wave_idle ? 0 : NTAP); t += 2) {
             step(F0, F1, g, t);
             if (t + 1 < NTAP) step(F1, F0, g, t + 1);
         }
+        if constexpr (AA_X3_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         if constexpr (DIAG & 4096) ts[2] = __builtin_amdgcn_s_memtime();
     }
 #undef X3_GLDS
