@@ -86,13 +86,18 @@ def test_spectrogram_bit_exact(gpu, n, seed):
     _assert_s_equal(got, want)
 
 
-@pytest.mark.parametrize("variant", ["r8", "base"])
+@pytest.mark.parametrize("variant", ["r8", "base", "table"])
 @pytest.mark.parametrize("n,seed", [(60 * SR, 35), (7 * SR + 999, 36), (5000, 37)])
 def test_spectrogram_variants_bit_exact(gpu, monkeypatch, variant, n, seed):
     """Both STFT kernels (sn_stft64: 128 threads, 16 x 16 x 8; sn_stft64r8: 256
-    threads, 8 x 8 x 8 x 4; AA_SN_STFT picks one at plan creation) give the
-    reference's magnitudes, and the detector built on either gives its mask."""
-    monkeypatch.setenv("AA_SN_STFT", variant)
+    threads, 8 x 8 x 8 x 4; AA_SN_STFT picks one at plan creation), and
+    sn_stft64 with every twiddle from the tables instead of the default
+    W, W^2, W^4 ladders (AA_SN_TW=table), give the reference's magnitudes, and
+    the detector built on any of them gives its mask."""
+    if variant == "table":
+        monkeypatch.setenv("AA_SN_TW", "table")
+    else:
+        monkeypatch.setenv("AA_SN_STFT", variant)
     x = _clip(n / SR, seed)
     det = _det(gpu)
     got = det.spectrogram(torch.from_numpy(x).to(gpu)).cpu().numpy()
