@@ -173,6 +173,10 @@ def parse_args(argv=None):
 
 def main(argv=None):
     from .analyse import init_logging
+    # hardware queues for the batch lanes' compute + copy streams (HIP's
+    # default 4 puts some of them on one queue; read once, before the first
+    # GPU call of the process: bench.py does the same)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     args = parse_args(argv)
     init_logging()
     if "WORLD_SIZE" in os.environ:

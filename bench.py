@@ -36,6 +36,13 @@ import tempfile
 import time
 from pathlib import Path
 
+# hardware queues per process: HIP maps streams onto them round-robin, and two
+# streams on one queue run back to back.  The corpus path keeps 3 lanes x
+# (compute + copy) streams busy beside the headline's two lanes; HIP's default
+# of 4 queues made some of them share (configs[3] line 108.5k -> 121.1k with 8,
+# same box; profiles/r05/hw_queues.txt).  Read once, at HIP's initialisation.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 ROOT = Path(__file__).resolve().parent
 for p in (str(ROOT), str(ROOT / "audio-analysis_amd")):
     if p not in sys.path:
@@ -248,6 +255,23 @@ def load_profiled_stages(traffic, precision):
     return None
 
 
+# The lanes' HIP streams, shared by every Step of the process: HIP maps
+# streams onto a few hardware queues (GPU_MAX_HW_QUEUES = 4) round-robin in
+# creation order, and two lanes whose streams land on one queue run back to
+# back -- a secondary measured after the headline had its two lanes on one
+# queue (the efficientnet route 52k standalone, 41k as a secondary: its serial
+# rate).  Reusing the headline's streams keeps every run's lanes on distinct
+# queues.
+_LANE_STREAMS = {}
+
+
+def lane_stream(dev, j):
+    key = (str(dev), j)
+    if key not in _LANE_STREAMS:
+        _LANE_STREAMS[key] = torch.cuda.Stream(device=dev)
+    return _LANE_STREAMS[key]
+
+
 class Step:
     """One configs[1] step on one device: FE -> model -> track mean, with the
     buffers of ``pairs`` resident clip pairs (1 = the headline; COLD_POOL =
@@ -285,7 +309,7 @@ class Step:
             self.lanes = []
             for j in range(int(pipeline)):
                 self.lanes.append(dict(
-                    s=torch.cuda.Stream(device=dev), logmel=self.logmel if j == 0 else torch.empty_like(self.logmel),
+                    s=lane_stream(dev, j), logmel=self.logmel if j == 0 else torch.empty_like(self.logmel),
                     fe_ws=self.fe_ws if j == 0 else torch.empty_like(self.fe_ws),
                     m_ws=self.m_ws if j == 0 else torch.empty_like(self.m_ws),
                     logits=self.logits if j == 0 else torch.empty_like(self.logits),
@@ -297,7 +321,7 @@ class Step:
         if self.pipeline:
             # batch k+1's front end on s_fe into buffer (k+1) % 2 while the CNN
             # of batch k reads buffer k % 2 on the current stream
-            self.s_fe = torch.cuda.Stream(device=dev)
+            self.s_fe = lane_stream(dev, "fe")
             self.lm2 = [self.logmel, torch.empty_like(self.logmel)]
             self.ws2 = [self.fe_ws, torch.empty_like(self.fe_ws)]
             self.fe_done = [torch.cuda.Event(), torch.cuda.Event()]
