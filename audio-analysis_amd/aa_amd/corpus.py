@@ -54,6 +54,12 @@ def gather_documents(local: dict, device=None, group=None) -> dict:
     return dict(sorted(out.items()))
 
 
+# host lanes (threads, each with its own HIP streams) of the batched path: 5
+# with 8 hardware queues measured 138k audio-s/s against 131k (4) and 117k
+# (3) on one box, three rounds each (profiles/r05/corpus_lanes.txt)
+DEFAULT_LANES = 5
+
+
 def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world=1, device=None, batch=16):
     """Classify this rank's share of ``files``; returns {file_idx: summary}
     of ALL files on every rank (after the gather).  ``summary`` is what
@@ -65,7 +71,7 @@ def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world
     if examine_fn is None and batch and torch.cuda.is_available():
         from .batch import BatchAnalyser
         ba = BatchAnalyser(bird_models, analyse_tracks, device=torch.device("cuda", torch.cuda.current_device()),
-                           batch=batch, lanes=int(os.environ.get("AA_BATCH_LANES", "3")))
+                           batch=batch, lanes=int(os.environ.get("AA_BATCH_LANES", str(DEFAULT_LANES))))
         return gather_documents(ba.run([(i, str(f)) for i, f in mine]), device=device)
     if examine_fn is None:
         from .analyse import examine as examine_fn

@@ -877,7 +877,7 @@ def run_corpus(args, world, rank, dev, files=None, roofline=False):
     # warm-up (untimed): plans, kernels, model upload, and every pinned staging
     # slot the timed run holds (aa_amd.batch: (lanes + 2) batches; a slot pool
     # grown inside the timed run allocated ~6 MB of pinned memory per slot there)
-    lanes = int(os.environ.get("AA_BATCH_LANES", "3"))
+    lanes = int(os.environ.get("AA_BATCH_LANES", str(corpus.DEFAULT_LANES)))
     corpus.run([files[0]] * (max(4, lanes + 2) * max(args.batch, 1)), models, rank=0, world=1, batch=args.batch)
     torch.cuda.synchronize()
     if world > 1:
