@@ -145,16 +145,22 @@ __device__ __forceinline__ void leaky_split2(float x0, float x1, float a, uint32
     typedef __attribute__((ext_vector_type(2))) float f2;
     typedef __attribute__((ext_vector_type(2))) __bf16 b2;
 #if AA_X3_SCALAR_SPLIT
-    // scalar f32 ops only (packed f32 VALU costs extra issue beside MFMAs)
-    float o0, o1, r0, r1;
-    asm("v_mul_f32 %0, %1, %2" : "=v"(r0) : "v"(x0), "v"(a));
-    asm("v_mul_f32 %0, %1, %2" : "=v"(r1) : "v"(x1), "v"(a));
+    // scalar f32 ops only (packed f32 VALU costs extra issue beside MFMAs).
+    // The products are compiler-visible because x0 / x1 usually come straight
+    // from an MFMA: the hazard recognizer pads the first VALU read of an MFMA
+    // result with the wait states the matrix pipe needs, but it does not see
+    // into inline asm -- an asm read right behind the MFMA took stale
+    // registers (conv_wgf, whose activation follows its first-layer MFMA
+    // directly).  The asm maxes below depend on r0 / r1, so they come later.
+    float o0, o1;
+    const float r0 = x0 * a, r1 = x1 * a;
     asm("v_max_f32 %0, %1, %2" : "=v"(o0) : "v"(x0), "v"(r0));
     asm("v_max_f32 %0, %1, %2" : "=v"(o1) : "v"(x1), "v"(r1));
     hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{o0, o1}, b2));
-    asm("v_sub_f32 %0, %1, %2" : "=v"(r0) : "v"(o0), "v"(__uint_as_float(hi << 16)));
-    asm("v_sub_f32 %0, %1, %2" : "=v"(r1) : "v"(o1), "v"(__uint_as_float(hi & 0xffff0000u)));
-    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{r0, r1}, b2));
+    float s0, s1;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(s0) : "v"(o0), "v"(__uint_as_float(hi << 16)));
+    asm("v_sub_f32 %0, %1, %2" : "=v"(s1) : "v"(o1), "v"(__uint_as_float(hi & 0xffff0000u)));
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{s0, s1}, b2));
 #else
     const f2 s = f2{x0, x1} * a;
     float o0, o1;

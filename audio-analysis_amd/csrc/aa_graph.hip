@@ -147,21 +147,26 @@ constexpr int GP4_STRIPES = 32;
 // fixed (pixel order within a stripe, a fixed combine tree), the same in the
 // pool and in the fused dwconv + pool: float4 loads give 16 lanes 256
 // contiguous bytes per pixel.
+// Stripe s sums the columns ox = s, s + GP4_STRIPES, ... of the map, each
+// from its top row down (the order gdwconv_pool4 produces its pixels in, so a
+// fused depthwise conv + pool and the two separate nodes give the same bits).
 template <int Q>
 __global__ __launch_bounds__(Q * GP4_STRIPES) void ggpool4(const float* __restrict__ in, float* __restrict__ out,
-                                                         int HW, int C, int avg, int act, float alpha) {
+                                                         int H, int W, int C, int avg, int act, float alpha) {
     __shared__ float part[GP4_STRIPES][4 * Q];
     const int cq = threadIdx.x % Q, s = threadIdx.x / Q;
     const int c = blockIdx.x * 4 * Q + 4 * cq;
     const int n = blockIdx.y;
+    const int HW = H * W;
     float4 m = avg ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
     if (c < C) {
         const float* p = in + (size_t)n * HW * C + c;
-        for (int i = s; i < HW; i += GP4_STRIPES) {
-            const float4 v = *reinterpret_cast<const float4*>(p + (size_t)i * C);
-            if (avg) { m.x += v.x; m.y += v.y; m.z += v.z; m.w += v.w; }
-            else { m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w); }
-        }
+        for (int ox = s; ox < W; ox += GP4_STRIPES)
+            for (int oy = 0; oy < H; ++oy) {
+                const float4 v = *reinterpret_cast<const float4*>(p + ((size_t)oy * W + ox) * C);
+                if (avg) { m.x += v.x; m.y += v.y; m.z += v.z; m.w += v.w; }
+                else { m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w); }
+            }
     }
     part[s][4 * cq] = m.x; part[s][4 * cq + 1] = m.y; part[s][4 * cq + 2] = m.z; part[s][4 * cq + 3] = m.w;
     __syncthreads();
@@ -181,7 +186,11 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void ggpool4(const float* __restri
 }
 
 // KS = 3: a 3x3 kernel, the taps unrolled and their weights held in
-// registers for every pixel; KS = 0: any kernel, weights re-read per tap
+// registers for every pixel; KS = 0: any kernel, weights re-read per tap.
+// Thread = (channel quad, column stripe s): it walks the columns ox = s, s +
+// GP4_STRIPES, ... top to bottom, so a stride-1 3x3 conv keeps its 3 x 3
+// input window in registers and loads one new row of 3 pixels per output
+// (3 float4 loads instead of 9); other shapes load their taps per pixel.
 template <int Q, int KS>
 __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
     const float* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out,
@@ -204,37 +213,72 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
             for (int t = 0; t < NW; ++t) wr[t] = *reinterpret_cast<const float4*>(w + t * C + c);
         }
         const int KH = KS ? KS : kh, KW = KS ? KS : kw;
-        // the pixel's (row, column), stepped on by the stripe count (no
-        // integer division per pixel)
-        int oy = s / Wout, ox = s - (s / Wout) * Wout;
-        for (int P = s; P < HW; P += GP4_STRIPES) {
-            float4 acc = b;
-#pragma unroll
-            for (int ky = 0; ky < KH; ++ky) {
-                const int iy = oy * sh - pt + ky;
-                if (iy < 0 || iy >= Hin) continue;
-#pragma unroll
-                for (int kx = 0; kx < KW; ++kx) {
-                    const int ix = ox * sw - pl + kx;
-                    if (ix < 0 || ix >= Win) continue;
-                    float4 wv;
-                    if constexpr (KS > 0) wv = wr[ky * KS + kx];
-                    else wv = *reinterpret_cast<const float4*>(w + (ky * kw + kx) * C + c);
-                    const float4 x = *reinterpret_cast<const float4*>(img + ((size_t)iy * Win + ix) * C);
-                    acc.x = fmaf(wv.x, x.x, acc.x);
-                    acc.y = fmaf(wv.y, x.y, acc.y);
-                    acc.z = fmaf(wv.z, x.z, acc.z);
-                    acc.w = fmaf(wv.w, x.w, acc.w);
-                }
-            }
+        auto fma4 = [](float4& acc, const float4& wv, const float4& x) {
+            acc.x = fmaf(wv.x, x.x, acc.x);
+            acc.y = fmaf(wv.y, x.y, acc.y);
+            acc.z = fmaf(wv.z, x.z, acc.z);
+            acc.w = fmaf(wv.w, x.w, acc.w);
+        };
+        auto emit = [&](int oy, int ox, const float4& acc) {
             const float4 y = make_float4(gact(acc.x, act, alpha), gact(acc.y, act, alpha), gact(acc.z, act, alpha),
                                          gact(acc.w, act, alpha));
-            *reinterpret_cast<float4*>(o + (size_t)P * C) = y;
+            *reinterpret_cast<float4*>(o + ((size_t)oy * Wout + ox) * C) = y;
             m.x += y.x; m.y += y.y; m.z += y.z; m.w += y.w;
-            ox += GP4_STRIPES;
-            while (ox >= Wout) {
-                ox -= Wout;
-                ++oy;
+        };
+        const bool slide = KS == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && Hout == Hin && Wout == Win;
+        for (int ox = s; ox < Wout; ox += GP4_STRIPES) {
+            if (slide) {
+                // window rows r = 0..2 hold input rows oy - 1 .. oy + 1 at columns ox - 1 .. ox + 1
+                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 x[3][3];
+                auto ld = [&](int iy, int ix) -> float4 {
+                    return (iy >= 0 && iy < Hin && ix >= 0 && ix < Win)
+                               ? *reinterpret_cast<const float4*>(img + ((size_t)iy * Win + ix) * C)
+                               : z;
+                };
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) {
+                    x[0][cc] = z;
+                    x[1][cc] = ld(0, ox - 1 + cc);
+                }
+                for (int oy = 0; oy < Hout; ++oy) {
+#pragma unroll
+                    for (int cc = 0; cc < 3; ++cc) x[2][cc] = ld(oy + 1, ox - 1 + cc);
+                    float4 acc = b;
+#pragma unroll
+                    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                        for (int kx = 0; kx < 3; ++kx) {
+                            // the per-pixel path skips padding taps; a zero tap adds
+                            // +0 * w: the same sum unless w is inf / nan
+                            fma4(acc, wr[KS ? ky * KS + kx : 0], x[ky][kx]);
+                        }
+                    emit(oy, ox, acc);
+#pragma unroll
+                    for (int cc = 0; cc < 3; ++cc) {
+                        x[0][cc] = x[1][cc];
+                        x[1][cc] = x[2][cc];
+                    }
+                }
+                continue;
+            }
+            for (int oy = 0; oy < Hout; ++oy) {
+                float4 acc = b;
+#pragma unroll
+                for (int ky = 0; ky < KH; ++ky) {
+                    const int iy = oy * sh - pt + ky;
+                    if (iy < 0 || iy >= Hin) continue;
+#pragma unroll
+                    for (int kx = 0; kx < KW; ++kx) {
+                        const int ix = ox * sw - pl + kx;
+                        if (ix < 0 || ix >= Win) continue;
+                        float4 wv;
+                        if constexpr (KS > 0) wv = wr[ky * KS + kx];
+                        else wv = *reinterpret_cast<const float4*>(w + (ky * kw + kx) * C + c);
+                        fma4(acc, wv, *reinterpret_cast<const float4*>(img + ((size_t)iy * Win + ix) * C));
+                    }
+                }
+                emit(oy, ox, acc);
             }
         }
     }
@@ -1031,7 +1075,7 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
         case AA_G_GAVGPOOL:
             if ((Cin & 3) == 0)
                 hipLaunchKernelGGL((ggpool4<16>), dim3((Cin + 63) / 64, n), dim3(16 * GP4_STRIPES), 0, st, a, out,
-                                   Hin * Win, Cin, d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
+                                   Hin, Win, Cin, d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);
             else
                 hipLaunchKernelGGL(ggpool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a, out, Hin * Win,
                                    Cin, d.op == AA_G_GAVGPOOL ? 1 : 0, act, d.alpha);

@@ -1,0 +1,227 @@
+// Diagnostic harness: conv_wgf (fused first layer + F(6,3) 3x3/32 pooled
+// conv) against a float64 CPU reference on random inputs, with the error
+// pattern by output position / channel, and its time at the bench's shape.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include
+//   tools/wgf_check.hip audio-analysis_amd/csrc/aa_api.cpp -o tools/wgf_check ; run on the GPU box.
+#include "../audio-analysis_amd/csrc/aa_cnn.hip"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace aa;
+
+// fills every CU's LDS with a NaN pattern (a dirty-LDS precondition for the check)
+__global__ void dirty_lds(int words) {
+    extern __shared__ uint32_t sm[];
+    for (int i = threadIdx.x; i < words; i += blockDim.x) sm[i] = 0x7fc00000u + (i & 0xff);
+    __syncthreads();
+    if (sm[(threadIdx.x * 7) % words] == 1u) sm[0] = 2u;  // keep the stores
+}
+
+static double urand(uint64_t& s) {
+    s = s * 6364136223846793005ull + 1442695040888963407ull;
+    return ((s >> 11) * (1.0 / 9007199254740992.0)) * 2.0 - 1.0;
+}
+
+int main(int argc, char** argv) {
+    constexpr int TH = 48, TW = 6, WM = 3, WN = 1, MF = 1, NF = 2;
+    const int n = argc > 1 ? atoi(argv[1]) : 2;
+    const int H0 = 160, W0 = 226, H1 = H0 - 2, W1 = W0 - 2, Hc = H1 - 2, Wc = W1 - 2, Ho = Hc / 3, Wo = Wc / 3;
+    uint64_t seed = 12345;
+    std::vector<float> x((size_t)n * H0 * W0), w1(32 * 9), b1(32), k2(9 * 32 * 32), b2(32);
+    const bool db = argc > 3 && strchr(argv[3], 'd');   // dB-like input: -45 +- 13, clipped to [-80, 0]
+    const bool osplit = argc > 3 && strchr(argv[3], 's');  // grouped-split output
+    for (auto& v : x) v = db ? (float)std::min(0.0, std::max(-80.0, -45.0 + 20.0 * urand(seed))) : (float)urand(seed);
+    for (auto& v : w1) v = (float)(0.5 * urand(seed));
+    for (auto& v : b1) v = (float)(0.1 * urand(seed));
+    for (auto& v : k2) v = (float)(0.1 * urand(seed));  // [tap][cin][cout]
+    for (auto& v : b2) v = (float)(0.1 * urand(seed));
+    const float slope = 0.3f;
+    if (const char* dir = getenv("WGF_DATA")) {  // folded weights + input written by tools/wgf_model_check.py --dump
+        auto rd = [&](const char* nm, std::vector<float>& v) {
+            char path[512];
+            snprintf(path, sizeof path, "%s/%s.bin", dir, nm);
+            FILE* f = fopen(path, "rb");
+            if (!f || fread(v.data(), 4, v.size(), f) != v.size()) { printf("cannot read %s\n", path); exit(2); }
+            fclose(f);
+        };
+        rd("x", x); rd("w1", w1); rd("b1", b1); rd("k2", k2); rd("b2", b2);
+    }
+    // float64 reference
+    std::vector<double> a1((size_t)n * H1 * W1 * 32);
+    for (int b = 0; b < n; ++b)
+        for (int r = 0; r < H1; ++r)
+            for (int c = 0; c < W1; ++c)
+                for (int o = 0; o < 32; ++o) {
+                    double s = b1[o];
+                    for (int t = 0; t < 9; ++t) s += (double)w1[o * 9 + t] * x[((size_t)b * H0 + r + t / 3) * W0 + c + t % 3];
+                    a1[(((size_t)b * H1 + r) * W1 + c) * 32 + o] = s > 0 ? s : slope * s;
+                }
+    std::vector<double> ref((size_t)n * Ho * Wo * 32, -1e300);
+    for (int b = 0; b < n; ++b)
+        for (int r = 0; r < Ho * 3; ++r)
+            for (int c = 0; c < Wo * 3; ++c)
+                for (int o = 0; o < 32; ++o) {
+                    double s = b2[o];
+                    for (int t = 0; t < 9; ++t)
+                        for (int i = 0; i < 32; ++i)
+                            s += (double)k2[(t * 32 + i) * 32 + o] * a1[(((size_t)b * H1 + r + t / 3) * W1 + c + t % 3) * 32 + i];
+                    s = s > 0 ? s : slope * s;
+                    double& m = ref[(((size_t)b * Ho + r / 3) * Wo + c / 3) * 32 + o];
+                    m = std::max(m, s);
+                }
+    // conv_wg weight packing (aa_cnn.hip): step kh * 8 + e, [32 rows][8 units]
+    std::vector<uint16_t> hw((size_t)3 * 8 * 32 * 64 * 2 + 1024, 0);
+    for (int kh = 0; kh < 3; ++kh)
+        for (int o = 0; o < 32; ++o)
+            for (int c = 0; c < 32; ++c) {
+                double w3[3];
+                for (int kw = 0; kw < 3; ++kw) w3[kw] = k2[((kh * 3 + kw) * 32 + c) * 32 + o];
+                for (int e = 0; e < 8; ++e) {
+                    const double v = wg_g(6, e, 0) * w3[0] + wg_g(6, e, 1) * w3[1] + wg_g(6, e, 2) * w3[2];
+                    const size_t row = ((size_t)(kh * 8 + e) * 32 + o) * 64;
+                    const float wf = (float)v;
+                    const uint16_t hi = f2bf(wf);
+                    const int u = c / 8;
+                    hw[row + ((u + o) & 7) * 8 + c % 8] = hi;
+                    hw[row + ((u + 4 + o) & 7) * 8 + c % 8] = f2bf(wf - bf2f(hi));
+                }
+            }
+    float *dx, *dw1, *db1, *db2, *dout;
+    void* dw;
+    (void)hipMalloc(&dx, x.size() * 4);
+    (void)hipMalloc(&dw1, w1.size() * 4);
+    (void)hipMalloc(&db1, 32 * 4);
+    (void)hipMalloc(&db2, 32 * 4);
+    (void)hipMalloc(&dw, hw.size() * 2);
+    (void)hipMalloc(&dout, (size_t)n * Ho * Wo * 32 * 4);
+    (void)hipMemcpy(dx, x.data(), x.size() * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(dw1, w1.data(), w1.size() * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(db1, b1.data(), 32 * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(db2, b2.data(), 32 * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(dw, hw.data(), hw.size() * 2, hipMemcpyHostToDevice);
+    (void)hipMemset(dout, 0, (size_t)n * Ho * Wo * 32 * 4);
+    const FirstConv fc{dw1, db1, ACT_LEAKY, slope, 0, 1.f, H0, W0, 0};
+    auto k = osplit ? conv_wgf<TH, TW, WM, WN, MF, NF, 0, true, 2, 2> : conv_wgf<TH, TW, WM, WN, MF, NF, 0, false, 2, 2>;
+    const size_t lds = wgf_lds_bytes<TH, TW, 32>();
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const int tiles_h = (Ho * 3 + TH - 1) / TH, tiles_w = (Wo * 3 + TW - 1) / TW;
+    dim3 grid(tiles_h * tiles_w, 1, n);
+    const bool dirty = argc > 3 && strchr(argv[3], 'z');
+    if (dirty) {
+        (void)hipFuncSetAttribute((const void*)dirty_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipLaunchKernelGGL(dirty_lds, dim3(4096), dim3(256), 160 * 1024, 0, 40960);
+        (void)hipMemset(dout, 0xff, (size_t)n * Ho * Wo * 32 * 4);  // unwritten outputs read as NaN
+    }
+    hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, 0, dx, H1, W1, (const bf16*)dw, db2, dout, Ho, Wo, 32, tiles_w,
+                       ACT_LEAKY, slope, fc);
+    if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
+    std::vector<float> out((size_t)n * Ho * Wo * 32);
+    (void)hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost);
+    if (osplit) {  // grouped split: per pixel 32 bf16 hi then 32 bf16 lo
+        std::vector<float> f(out.size());
+        const uint16_t* hs = reinterpret_cast<const uint16_t*>(out.data());
+        for (size_t px = 0; px < out.size() / 32; ++px)
+            for (int c = 0; c < 32; ++c) f[px * 32 + c] = bf2f(hs[px * 64 + c]) + bf2f(hs[px * 64 + 32 + c]);
+        out.swap(f);
+    }
+    double mx = 0, scale = 0;
+    std::vector<double> by_row(16, 0), by_col(2, 0), by_ch(32, 0), by_tile_r(8, 0);
+    for (int b = 0; b < n; ++b)
+        for (int r = 0; r < Ho; ++r)
+            for (int c = 0; c < Wo; ++c)
+                for (int o = 0; o < 32; ++o) {
+                    const size_t i = (((size_t)b * Ho + r) * Wo + c) * 32 + o;
+                    const double d = std::isnan(out[i]) ? 1e30 : std::fabs(out[i] - ref[i]);
+                    mx = std::max(mx, d);
+                    scale = std::max(scale, std::fabs(ref[i]));
+                    by_row[r % 16] = std::max(by_row[r % 16], d);
+                    by_col[c % 2] = std::max(by_col[c % 2], d);
+                    by_ch[o] = std::max(by_ch[o], d);
+                    by_tile_r[r / 16] = std::max(by_tile_r[r / 16], d);
+                }
+    printf("conv_wgf %dx%d: max |err| %.3e (|ref| up to %.3f), LDS %zu\n", TH, TW, mx, scale, lds);
+    printf("by pooled row %% 16:");
+    for (double v : by_row) printf(" %.1e", v);
+    printf("\nby pooled col %% 2: %.1e %.1e\nby channel:", by_col[0], by_col[1]);
+    for (double v : by_ch) printf(" %.1e", v);
+    printf("\nby tile row:");
+    for (double v : by_tile_r) printf(" %.1e", v);
+    printf("\nsample (0,0,0,0..7): ");
+    for (int o = 0; o < 8; ++o) printf("%.4f/%.4f ", out[o], ref[o]);
+    printf("\n");
+    if (argc > 2 && argv[2][0] == 'a') {  // ablations / variants at the bench's 64 windows
+        const int nb = 64;
+        float *big, *bo;
+        (void)hipMalloc(&big, (size_t)nb * H0 * W0 * 4);
+        (void)hipMemset(big, 0, (size_t)nb * H0 * W0 * 4);
+        (void)hipMalloc(&bo, (size_t)nb * Ho * Wo * 32 * 4);
+        dim3 g2(tiles_h * tiles_w, 1, nb);
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        auto run = [&](const char* tag, auto kern, size_t ldsb, int nthr) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsb);
+            for (int i = 0; i < 3; ++i)
+                hipLaunchKernelGGL(kern, g2, dim3(nthr), ldsb, 0, big, H1, W1, (const bf16*)dw, db2, bo, Ho, Wo, 32,
+                                   tiles_w, ACT_LEAKY, slope, fc);
+            (void)hipEventRecord(e0, 0);
+            for (int i = 0; i < 20; ++i)
+                hipLaunchKernelGGL(kern, g2, dim3(nthr), ldsb, 0, big, H1, W1, (const bf16*)dw, db2, bo, Ho, Wo, 32,
+                                   tiles_w, ACT_LEAKY, slope, fc);
+            (void)hipEventRecord(e1, 0);
+            (void)hipEventSynchronize(e1);
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            printf("%-28s %7.1f us\n", tag, 1e3f * ms / 20);
+        };
+#define WV(TAG, BD, NU, DG) run(TAG, conv_wgf<TH, TW, WM, WN, MF, NF, 0, false, BD, NU, DG>, lds, WM * WN * 64);
+        WV("base BD2 NU2", 2, 2, 0)
+        WV("no first layer", 2, 2, 1)
+        WV("no main MFMA", 2, 2, 2)
+        WV("no main B loads", 2, 2, 4)
+        WV("first layer only", 2, 2, 6)
+        WV("nothing", 2, 2, 7)
+        WV("BD4", 4, 2, 0)
+        WV("BD8", 8, 2, 0)
+        WV("NU1", 2, 1, 0)
+        WV("NU3", 2, 3, 0)
+#define WX(TAG, WM_, WN_, MF_, NF_, BD, NU, DG) run(TAG, conv_wgf<TH, TW, WM_, WN_, MF_, NF_, 0, false, BD, NU, DG>, lds, WM_ * WN_ * 64);
+        WX("WM1 WN2 MF3 NF1", 1, 2, 3, 1, 2, 2, 0)
+        WX("WM1 WN2 MF3 NF1 BD4", 1, 2, 3, 1, 4, 2, 0)
+        WX("WM1 WN2 MF3 NF1 no first", 1, 2, 3, 1, 2, 2, 1)
+        WX("WM1 WN2 MF3 NF1 nothing", 1, 2, 3, 1, 2, 2, 7)
+        WX("WM3 WN2 MF1 NF1", 3, 2, 1, 1, 2, 2, 0)
+        WX("WM3 WN2 MF1 NF1 BD4", 3, 2, 1, 1, 4, 1, 0)
+        return 0;
+    }
+    if (argc > 2) {  // timing at the bench's 64 windows
+        const int nb = 64;
+        float* big;
+        (void)hipMalloc(&big, (size_t)nb * H0 * W0 * 4);
+        (void)hipMemset(big, 0, (size_t)nb * H0 * W0 * 4);
+        float* bo;
+        (void)hipMalloc(&bo, (size_t)nb * Ho * Wo * 32 * 4);
+        const FirstConv f2{dw1, db1, ACT_LEAKY, slope, 0, 1.f, H0, W0, 0};
+        dim3 g2(tiles_h * tiles_w, 1, nb);
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        for (int i = 0; i < 3; ++i)
+            hipLaunchKernelGGL(k, g2, dim3(WM * WN * 64), lds, 0, big, H1, W1, (const bf16*)dw, db2, bo, Ho, Wo, 32,
+                               tiles_w, ACT_LEAKY, slope, f2);
+        (void)hipEventRecord(e0, 0);
+        for (int i = 0; i < 20; ++i)
+            hipLaunchKernelGGL(k, g2, dim3(WM * WN * 64), lds, 0, big, H1, W1, (const bf16*)dw, db2, bo, Ho, Wo, 32,
+                               tiles_w, ACT_LEAKY, slope, f2);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        printf("64 windows: %.1f us per launch\n", 1e3f * ms / 20);
+    }
+    return mx < 1e-3 * std::max(1.0, scale) ? 0 : 3;
+}

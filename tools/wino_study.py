@@ -74,7 +74,7 @@ def conv_split(x, w, b):
     return (y + b[None, :, None, None]).float().double()
 
 
-def conv_wino(x, w, b, m, pts):
+def conv_wino(x, w, b, m, pts, presplit=False):
     """The kh x 3 valid conv through F(m, 3) along W: input transform in f32,
     weight transform in f64, both split, products exact, output transform in
     f32 (outputs past the last whole group computed on zero columns and cut)."""
@@ -87,7 +87,12 @@ def conv_wino(x, w, b, m, pts):
     xp = F.pad(x, (0, J * m + 2 - W))
     # d[:, :, :, j, t] = x[:, :, :, m j + t]
     d = torch.stack([xp[..., m * j:m * j + a] for j in range(J)], dim=3).float()
-    U = torch.einsum("et,nchjt->nechj", torch.from_numpy(BT).float(), d)  # f32 transform
+    if presplit:  # the transform as an MFMA on the bf16 hi + lo of d (products exact, f32 sums)
+        dh, dl = split(d)
+        U = (torch.einsum("et,nchjt->nechj", torch.from_numpy(BT), dh) +
+             torch.einsum("et,nchjt->nechj", torch.from_numpy(BT), dl)).float()
+    if not presplit:
+        U = torch.einsum("et,nchjt->nechj", torch.from_numpy(BT).float(), d)  # f32 transform
     V = torch.einsum("et,ockt->eock", torch.from_numpy(G), w)  # f64
     M = []
     for e in range(a):
@@ -121,8 +126,10 @@ def forward(arch, tensors, x, wino=None):
                 i += 1
             if not emu:
                 h = F.conv2d(h, w) + b[None, :, None, None]
-            elif wino and tuple(w.shape[2:]) == (9, 3):
-                h = conv_wino(h, w, b, *wino)
+            elif wino and len(wino) > 2 and wino[2] and tuple(w.shape[2:]) == (9, 3):  # the shipped F(6,3) 9x3
+                h = conv_wino(h, w, b, 6, [0, 1, -1, 2, -2, 0.5, -0.5])
+            elif wino and (tuple(w.shape[2:]) == (9, 3) or (len(wino) > 2 and wino[2] and tuple(w.shape[1:]) == (32, 3, 3))):
+                h = conv_wino(h, w, b, *wino[:2], presplit=len(wino) > 3 and wino[3] and tuple(w.shape[2:]) == (3, 3))
             else:
                 h = conv_split(h, w, b)
         elif kind == "leakyrelu":
@@ -141,6 +148,8 @@ def forward(arch, tensors, x, wino=None):
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--windows", type=int, default=64)
+    ap.add_argument("--calib", action="store_true", help="the GPU tests' dB-like inputs (make_models.calibration_input)")
+    ap.add_argument("--first", action="store_true", help="Winograd variants on the 3x3/32 pooled conv (with F(6,3) 9x3)")
     args = ap.parse_args(argv)
     import bench
     from oracle import cnn_oracle, fe_oracle
@@ -150,15 +159,28 @@ def main(argv=None):
     pcm, _, views = bench.make_batch(0, fe_s)
     x = np.stack([fe_oracle.window_logmel(bench.window_samples(pcm, v, cfg["win_len"]), cfg)
                   for v in views[:args.windows]]).astype(np.float32)
+    if args.calib:
+        from tools.make_models import calibration_input
+        x = calibration_input(6, 160, 226, True, np.random.default_rng(226 + 6))
+    print(f"input {x.shape} mean {x.mean():.2f} std {x.std():.2f}")
     torch.set_num_threads(8)
     p = make_model(Path(tempfile.mkdtemp()) / "model1", "model1", seed=1)
     arch, tensors = cnn_oracle.load_arch(p)
     ref = forward(arch, tensors, x, wino=False)
     print(f"logits {ref.min():.3f} .. {ref.max():.3f}")
-    for name, wino in [("direct split-bf16", None), ("F(2,3) {0,1,-1}", (2, [0, 1, -1])),
+    variants = [("F(6,3) 9x3 + 3x3/32 presplit", (6, [0, 1, -1, 2, -2, 0.5, -0.5], True, True)),
+                       ("F(6,3) 9x3 + 3x3/32", (6, [0, 1, -1, 2, -2, 0.5, -0.5], True)),
+                       ("F(6,3) 9x3 only", (6, [0, 1, -1, 2, -2, 0.5, -0.5])),
+                       ("direct split-bf16", None), ("F(2,3) {0,1,-1}", (2, [0, 1, -1])),
                        ("F(3,3) {0,1,-1,2}", (3, [0, 1, -1, 2])), ("F(3,3) {0,1,-1,1/2}", (3, [0, 1, -1, 0.5])),
                        ("F(4,3) {0,1,-1,2,-2}", (4, [0, 1, -1, 2, -2])),
-                       ("F(4,3) {0,1,-1,1/2,-1/2}", (4, [0, 1, -1, 0.5, -0.5]))]:
+                       ("F(4,3) {0,1,-1,1/2,-1/2}", (4, [0, 1, -1, 0.5, -0.5]))]
+    if args.first:
+        variants = [("direct split-bf16", None)] + [
+            (f"3x3/32 F({m},3) {pts}", (m, pts, True, True)) for m, pts in
+            [(2, [0, 1, -1]), (3, [0, 1, -1, 0.5]), (3, [0, 1, -1, 2]), (4, [0, 1, -1, 0.5, -0.5]), (4, [0, 1, -1, 2, -2]),
+             (6, [0, 1, -1, 2, -2, 0.5, -0.5])]]
+    for name, wino in variants:
         lg = forward(arch, tensors, x, wino=wino)
         print(f"{name:28s} max|dlogit| {np.abs(lg - ref).max():.3e}  mean {np.abs(lg - ref).mean():.3e}", flush=True)
 
