@@ -103,10 +103,20 @@ __host__ __device__ constexpr size_t wg_patch_bytes() {
     return (size_t)((WO + 2) / NPASS) * (TH + KH - 1) * (TW / WO) * 128;
 }
 
+// AA_WG_EPH: the epilogue's f32 tile holds BN / AA_WG_EPH channels at a time,
+// the slices stored one after the other.  2 (default): the 9x3 layer's tile
+// 60 -> 30 KiB, so its block's LDS is set by the 48 KiB of planes (72 -> 48
+// KiB); the kernel alone is unchanged (115.5 -> 116 us, 2 waves/SIMD by its
+// 180 VGPRs) but the other stream's blocks find room beside it: step 267.9k ->
+// 270.6k audio-s/s, ahead in each of 3 alternating rounds
+// (profiles/r05/ab_wg_eph.txt)
+#ifndef AA_WG_EPH
+#define AA_WG_EPH 2
+#endif
 template <int KH, int BN, int TH, int TW, int WO, int NPASS>
 constexpr size_t wg_lds_bytes() {
     const size_t main = wg_patch_bytes<KH, TH, TW, WO, NPASS>();
-    const size_t epi = (size_t)TH * TW * BN * 4;
+    const size_t epi = (size_t)TH * TW * (BN / AA_WG_EPH) * 4;
     return main > epi ? main : epi;
 }
 
@@ -352,35 +362,45 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     // layout: a store's 8 lanes hold pixels WO apart, PSH keeps their units in
     // distinct 16-B slots) ----
     constexpr int PSH = wg_psh(WO);
+    constexpr int EH = AA_WG_EPH, WNE = WN / EH, BNE = BN / EH;  // channel slices of the epilogue tile
+    static_assert(WN % EH == 0 && BNE / 4 >= 8, "whole waves per slice, >= 32 channels");
     float* E = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int j = 0; j < NF; ++j) {
-        const int u = wn * NF * 4 + j * 4 + q;
+    for (int h = 0; h < EH; ++h) {
+        if (h > 0) __syncthreads();  // the previous slice's pooled reads are done
+        if (wn / WNE == h) {
 #pragma unroll
-        for (int i = 0; i < MF; ++i) {
-            const int p = (wm * MF + i) * 16 + (lane & 15);
-            if (p < TP) {
-                const int r = p / NP, jp = p - (p / NP) * NP;
-                const int px = r * TW + WO * jp;
+            for (int j = 0; j < NF; ++j) {
+                const int u = (wn % WNE) * NF * 4 + j * 4 + q;
 #pragma unroll
-                for (int k = 0; k < WO; ++k) {
-                    f32x4 y = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int i = 0; i < MF; ++i) {
+                    const int p = (wm * MF + i) * 16 + (lane & 15);
+                    if (p < TP) {
+                        const int r = p / NP, jp = p - (p / NP) * NP;
+                        const int px = r * TW + WO * jp;
 #pragma unroll
-                    for (int e = 0; e < A; ++e) {
-                        const float c = wg_at(WO, k, e);
-                        if (c == 0.f) continue;
-                        if (c == 1.f) y += acc[e][i][j];
-                        else if (c == -1.f) y -= acc[e][i][j];
-                        else y += c * acc[e][i][j];
+                        for (int k = 0; k < WO; ++k) {
+                            f32x4 y = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                            for (int e = 0; e < A; ++e) {
+                                const float c = wg_at(WO, k, e);
+                                if (c == 0.f) continue;
+                                if (c == 1.f) y += acc[e][i][j];
+                                else if (c == -1.f) y -= acc[e][i][j];
+                                else y += c * acc[e][i][j];
+                            }
+                            *reinterpret_cast<float4*>(E + x3_eoff<BNE, PSH>(px + k, u)) =
+                                make_float4(y[0], y[1], y[2], y[3]);
+                        }
                     }
-                    *reinterpret_cast<float4*>(E + x3_eoff<BN, PSH>(px + k, u)) = make_float4(y[0], y[1], y[2], y[3]);
                 }
             }
         }
+        __syncthreads();
+        // slice h of block cb: channels cb BN + h BNE .. (x3_store's channel base is its cb x its BN)
+        x3_store<TH, TW, POOL, BNE, NTHR, OUT_SPLIT, false, PSH>(E, bias, out, n, cb * EH + h, oh0, ow0, Hout, Wout,
+                                                                cout_store, act, alpha);
     }
-    __syncthreads();
-    x3_store<TH, TW, POOL, BN, NTHR, OUT_SPLIT, false, PSH>(E, bias, out, n, cb, oh0, ow0, Hout, Wout, cout_store,
-                                                           act, alpha);
 }
 
 // ---------------------------------------------------------------------------

@@ -101,7 +101,10 @@ constexpr size_t x3_lds_bytes_nb(int nb) {  // nb = 0: no LDS ring (B fragments 
 }
 
 // ring depth: as in conv_ring, deepen while the blocks per CU a 3-deep ring
-// allows stay resident (at most 8 slices, one per step)
+// allows stay resident (at most AA_X3_RING_MAX slices, one per step)
+#ifndef AA_X3_RING_MAX
+#define AA_X3_RING_MAX 8
+#endif
 template <int KH, int KW, int CIN, int BN, int TH, int TW, bool FUSED, bool RING = true>
 constexpr int x3_ring() {
     if (!RING) return 0;
@@ -109,7 +112,8 @@ constexpr int x3_ring() {
     constexpr int NSTEP = KH * KW * (CIN / X3_CG);
     const size_t blocks = cap / x3_lds_bytes_nb<KH, KW, BN, TH, TW, FUSED>(3);
     int nb = 3;  // the pipelined loop reads slice s+1 while s+NB-1 is issued
-    while (nb < 8 && nb < NSTEP && blocks * x3_lds_bytes_nb<KH, KW, BN, TH, TW, FUSED>(nb + 1) <= cap) ++nb;
+    while (nb < AA_X3_RING_MAX && nb < NSTEP && blocks * x3_lds_bytes_nb<KH, KW, BN, TH, TW, FUSED>(nb + 1) <= cap)
+        ++nb;
     return nb;
 }
 
