@@ -1415,9 +1415,13 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
             // the last conv stage and the head in one launch (aa_conv_tail.h):
             // per-tile label maxima into `out`, then head_final over the tiles
             const Stage& c = *first;
-            constexpr int TH = 13, TW = 5;
+#ifndef AA_TAIL_TW  // (A/B knobs: tile width and pixel fragments per wave)
+#define AA_TAIL_TW 5
+#define AA_TAIL_MF 5
+#endif
+            constexpr int TH = 13, TW = AA_TAIL_TW;
             const int tiles_h = (c.Hc + TH - 1) / TH, tiles_w = (c.Wc + TW - 1) / TW;
-            auto k = conv_tail_x3<1, 3, 128, 5, TH, TW>;
+            auto k = conv_tail_x3<1, 3, 128, AA_TAIL_MF, TH, TW>;
             constexpr size_t lds = tail_lds_bytes<1, 3, 128, TH, TW>();
             AA_DYN_LDS(k, lds);
             float* part = static_cast<float*>(out);
