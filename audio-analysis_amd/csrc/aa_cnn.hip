@@ -1315,7 +1315,7 @@ static int launch_wg(const Stage& s, const void* in, void* out, int n, hipStream
     constexpr int BN = WN * NF * 16;
     AA_CHECK((double)s.Hin * s.Win * s.cin * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
              "conv %s: one window's activations exceed 2 GiB", s.name.c_str());
-    const size_t lds = wg_lds_bytes<KH, BN, TH, TW, WO, NPASS>();
+    const size_t lds = wg_lds_bytes<KH, BN, TH, TW, WO, NPASS, WN>();
     AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
     AA_DYN_LDS(k, lds);
     const int tiles_h = (s.Hout * POOL + TH - 1) / TH;

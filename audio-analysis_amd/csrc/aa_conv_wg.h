@@ -113,10 +113,15 @@ __host__ __device__ constexpr size_t wg_patch_bytes() {
 #ifndef AA_WG_EPH
 #define AA_WG_EPH 2
 #endif
-template <int KH, int BN, int TH, int TW, int WO, int NPASS>
+// epilogue slices of a BN-channel block over WN waves: whole waves per slice,
+// at least 32 channels (x3_store's 8 units) each
+__host__ __device__ constexpr int wg_eph(int BN, int WN) {
+    return (AA_WG_EPH > 1 && WN % AA_WG_EPH == 0 && BN / AA_WG_EPH >= 32) ? AA_WG_EPH : 1;
+}
+template <int KH, int BN, int TH, int TW, int WO, int NPASS, int WN = 1>
 constexpr size_t wg_lds_bytes() {
     const size_t main = wg_patch_bytes<KH, TH, TW, WO, NPASS>();
-    const size_t epi = (size_t)TH * TW * (BN / AA_WG_EPH) * 4;
+    const size_t epi = (size_t)TH * TW * (BN / wg_eph(BN, WN)) * 4;
     return main > epi ? main : epi;
 }
 
@@ -362,8 +367,7 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
     // layout: a store's 8 lanes hold pixels WO apart, PSH keeps their units in
     // distinct 16-B slots) ----
     constexpr int PSH = wg_psh(WO);
-    constexpr int EH = AA_WG_EPH, WNE = WN / EH, BNE = BN / EH;  // channel slices of the epilogue tile
-    static_assert(WN % EH == 0 && BNE / 4 >= 8, "whole waves per slice, >= 32 channels");
+    constexpr int EH = wg_eph(BN, WN), WNE = WN / EH, BNE = BN / EH;  // channel slices of the epilogue tile
     float* E = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int h = 0; h < EH; ++h) {

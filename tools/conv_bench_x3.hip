@@ -56,7 +56,7 @@ static void time_wg(const char* tag, int n, int Hin, int Win, int cout, const vo
                     void* out, int iters) {
     auto k = conv_wg<KH, CIN, WM, WN, MF, NF, POOL, TH, TW, OCC, IS, OS, DIAG, WO, NPASS>;
     constexpr int BN = WN * NF * 16;
-    const size_t lds = wg_lds_bytes<KH, BN, TH, TW, WO, NPASS>();
+    const size_t lds = wg_lds_bytes<KH, BN, TH, TW, WO, NPASS, WN>();
     if (lds > 160 * 1024) { printf("%s LDS %zu: skip\n", tag, lds); return; }
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     const int Hc = Hin - KH + 1, Wc = Win - 3 + 1;
@@ -112,7 +112,7 @@ int main(int argc, char** argv) {
         // DIAG bits (aa_cnn.hip): 1 no staging, 4 no stores, 32 no weight stream,
         // 128 no fragment reads after the first, 2 no MFMA loop
 #define ABL5(D) time_one<9, 3, 64, 4, 2, 4, 4, 3, 39, 6, false, D, false, true, 2>("c5 d" #D, n, 48, 70, 128, in, w, b, out, fc, it);
-#define ABL2(D) time_one<3, 3, 32, 4, 1, 3, 2, 3, 9, 21, true, D, false, true, 4>("c2 d" #D, n, 158, 224, 32, in, w, b, out, f1, it);
+#define ABL2(D) time_one<3, 3, 32, 4, 1, 4, 2, 3, 12, 21, true, D, false, true, 0>("c2 d" #D, n, 158, 224, 32, in, w, b, out, f1, it);
 #define ABL4(D) time_one<3, 3, 64, 4, 2, 3, 2, 1, 12, 14, false, D, true, true, 4>("c4 d" #D, n, 50, 72, 64, in, w, b, out, fc, it);
 #define ABL3(D) time_one<3, 3, 32, 4, 2, 3, 2, 1, 10, 18, false, D, true, false, 0>("c3 d" #D, n, 52, 74, 64, in, w, b, out, fc, it);
         ABL5(0) ABL5(1) ABL5(2) ABL5(4) ABL5(5) ABL5(33) ABL5(161) ABL5(165) ABL5(37)
