@@ -264,11 +264,10 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
             }
             for (int oy = 0; oy < Hout; ++oy) {
                 float4 acc = b;
-#pragma unroll
+                // (KS > 0: constant trip counts, unrolled by the compiler)
                 for (int ky = 0; ky < KH; ++ky) {
                     const int iy = oy * sh - pt + ky;
                     if (iy < 0 || iy >= Hin) continue;
-#pragma unroll
                     for (int kx = 0; kx < KW; ++kx) {
                         const int ix = ox * sw - pl + kx;
                         if (ix < 0 || ix >= Win) continue;
