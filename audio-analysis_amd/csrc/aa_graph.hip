@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <string>
 
 #include "aa_common.h"
 #include "aa_gconv.h"
@@ -147,9 +148,10 @@ constexpr int GP4_STRIPES = 32;
 // fixed (pixel order within a stripe, a fixed combine tree), the same in the
 // pool and in the fused dwconv + pool: float4 loads give 16 lanes 256
 // contiguous bytes per pixel.
-// Stripe s sums the columns ox = s, s + GP4_STRIPES, ... of the map, each
-// from its top row down (the order gdwconv_pool4 produces its pixels in, so a
-// fused depthwise conv + pool and the two separate nodes give the same bits).
+// Stripe s sums the pixels p = s, s + GP4_STRIPES, ... of the map in row-major
+// order (the order gdwconv_pool4 produces its pixels in, so a fused depthwise
+// conv + pool and the two separate nodes give the same bits; every stripe
+// gets HW / GP4_STRIPES pixels within one, whatever the map's width).
 template <int Q>
 __global__ __launch_bounds__(Q * GP4_STRIPES) void ggpool4(const float* __restrict__ in, float* __restrict__ out,
                                                          int H, int W, int C, int avg, int act, float alpha) {
@@ -161,12 +163,11 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void ggpool4(const float* __restri
     float4 m = avg ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
     if (c < C) {
         const float* p = in + (size_t)n * HW * C + c;
-        for (int ox = s; ox < W; ox += GP4_STRIPES)
-            for (int oy = 0; oy < H; ++oy) {
-                const float4 v = *reinterpret_cast<const float4*>(p + ((size_t)oy * W + ox) * C);
-                if (avg) { m.x += v.x; m.y += v.y; m.z += v.z; m.w += v.w; }
-                else { m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w); }
-            }
+        for (int px = s; px < HW; px += GP4_STRIPES) {
+            const float4 v = *reinterpret_cast<const float4*>(p + (size_t)px * C);
+            if (avg) { m.x += v.x; m.y += v.y; m.z += v.z; m.w += v.w; }
+            else { m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w); }
+        }
     }
     part[s][4 * cq] = m.x; part[s][4 * cq + 1] = m.y; part[s][4 * cq + 2] = m.z; part[s][4 * cq + 3] = m.w;
     __syncthreads();
@@ -187,15 +188,22 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void ggpool4(const float* __restri
 
 // KS = 3: a 3x3 kernel, the taps unrolled and their weights held in
 // registers for every pixel; KS = 0: any kernel, weights re-read per tap.
-// Thread = (channel quad, column stripe s): it walks the columns ox = s, s +
-// GP4_STRIPES, ... top to bottom, so a stride-1 3x3 conv keeps its 3 x 3
-// input window in registers and loads one new row of 3 pixels per output
-// (3 float4 loads instead of 9); other shapes load their taps per pixel.
-template <int Q, int KS>
+// Thread = (channel quad, stripe s): it computes the pixels p = s, s +
+// GP4_STRIPES, ... in row-major order, so every stripe has HW / GP4_STRIPES
+// pixels within one.  S = 1 or 2 (KS = 3, both strides S): R of the thread's
+// pixels at a time, their 9 R taps loaded unconditionally from clamped
+// addresses and zeroed by a value select (R = 1 by default: the fewest
+// registers).  Round 5's column walk with a sliding 3 x 3 window was
+// latency-bound -- one round trip per output row, 0.69-0.86 of the wave
+// cycles parked on loads, its padding zeros read through flat loads from
+// scratch, and on a 33-column map stripe 0 walked two columns while the
+// others walked one (profiles/r05/pmc_ev2_top.txt).
+template <int Q, int KS, int S = 0, int R = 1>
 __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
     const float* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out,
     float* __restrict__ pooled, int Hin, int Win, int C, int Hout, int Wout, int kh, int kw, int sh, int sw, int pt,
     int pl, int act, float alpha, int pact, float palpha) {
+    static_assert(S == 0 || KS == 3, "chunked rows: 3x3 kernels");
     __shared__ float part[GP4_STRIPES][4 * Q];
     const int cq = threadIdx.x % Q, s = threadIdx.x / Q;
     const int c = blockIdx.x * 4 * Q + 4 * cq;
@@ -225,44 +233,46 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
             *reinterpret_cast<float4*>(o + ((size_t)oy * Wout + ox) * C) = y;
             m.x += y.x; m.y += y.y; m.z += y.z; m.w += y.w;
         };
-        const bool slide = KS == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && Hout == Hin && Wout == Win;
-        for (int ox = s; ox < Wout; ox += GP4_STRIPES) {
-            if (slide) {
-                // window rows r = 0..2 hold input rows oy - 1 .. oy + 1 at columns ox - 1 .. ox + 1
-                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-                float4 x[3][3];
-                auto ld = [&](int iy, int ix) -> float4 {
-                    return (iy >= 0 && iy < Hin && ix >= 0 && ix < Win)
-                               ? *reinterpret_cast<const float4*>(img + ((size_t)iy * Win + ix) * C)
-                               : z;
-                };
+        if constexpr (S > 0) {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float* imgw = in + (size_t)n * Hin * Win * C;
+            for (int p0 = s; p0 < HW; p0 += GP4_STRIPES * R) {
+                float4 x[R][9];
+                int oyv[R], oxv[R];
 #pragma unroll
-                for (int cc = 0; cc < 3; ++cc) {
-                    x[0][cc] = z;
-                    x[1][cc] = ld(0, ox - 1 + cc);
-                }
-                for (int oy = 0; oy < Hout; ++oy) {
-#pragma unroll
-                    for (int cc = 0; cc < 3; ++cc) x[2][cc] = ld(oy + 1, ox - 1 + cc);
-                    float4 acc = b;
+                for (int u = 0; u < R; ++u) {
+                    const int p = p0 + u * GP4_STRIPES;
+                    const bool pv = p < HW;
+                    oyv[u] = pv ? p / Wout : 0;
+                    oxv[u] = pv ? p - oyv[u] * Wout : 0;
 #pragma unroll
                     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
                         for (int kx = 0; kx < 3; ++kx) {
-                            // the per-pixel path skips padding taps; a zero tap adds
-                            // +0 * w: the same sum unless w is inf / nan
-                            fma4(acc, wr[KS ? ky * KS + kx : 0], x[ky][kx]);
+                            // a load from the clamped pixel, zeroed outside the image: a
+                            // value select (a `cond ? *p : z` becomes a select of
+                            // pointers -- flat loads, z in scratch)
+                            const int iy = oyv[u] * S - pt + ky, ix = oxv[u] * S - pl + kx;
+                            const int iyc = min(max(iy, 0), Hin - 1), ixc = min(max(ix, 0), Win - 1);
+                            // (a 32-bit offset from the window's base: one VGPR per address)
+                            const float4 t = *reinterpret_cast<const float4*>(
+                                imgw + (uint32_t)((iyc * Win + ixc) * C + c));
+                            x[u][ky * 3 + kx] = (pv && iy == iyc && ix == ixc) ? t : z;
                         }
-                    emit(oy, ox, acc);
-#pragma unroll
-                    for (int cc = 0; cc < 3; ++cc) {
-                        x[0][cc] = x[1][cc];
-                        x[1][cc] = x[2][cc];
-                    }
                 }
-                continue;
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    if (p0 + u * GP4_STRIPES >= HW) break;
+                    float4 acc = b;
+                    // padding taps add +0 * w: the same sum unless w is inf / nan
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) fma4(acc, wr[t], x[u][t]);
+                    emit(oyv[u], oxv[u], acc);
+                }
             }
-            for (int oy = 0; oy < Hout; ++oy) {
+        } else {
+            for (int p = s; p < HW; p += GP4_STRIPES) {
+                const int oy = p / Wout, ox = p - oy * Wout;
                 float4 acc = b;
                 // (KS > 0: constant trip counts, unrolled by the compiler)
                 for (int ky = 0; ky < KH; ++ky) {
@@ -874,6 +884,26 @@ static int dw_q() {
     return q;
 }
 
+// AA_GRAPH_DW_ROWWALK=1: the 3x3 depthwise convs pixel by pixel (no
+// chunks; A/B and test knob -- the same sums up to the sign of a zero)
+static bool dw_rowwalk() {
+    static const bool r = getenv("AA_GRAPH_DW_ROWWALK") != nullptr;
+    return r;
+}
+// pixels per thread whose taps are loaded together in the 3x3 depthwise
+// convs (A/B knob AA_GRAPH_DW_PX = 1, 2 or 3).  The dwconv stages of the
+// EfficientNet step: 526 us as round 5's column walk, 363 / 390 / 436 us at
+// 1 / 2 / 3 pixels (4: 456, 252 VGPRs) -- the balance over the stripes and
+// the occupancy matter, not the loads' depth (profiles/r05/graph_ab_dw.txt)
+static int dw_chunk() {
+    static const int r = [] {
+        const char* e = getenv("AA_GRAPH_DW_PX");
+        const int v = e ? std::atoi(e) : 1;
+        return v >= 1 && v <= 3 ? v : 1;
+    }();
+    return r;
+}
+
 static int graph_run_node(const Graph& G, const GNode& N, const float* x, float* ws, int n, hipStream_t st) {
     const aa_node& d = N.d;
     auto buf = [&](int k) -> const float* {
@@ -1039,16 +1069,26 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                 const GNode& P = G.nodes[N.pool_into];
                 float* pooled = ws + P.off * (size_t)n;
                 if ((Cin & 3) == 0) {
-#define AA_DWP(Q, KS)                                                                                          \
-    hipLaunchKernelGGL((gdwconv_pool4<Q, KS>), dim3((Cin + 4 * Q - 1) / (4 * Q), n), dim3(Q * GP4_STRIPES), 0, st, \
-                       a, (const float*)N.d_w, N.d_b, out, pooled, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh, d.sw,  \
-                       d.pt, d.pl, act, d.alpha, P.d.act, P.d.alpha)
+#define AA_DWP(Q, KS, S, R)                                                                                    \
+    hipLaunchKernelGGL((gdwconv_pool4<Q, KS, S, R>), dim3((Cin + 4 * Q - 1) / (4 * Q), n), dim3(Q * GP4_STRIPES), 0, \
+                       st, a, (const float*)N.d_w, N.d_b, out, pooled, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh,    \
+                       d.sw, d.pt, d.pl, act, d.alpha, P.d.act, P.d.alpha)
                     const bool k3 = d.kh == 3 && d.kw == 3;
+                    const int cs = k3 && d.sh == d.sw && (d.sh == 1 || d.sh == 2) && !dw_rowwalk() ? d.sh : 0;
+                    const int px = dw_chunk();
                     if (dw_q() == 8) {
-                        if (k3) AA_DWP(8, 3);
-                        else AA_DWP(8, 0);
-                    } else if (k3) AA_DWP(16, 3);
-                    else AA_DWP(16, 0);
+                        if (cs == 1 && px == 2) AA_DWP(8, 3, 1, 2);
+                        else if (cs == 1 && px == 3) AA_DWP(8, 3, 1, 3);
+                        else if (cs == 1) AA_DWP(8, 3, 1, 1);
+                        else if (cs == 2 && px == 2) AA_DWP(8, 3, 2, 2);
+                        else if (cs == 2 && px == 3) AA_DWP(8, 3, 2, 3);
+                        else if (cs == 2) AA_DWP(8, 3, 2, 1);
+                        else if (k3) AA_DWP(8, 3, 0, 1);
+                        else AA_DWP(8, 0, 0, 1);
+                    } else if (cs == 1) AA_DWP(16, 3, 1, 1);
+                    else if (cs == 2) AA_DWP(16, 3, 2, 1);
+                    else if (k3) AA_DWP(16, 3, 0, 1);
+                    else AA_DWP(16, 0, 0, 1);
 #undef AA_DWP
                 } else {
                     hipLaunchKernelGGL(gdwconv_pool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a,

@@ -12,8 +12,13 @@ for r in $(seq 1 $R); do
     python - "${V:--}" <<'PY'
 import json, sys
 d = json.loads(open("gpurun_out/gab.log").read().strip().splitlines()[-1])
-st = sorted(d["roofline"]["stages_ms"].items(), key=lambda kv: -kv[1])[:6]
-print(f"{sys.argv[1]:28s} {d['value']:9.1f} sum={1e3 * d['roofline']['stages_sum_ms']:7.1f}us  " + " ".join(f"{k}={1e3*v:.0f}" for k, v in st), flush=True)
+import re
+g = {}
+for k, v in d["roofline"]["stages_ms"].items():
+    m = re.match(r"(dwconv|matvec|conv_gx3_1x1|conv_gx3_3x3|conv_gf32|fe_)", k)
+    key = m.group(1) if m else "other"
+    g[key] = g.get(key, 0.0) + v
+print(f"{sys.argv[1]:28s} {d['value']:9.1f} sum={1e3 * d['roofline']['stages_sum_ms']:7.1f}us  " + " ".join(f"{k}={1e3*v:.0f}" for k, v in sorted(g.items())), flush=True)
 PY
   done
 done

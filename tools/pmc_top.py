@@ -17,7 +17,8 @@ for path in sys.argv[3:]:
         for r in csv.DictReader(open(f)):
             d = int(r["Dispatch_Id"])
             agg[d][r["Counter_Name"]] += float(r["Counter_Value"])
-            meta[d] = (r["Kernel_Name"][:70], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            extra = " ".join(f"{k}={r[k]}" for k in ("Grid_Size", "LDS_Block_Size", "VGPR_Count", "Accum_VGPR_Count", "Scratch_Size") if k in r)
+            meta[d] = (r["Kernel_Name"][:70] + "  " + extra, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     ids = sorted(meta)[-n_last:]
     per.append([(meta[d][0], meta[d][1], agg[d]) for d in ids])
 rows = []
