@@ -114,7 +114,10 @@ __device__ __forceinline__ void xcd_order(int xord, int& bx, int& by, int& bz) {
 // steps of 12 MFMAs.  scale_hw > 0: the pixels of n windows run flattened as
 // one image (pointwise convs) and pixel P's squeeze-and-excite scale is that
 // of window P / scale_hw.
-template <int WM, int WN, int MF, int NF, int KC = 1>
+//
+// PD: K steps whose loads are in flight at once (a register ring PD deep):
+// step s's pixels and weights are loaded PD steps ahead.
+template <int WM, int WN, int MF, int NF, int KC = 1, int PD = 1>
 __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
                                                  const float* __restrict__ bias, float* __restrict__ out,
                                                  ConvGeom g, int cout_pad, int act, float alpha,
@@ -166,18 +169,20 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
 #pragma unroll
         for (int j = 0; j < MF; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
     const bool vec = (g.Cin & 7) == 0;
-    float v[AI][KC][8];
-    uint4 wh[BI][KC], wl[BI][KC];
+    float v[PD][AI][KC][8];
+    uint4 wh[PD][BI][KC], wl[PD][BI][KC];
 #pragma unroll
-    for (int ib = 0; ib < BI; ++ib)
+    for (int u = 0; u < PD; ++u)
 #pragma unroll
-        for (int k = 0; k < KC; ++k) wh[ib][k] = wl[ib][k] = make_uint4(0, 0, 0, 0);
+        for (int ib = 0; ib < BI; ++ib)
+#pragma unroll
+            for (int k = 0; k < KC; ++k) wh[u][ib][k] = wl[u][ib][k] = make_uint4(0, 0, 0, 0);
     // step s = (tap, chunks KC gs .. KC gs + KC - 1): this thread's 8 channels
     // of AI pixels per chunk and its 8 hi + 8 lo weights per chunk
     // the coordinates (kernel row, column, chunk group) of the next step to
     // load, stepped on by one per load (no integer divisions per step)
     int l_ky = 0, l_kx = 0, l_gs = 0;
-    auto load = [&]() {
+    auto load = [&](float (&vb)[AI][KC][8], uint4 (&whb)[BI][KC], uint4 (&wlb)[BI][KC]) {
         const int ky = l_ky, kx = l_kx, gs = l_gs, tap = ky * g.kw + kx;
         if (++l_gs == ngs) {
             l_gs = 0;
@@ -198,19 +203,19 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
                 if (inside && vec && c0 + 8 <= g.Cin) {
                     const float4 a = *reinterpret_cast<const float4*>(px + c0);
                     const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
-                    v[it][k][0] = a.x; v[it][k][1] = a.y; v[it][k][2] = a.z; v[it][k][3] = a.w;
-                    v[it][k][4] = b.x; v[it][k][5] = b.y; v[it][k][6] = b.z; v[it][k][7] = b.w;
+                    vb[it][k][0] = a.x; vb[it][k][1] = a.y; vb[it][k][2] = a.z; vb[it][k][3] = a.w;
+                    vb[it][k][4] = b.x; vb[it][k][5] = b.y; vb[it][k][6] = b.z; vb[it][k][7] = b.w;
                     if (scl) {
                         const float4 sa = *reinterpret_cast<const float4*>(scl + c0);
                         const float4 sb = *reinterpret_cast<const float4*>(scl + c0 + 4);
-                        v[it][k][0] *= sa.x; v[it][k][1] *= sa.y; v[it][k][2] *= sa.z; v[it][k][3] *= sa.w;
-                        v[it][k][4] *= sb.x; v[it][k][5] *= sb.y; v[it][k][6] *= sb.z; v[it][k][7] *= sb.w;
+                        vb[it][k][0] *= sa.x; vb[it][k][1] *= sa.y; vb[it][k][2] *= sa.z; vb[it][k][3] *= sa.w;
+                        vb[it][k][4] *= sb.x; vb[it][k][5] *= sb.y; vb[it][k][6] *= sb.z; vb[it][k][7] *= sb.w;
                     }
                 } else {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         const bool ok = inside && c0 + e < g.Cin;
-                        v[it][k][e] = ok ? (scl ? px[c0 + e] * scl[c0 + e] : px[c0 + e]) : 0.f;
+                        vb[it][k][e] = ok ? (scl ? px[c0 + e] * scl[c0 + e] : px[c0 + e]) : 0.f;
                     }
                 }
             }
@@ -222,13 +227,19 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             for (int k = 0; k < KC; ++k) {
                 const uint16_t* wrow =
                     wpk + (((size_t)(tap * ncc + cbase + gs * KC + k) * cout_pad) + ch0 + r + 64 * ib) * 64;
-                wh[ib][k] = *reinterpret_cast<const uint4*>(wrow + 8 * q);
-                wl[ib][k] = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
+                whb[ib][k] = *reinterpret_cast<const uint4*>(wrow + 8 * q);
+                wlb[ib][k] = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * q);
             }
         }
     };
-    load();
-    for (int s = 0; s < nsteps; ++s) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u)
+        if (u < nsteps) load(v[u], wh[u], wl[u]);
+    for (int s0 = 0; s0 < nsteps; s0 += PD)
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+        const int s = s0 + u;
+        if (s >= nsteps) break;  // block-uniform
         gbf16x8 h[AI][KC], l[AI][KC];
 #pragma unroll
         for (int it = 0; it < AI; ++it)
@@ -236,8 +247,8 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             for (int k = 0; k < KC; ++k)
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    h[it][k][e] = (__bf16)v[it][k][e];
-                    l[it][k][e] = (__bf16)(v[it][k][e] - (float)h[it][k][e]);
+                    h[it][k][e] = (__bf16)v[u][it][k][e];
+                    l[it][k][e] = (__bf16)(v[u][it][k][e] - (float)h[it][k][e]);
                 }
         __syncthreads();  // the previous step's fragments are read
 #pragma unroll
@@ -252,12 +263,12 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             if (r + 64 * ib >= BN) continue;
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
-                *reinterpret_cast<uint4*>(Bh + (r + 64 * ib) * ROW + 32 * k + 8 * q) = wh[ib][k];
-                *reinterpret_cast<uint4*>(Bl + (r + 64 * ib) * ROW + 32 * k + 8 * q) = wl[ib][k];
+                *reinterpret_cast<uint4*>(Bh + (r + 64 * ib) * ROW + 32 * k + 8 * q) = wh[u][ib][k];
+                *reinterpret_cast<uint4*>(Bl + (r + 64 * ib) * ROW + 32 * k + 8 * q) = wl[u][ib][k];
             }
         }
         __syncthreads();
-        if (s + 1 < nsteps) load();
+        if (s + PD < nsteps) load(v[u], wh[u], wl[u]);
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
             const int ko = 32 * k + 8 * (lane >> 4);

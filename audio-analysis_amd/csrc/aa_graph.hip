@@ -584,6 +584,17 @@ static void graph_fuse(Graph* G) {
     }
 }
 
+// a pointwise conv over >= 384 channels on a small map (<= split_hw() pixels
+// per window) is a short grid of long K loops: its K is split over blocks
+// (A/B knob AA_GRAPH_SPLITHW)
+static int split_hw() {
+    static const int v = [] {
+        const char* e = getenv("AA_GRAPH_SPLITHW");
+        return e ? std::atoi(e) : 128;
+    }();
+    return v;
+}
+
 static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float* blob, int64_t blob_len) {
     auto get = [&](int64_t off, int64_t n) -> const float* {
         if (off < 0 || n < 0 || off + n > blob_len) return nullptr;
@@ -629,6 +640,7 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                 N.mfma = G->prec == AA_PREC_BF16X3 && C >= 16 && !N.matvec;
                 const int ntap = d.kh * d.kw;
                 int rc;
+                const bool pointwise = ntap == 1 && d.sh == 1 && d.sw == 1 && d.pt == 0 && d.pl == 0;
                 if (N.mfma) {
                     N.bn = gconv_bn(N.C);
                     N.cout_pad = (N.C + N.bn - 1) / N.bn * N.bn;
@@ -665,15 +677,9 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                 }
                 N.flops = 2.0 * N.H * N.W * K * N.C;
                 N.bytes = 4.0 * (H * W * C + N.H * N.W * N.C);
-                // a pointwise conv over >= 384 channels on a small map (<= 128
-                // pixels per window) is a short grid of long K loops: split K
-                // over blocks (shape-only choice: the sums do not depend on n)
-                static const int split_hw = [] {  // (A/B knob AA_GRAPH_SPLITHW)
-                    const char* e = getenv("AA_GRAPH_SPLITHW");
-                    return e ? std::atoi(e) : 128;
-                }();
-                if (N.mfma && ntap == 1 && d.sh == 1 && d.sw == 1 && d.pt == 0 && d.pl == 0 && N.H * N.W <= split_hw &&
-                    getenv("AA_GRAPH_NOSPLIT") == nullptr) {
+                // split K over blocks on small maps (shape-only choice: the
+                // sums do not depend on n)
+                if (N.mfma && pointwise && N.H * N.W <= split_hw() && getenv("AA_GRAPH_NOSPLIT") == nullptr) {
                     const int ncc = N.g.cin_pad / 32;
                     for (int cs : {6, 7, 4, 5, 8, 9})
                         if (ncc >= 12 && ncc % cs == 0) {
@@ -890,6 +896,20 @@ static bool dw_rowwalk() {
     static const bool r = getenv("AA_GRAPH_DW_ROWWALK") != nullptr;
     return r;
 }
+// K steps in flight in the one-chunk 64 x 64 gconv_x3t launches over >= 8
+// chunks (A/B knob AA_GRAPH_PD = 1, 2 or 3; 2: the 672 -> 112 project convs
+// 46 -> 42 us, the step unchanged; 64 / 128 x 224 / 192 / 112 tiles for the
+// pointwise convs measured slower, 112 -> 672 35 -> 46 us:
+// profiles/r05/graph_ab_pw.txt)
+static int gx_pd() {
+    static const int r = [] {
+        const char* e = getenv("AA_GRAPH_PD");
+        const int v = e ? std::atoi(e) : 2;
+        return v >= 1 && v <= 3 ? v : 2;
+    }();
+    return r;
+}
+
 // pixels per thread whose taps are loaded together in the 3x3 depthwise
 // convs (A/B knob AA_GRAPH_DW_PX = 1, 2 or 3).  The dwconv stages of the
 // EfficientNet step: 526 us as round 5's column walk, 363 / 390 / 436 us at
@@ -1035,6 +1055,14 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     if (KC == 4) AA_GX(4);
                     else if (KC == 3) AA_GX(3);
                     else if (KC == 2) AA_GX(2);
+                    else if (gx_pd() == 2 && ncc >= 8)
+                        hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 1, 2>), dim3((HWo + 63) / 64, N.cout_pad / 64, nz),
+                                           dim3(256), 0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act,
+                                           d.alpha, scl, res, scale_hw, 0, nullptr, xo);
+                    else if (gx_pd() == 3 && ncc >= 8)
+                        hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 1, 3>), dim3((HWo + 63) / 64, N.cout_pad / 64, nz),
+                                           dim3(256), 0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act,
+                                           d.alpha, scl, res, scale_hw, 0, nullptr, xo);
                     else AA_GX(1);
 #undef AA_GX
                 }

@@ -19,6 +19,10 @@ for k, v in d["roofline"]["stages_ms"].items():
     key = m.group(1) if m else "other"
     g[key] = g.get(key, 0.0) + v
 print(f"{sys.argv[1]:28s} {d['value']:9.1f} sum={1e3 * d['roofline']['stages_sum_ms']:7.1f}us  " + " ".join(f"{k}={1e3*v:.0f}" for k, v in sorted(g.items())), flush=True)
+st = d["roofline"]["stages_ms"]
+pick = ["conv_gx3_1x1_s1_112_672", "conv_gx3_1x1_s1_672_112+add+se", "conv_gx3_1x1_s1_192_1152", "conv_gx3_1x1_s1_1152_192+add+se",
+        "conv_gx3_1x1_s1_96_384", "conv_gx3_1x1_s1_384_96+add+se", "conv_gx3_1x1_s1_672_192+se", "conv_gx3_1x1_s1_192_1280"]
+print(" " * 30 + " ".join(f"{k[13:]}={1e3 * st[k]:.1f}" for k in pick if k in st), flush=True)
 PY
   done
 done
