@@ -18,6 +18,8 @@
 // and the f32 parity mode.
 #pragma once
 
+#include <type_traits>
+
 #include "aa_common.h"
 
 namespace aa {
@@ -200,7 +202,10 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
                 const int c0 = (cbase + gs * KC + k) * 32 + 8 * q;
-                if (inside && vec && c0 + 8 <= g.Cin) {
+                if (vec && c0 >= g.Cin) {  // a padding chunk's quad: zeros, no loads
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) vb[it][k][e] = 0.f;
+                } else if (inside && vec && c0 + 8 <= g.Cin) {
                     const float4 a = *reinterpret_cast<const float4*>(px + c0);
                     const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
                     vb[it][k][0] = a.x; vb[it][k][1] = a.y; vb[it][k][2] = a.z; vb[it][k][3] = a.w;
@@ -320,28 +325,51 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             for (int e = 0; e < 4; ++e) bv[i][e] = c + e < g.Cout ? bias[c + e] : 0.f;
         }
     }
+    // the activation resolved once per block (a per-element switch was
+    // if-converted into every variant's instructions), the residual read as
+    // float4 where the lane's 4 channels are whole
+    const bool full4 = (g.Cout & 3) == 0;
+    auto epi = [&](auto actc) {
+        constexpr int A = decltype(actc)::value;
 #pragma unroll
-    for (int j = 0; j < MF; ++j) {
-        const int Pj = pix0 + wm * MF * 16 + j * 16 + (lane & 15);
-        if (Pj >= HWo) continue;
-        float* o = out + ((size_t)n * HWo + Pj) * g.Cout;
-        const float* rp = res ? res + ((size_t)n * HWo + Pj) * g.Cout : nullptr;
+        for (int j = 0; j < MF; ++j) {
+            const int Pj = pix0 + wm * MF * 16 + j * 16 + (lane & 15);
+            if (Pj >= HWo) continue;
+            float* o = out + ((size_t)n * HWo + Pj) * g.Cout;
+            const float* rp = res ? res + ((size_t)n * HWo + Pj) * g.Cout : nullptr;
 #pragma unroll
-        for (int i = 0; i < NF; ++i) {
-            const int c = ch0 + wn * NF * 16 + i * 16 + 4 * (lane >> 4);
-            float y[4];
+            for (int i = 0; i < NF; ++i) {
+                const int c = ch0 + wn * NF * 16 + i * 16 + 4 * (lane >> 4);
+                float y[4];
+                if (full4 && c + 4 <= g.Cout) {
+                    float z[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float z = acc[i][j][e] + bv[i][e];
-                if (rp && c + e < g.Cout) z += rp[c + e];
-                y[e] = gact(z, act, alpha);
-            }
-            if (c + 4 <= g.Cout && (g.Cout & 3) == 0) {
-                *reinterpret_cast<float4*>(o + c) = make_float4(y[0], y[1], y[2], y[3]);
-            } else {
-                for (int e = 0; e < 4 && c + e < g.Cout; ++e) o[c + e] = y[e];
+                    for (int e = 0; e < 4; ++e) z[e] = acc[i][j][e] + bv[i][e];
+                    if (rp) {
+                        const float4 r4 = *reinterpret_cast<const float4*>(rp + c);
+                        z[0] += r4.x; z[1] += r4.y; z[2] += r4.z; z[3] += r4.w;
+                    }
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) y[e] = gact(z[e], A, alpha);
+                    *reinterpret_cast<float4*>(o + c) = make_float4(y[0], y[1], y[2], y[3]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float z = acc[i][j][e] + bv[i][e];
+                        if (rp && c + e < g.Cout) z += rp[c + e];
+                        y[e] = gact(z, A, alpha);
+                    }
+                    for (int e = 0; e < 4 && c + e < g.Cout; ++e) o[c + e] = y[e];
+                }
             }
         }
+    };
+    switch (act) {
+        case GACT_RELU: epi(std::integral_constant<int, GACT_RELU>{}); break;
+        case GACT_LEAKY: epi(std::integral_constant<int, GACT_LEAKY>{}); break;
+        case GACT_SIGMOID: epi(std::integral_constant<int, GACT_SIGMOID>{}); break;
+        case GACT_SWISH: epi(std::integral_constant<int, GACT_SWISH>{}); break;
+        default: epi(std::integral_constant<int, GACT_NONE>{}); break;
     }
 }
 

@@ -1026,59 +1026,46 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     else
                         hipLaunchKernelGGL((gconv_x3p<2, 2, 2, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
                                            N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res, xo);
-                } else if (N.bn == 16)
-                    hipLaunchKernelGGL((gconv_x3t<4, 1, 4, 1>), dim3((HWo + 255) / 256, N.cout_pad / 16, nz), dim3(256),
-                                       0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res, scale_hw, 0, nullptr, xo);
-                else if (N.bn == 32)
-                    hipLaunchKernelGGL((gconv_x3t<4, 1, 2, 2>), dim3((HWo + 127) / 128, N.cout_pad / 32, nz), dim3(256),
-                                       0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res, scale_hw, 0, nullptr, xo);
-                else if (wide_n() && (d.kh * d.kw == 1 || wide_n3()) && N.C >= 128 && N.g.cin_pad <= 256 && N.cout_pad % 128 == 0)
-                    // 64 x 128 tiles: half the re-reads of the pixel tile
-                    hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 4>), dim3((HWo + 63) / 64, N.cout_pad / 128, nz), dim3(256),
-                                       0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res, scale_hw, 0, nullptr, xo);
-                else if (wide_tile(d.kh * d.kw > 1))
-                    hipLaunchKernelGGL((gconv_x3t<2, 2, 4, 2>), dim3((HWo + 127) / 128, N.cout_pad / 64, nz), dim3(256),
-                                       0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl,
-                                       res, scale_hw, 0, nullptr, xo);
-                else if (N.split > 1 && nz == 1) {
-                    // split K: slices of cslice chunks on blockIdx.z, then the ordered sum
-                    float* part = ws + G.part_off * (size_t)n;
-                    const dim3 grid((HWo + 63) / 64, N.cout_pad / 64, N.split);
-                    if (N.cslice % 2 == 0 && kc_max() >= 2)
-                        hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 2>), grid, dim3(256), 0, st, a, (const uint16_t*)N.d_w,
-                                           N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, N.cslice, part, xo);
-                    else
-                        hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 1>), grid, dim3(256), 0, st, a, (const uint16_t*)N.d_w,
-                                           N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, N.cslice, part, xo);
-                    AA_LAUNCH_CHECK();
-                    const size_t total = (size_t)HWo * N.C;
-                    hipLaunchKernelGGL(gsplit_reduce, dim3((unsigned)((total / 4 + 255) / 256 + 1)), dim3(256), 0, st, part,
-                                       N.split, total, N.C, N.d_b, res, out, act, d.alpha);
                 } else {
-                    // 64 x 64 tiles, KC 32-channel chunks per K step (the same
-                    // products summed in the same order whatever KC is)
-                    const int ncc = N.g.cin_pad / 32, kmax = kc_max();
-                    const int KC = ncc % 4 == 0 && kmax >= 4 ? 4 : ncc % 3 == 0 && kmax >= 3 ? 3
-                                   : ncc % 2 == 0 && kmax >= 2 ? 2 : 1;
-#define AA_GX(K_)                                                                                                   \
-    hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, K_>), dim3((HWo + 63) / 64, N.cout_pad / 64, nz), dim3(256), 0, st, a, \
-                       (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, 0, nullptr, xo)
-                    if (KC == 4) AA_GX(4);
-                    else if (KC == 3) AA_GX(3);
-                    else if (KC == 2) AA_GX(2);
-                    else if (gx_pd() == 2 && ncc >= 8)
-                        hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 1, 2>), dim3((HWo + 63) / 64, N.cout_pad / 64, nz),
-                                           dim3(256), 0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act,
-                                           d.alpha, scl, res, scale_hw, 0, nullptr, xo);
-                    else if (gx_pd() == 3 && ncc >= 8)
-                        hipLaunchKernelGGL((gconv_x3t<2, 2, 2, 2, 1, 3>), dim3((HWo + 63) / 64, N.cout_pad / 64, nz),
-                                           dim3(256), 0, st, a, (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act,
-                                           d.alpha, scl, res, scale_hw, 0, nullptr, xo);
-                    else AA_GX(1);
-#undef AA_GX
+                    // gconv_x3t (64 x 64 by default)
+#define AA_X3T(GRID, WM_, WN_, MF_, NF_, KC_, PD_, CS_, PART_)                                                     \
+    hipLaunchKernelGGL((gconv_x3t<WM_, WN_, MF_, NF_, KC_, PD_>), GRID, dim3(256), 0, st, a, (const uint16_t*)N.d_w, \
+                       N.d_b, out, g, N.cout_pad, act, d.alpha, scl, res, scale_hw, CS_, PART_, xo)
+                    if (N.bn == 16)
+                        AA_X3T(dim3((HWo + 255) / 256, N.cout_pad / 16, nz), 4, 1, 4, 1, 1, 1, 0, nullptr);
+                    else if (N.bn == 32)
+                        AA_X3T(dim3((HWo + 127) / 128, N.cout_pad / 32, nz), 4, 1, 2, 2, 1, 1, 0, nullptr);
+                    else if (wide_n() && (d.kh * d.kw == 1 || wide_n3()) && N.C >= 128 && N.g.cin_pad <= 256 &&
+                             N.cout_pad % 128 == 0)
+                        // 64 x 128 tiles: half the re-reads of the pixel tile
+                        AA_X3T(dim3((HWo + 63) / 64, N.cout_pad / 128, nz), 2, 2, 2, 4, 1, 1, 0, nullptr);
+                    else if (wide_tile(d.kh * d.kw > 1))
+                        AA_X3T(dim3((HWo + 127) / 128, N.cout_pad / 64, nz), 2, 2, 4, 2, 1, 1, 0, nullptr);
+                    else if (N.split > 1 && nz == 1) {
+                        // split K: slices of cslice chunks on blockIdx.z, then the ordered sum
+                        float* part = ws + G.part_off * (size_t)n;
+                        const dim3 grid((HWo + 63) / 64, N.cout_pad / 64, N.split);
+                        if (N.cslice % 2 == 0 && kc_max() >= 2) AA_X3T(grid, 2, 2, 2, 2, 2, 1, N.cslice, part);
+                        else AA_X3T(grid, 2, 2, 2, 2, 1, 1, N.cslice, part);
+                        AA_LAUNCH_CHECK();
+                        const size_t total = (size_t)HWo * N.C;
+                        hipLaunchKernelGGL(gsplit_reduce, dim3((unsigned)((total / 4 + 255) / 256 + 1)), dim3(256), 0, st,
+                                           part, N.split, total, N.C, N.d_b, res, out, act, d.alpha);
+                    } else {
+                        // 64 x 64 tiles, KC 32-channel chunks per K step (the same
+                        // products summed in the same order whatever KC is)
+                        const int ncc = N.g.cin_pad / 32, kmax = kc_max();
+                        const int KC = ncc % 4 == 0 && kmax >= 4 ? 4 : ncc % 3 == 0 && kmax >= 3 ? 3
+                                       : ncc % 2 == 0 && kmax >= 2 ? 2 : 1;
+                        const dim3 grid((HWo + 63) / 64, N.cout_pad / 64, nz);
+                        if (KC == 4) AA_X3T(grid, 2, 2, 2, 2, 4, 1, 0, nullptr);
+                        else if (KC == 3) AA_X3T(grid, 2, 2, 2, 2, 3, 1, 0, nullptr);
+                        else if (KC == 2) AA_X3T(grid, 2, 2, 2, 2, 2, 1, 0, nullptr);
+                        else if (gx_pd() == 2 && ncc >= 8) AA_X3T(grid, 2, 2, 2, 2, 1, 2, 0, nullptr);
+                        else if (gx_pd() == 3 && ncc >= 8) AA_X3T(grid, 2, 2, 2, 2, 1, 3, 0, nullptr);
+                        else AA_X3T(grid, 2, 2, 2, 2, 1, 1, 0, nullptr);
+                    }
+#undef AA_X3T
                 }
             } else if (N.matvec == 2) {
                 hipLaunchKernelGGL(gmatvec_t, dim3((N.C + 255) / 256, n), dim3(256), 0, st, a, (const float*)N.d_w,
