@@ -52,6 +52,20 @@ __device__ __forceinline__ float gact(float v, int act, float alpha) {
     }
 }
 
+// f(integral_constant<int, act>): the activation resolved once, outside a
+// kernel's per-element loops (a runtime `act` inside them is if-converted
+// into every variant's instructions)
+template <class F>
+__device__ __forceinline__ void with_act(int act, F&& f) {
+    switch (act) {
+        case GACT_RELU: f(std::integral_constant<int, GACT_RELU>{}); break;
+        case GACT_LEAKY: f(std::integral_constant<int, GACT_LEAKY>{}); break;
+        case GACT_SIGMOID: f(std::integral_constant<int, GACT_SIGMOID>{}); break;
+        case GACT_SWISH: f(std::integral_constant<int, GACT_SWISH>{}); break;
+        default: f(std::integral_constant<int, GACT_NONE>{}); break;
+    }
+}
+
 struct ConvGeom {
     int Hin, Win, Cin;   // input (NHWC)
     int Hout, Wout, Cout;
@@ -364,13 +378,7 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
             }
         }
     };
-    switch (act) {
-        case GACT_RELU: epi(std::integral_constant<int, GACT_RELU>{}); break;
-        case GACT_LEAKY: epi(std::integral_constant<int, GACT_LEAKY>{}); break;
-        case GACT_SIGMOID: epi(std::integral_constant<int, GACT_SIGMOID>{}); break;
-        case GACT_SWISH: epi(std::integral_constant<int, GACT_SWISH>{}); break;
-        default: epi(std::integral_constant<int, GACT_NONE>{}); break;
-    }
+    with_act(act, epi);
 }
 
 // gconv_x3q: stride-1 kernels larger than 1x1 at 64 output channels per
@@ -854,17 +862,20 @@ __global__ __launch_bounds__(256) void gconv_f32_lds(const float* __restrict__ i
         }
     }
     float* o = out + ((size_t)n * g.Hout * g.Wout + P) * g.Cout;
-    if ((g.Cout & 3) == 0 && c0 + 32 <= g.Cout) {
+    with_act(act, [&](auto actc) {
+        constexpr int A = decltype(actc)::value;
+        if ((g.Cout & 3) == 0 && c0 + 32 <= g.Cout) {
 #pragma unroll
-        for (int c = 0; c < 32; c += 4)
-            *reinterpret_cast<float4*>(o + c0 + c) = make_float4(gact(acc[c], act, alpha), gact(acc[c + 1], act, alpha),
-                                                                 gact(acc[c + 2], act, alpha),
-                                                                 gact(acc[c + 3], act, alpha));
-    } else {
+            for (int c = 0; c < 32; c += 4)
+                *reinterpret_cast<float4*>(o + c0 + c) = make_float4(gact(acc[c], A, alpha), gact(acc[c + 1], A, alpha),
+                                                                     gact(acc[c + 2], A, alpha),
+                                                                     gact(acc[c + 3], A, alpha));
+        } else {
 #pragma unroll
-        for (int c = 0; c < 32; ++c)
-            if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], act, alpha);
-    }
+            for (int c = 0; c < 32; ++c)
+                if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], A, alpha);
+        }
+    });
 }
 
 // gconv_f32_s: the same conv for a compile-time KH x KW x CI (a 3-channel
@@ -909,17 +920,20 @@ __global__ __launch_bounds__(256) void gconv_f32_s(const float* __restrict__ in,
                 for (int c = 0; c < 32; ++c) acc[c] = fmaf(wq[(t * CI + ci) * 32 + c], xv[t * CI + ci], acc[c]);
         }
     float* o = out + ((size_t)n * g.Hout * g.Wout + P) * g.Cout;
-    if ((g.Cout & 3) == 0 && c0 + 32 <= g.Cout) {
+    with_act(act, [&](auto actc) {
+        constexpr int A = decltype(actc)::value;
+        if ((g.Cout & 3) == 0 && c0 + 32 <= g.Cout) {
 #pragma unroll
-        for (int c = 0; c < 32; c += 4)
-            *reinterpret_cast<float4*>(o + c0 + c) = make_float4(gact(acc[c], act, alpha), gact(acc[c + 1], act, alpha),
-                                                                 gact(acc[c + 2], act, alpha),
-                                                                 gact(acc[c + 3], act, alpha));
-    } else {
+            for (int c = 0; c < 32; c += 4)
+                *reinterpret_cast<float4*>(o + c0 + c) = make_float4(gact(acc[c], A, alpha), gact(acc[c + 1], A, alpha),
+                                                                     gact(acc[c + 2], A, alpha),
+                                                                     gact(acc[c + 3], A, alpha));
+        } else {
 #pragma unroll
-        for (int c = 0; c < 32; ++c)
-            if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], act, alpha);
-    }
+            for (int c = 0; c < 32; ++c)
+                if (c0 + c < g.Cout) o[c0 + c] = gact(acc[c], A, alpha);
+        }
+    });
 }
 
 // max / average pooling with explicit padding (average over the taps inside

@@ -210,7 +210,8 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
     const int n = blockIdx.y;
     const int HW = Hout * Wout;
     float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < C) {
+    if (c < C) with_act(act, [&](auto actc) {
+        constexpr int AV = decltype(actc)::value;
         const float* img = in + (size_t)n * Hin * Win * C + c;
         float* o = out + (size_t)n * HW * C + c;
         const float4 b = bias ? *reinterpret_cast<const float4*>(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -228,8 +229,13 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
             acc.w = fmaf(wv.w, x.w, acc.w);
         };
         auto emit = [&](int oy, int ox, const float4& acc) {
-            const float4 y = make_float4(gact(acc.x, act, alpha), gact(acc.y, act, alpha), gact(acc.z, act, alpha),
-                                         gact(acc.w, act, alpha));
+            // no contraction of the activation's last product into the pool's
+            // add: the pool sums the stored (rounded) outputs, as the unfused
+            // ggpool4 does (with the activation a constant the compiler would
+            // otherwise fuse swish's v * logistic(v) into an FMA with m)
+#pragma clang fp contract(off)
+            const float4 y = make_float4(gact(acc.x, AV, alpha), gact(acc.y, AV, alpha), gact(acc.z, AV, alpha),
+                                         gact(acc.w, AV, alpha));
             *reinterpret_cast<float4*>(o + ((size_t)oy * Wout + ox) * C) = y;
             m.x += y.x; m.y += y.y; m.z += y.z; m.w += y.w;
         };
@@ -290,7 +296,7 @@ __global__ __launch_bounds__(Q * GP4_STRIPES) void gdwconv_pool4(
                 emit(oy, ox, acc);
             }
         }
-    }
+    });
     part[s][4 * cq] = m.x; part[s][4 * cq + 1] = m.y; part[s][4 * cq + 2] = m.z; part[s][4 * cq + 3] = m.w;
     __syncthreads();
     const int k = threadIdx.x;
