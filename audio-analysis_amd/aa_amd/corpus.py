@@ -56,8 +56,25 @@ def gather_documents(local: dict, device=None, group=None) -> dict:
 
 # host lanes (threads, each with its own HIP streams) of the batched path: 5
 # with 8 hardware queues measured 138k audio-s/s against 131k (4) and 117k
-# (3) on one box, three rounds each (profiles/r05/corpus_lanes.txt)
+# (3) on one box, three rounds each (profiles/r05/corpus_lanes.txt).  That was
+# measured with GPU_MAX_HW_QUEUES=8 (corpus.main and bench.py set it); with
+# HIP's default 4 queues the lanes' compute + copy streams would share queues,
+# so a library user who did not raise it keeps the 3 lanes measured there.
 DEFAULT_LANES = 5
+DEFAULT_LANES_4Q = 3
+
+
+def default_lanes() -> int:
+    """AA_BATCH_LANES if set, else the lane count for the process's
+    hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4 when unset)."""
+    env = os.environ.get("AA_BATCH_LANES")
+    if env:
+        return int(env)
+    try:
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        queues = 4
+    return DEFAULT_LANES if queues >= 8 else DEFAULT_LANES_4Q
 
 
 def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world=1, device=None, batch=16):
@@ -71,7 +88,7 @@ def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world
     if examine_fn is None and batch and torch.cuda.is_available():
         from .batch import BatchAnalyser
         ba = BatchAnalyser(bird_models, analyse_tracks, device=torch.device("cuda", torch.cuda.current_device()),
-                           batch=batch, lanes=int(os.environ.get("AA_BATCH_LANES", str(DEFAULT_LANES))))
+                           batch=batch, lanes=default_lanes())
         return gather_documents(ba.run([(i, str(f)) for i, f in mine]), device=device)
     if examine_fn is None:
         from .analyse import examine as examine_fn

@@ -141,40 +141,31 @@ __device__ __forceinline__ void split2(float x0, float x1, uint32_t& hi, uint32_
 }
 
 // Two activations max(x, a x) (0 <= a <= 1) as packed bf16 hi and lo
-// words, in 8 VALU ops: one packed multiply, two raw maxes (no NaN
-// canonicalisation: the inputs are MFMA results), one packed conversion for
-// hi, its two halves back to f32 (shift / mask), one packed subtract, one
-// packed conversion for lo.
+// words, in 8 VALU ops: two multiplies, two raw maxes, one packed conversion
+// for hi, its two halves back to f32 (shift / mask), two subtracts, one
+// packed conversion for lo.  The max is v_med3_f32(x, a x, +inf) through the
+// builtin: max(x, a x) for every non-NaN x (the inputs are MFMA results),
+// without the NaN canonicalisation a plain fmaxf adds, and -- unlike the
+// inline-asm v_max_f32 of round 5 -- visible to the hazard recognizer, which
+// pads the first VALU read of an MFMA result with the wait states the matrix
+// pipe needs (an asm read right behind the MFMA took stale registers in
+// conv_wgf).  AA_X3_SCALAR_SPLIT 0: the multiply as one packed op.
 __device__ __forceinline__ void leaky_split2(float x0, float x1, float a, uint32_t& hi, uint32_t& lo) {
     typedef __attribute__((ext_vector_type(2))) float f2;
     typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+    constexpr float inf = __builtin_inff();
 #if AA_X3_SCALAR_SPLIT
-    // scalar f32 ops only (packed f32 VALU costs extra issue beside MFMAs).
-    // The products are compiler-visible because x0 / x1 usually come straight
-    // from an MFMA: the hazard recognizer pads the first VALU read of an MFMA
-    // result with the wait states the matrix pipe needs, but it does not see
-    // into inline asm -- an asm read right behind the MFMA took stale
-    // registers (conv_wgf, whose activation follows its first-layer MFMA
-    // directly).  The asm maxes below depend on r0 / r1, so they come later.
-    float o0, o1;
     const float r0 = x0 * a, r1 = x1 * a;
-    asm("v_max_f32 %0, %1, %2" : "=v"(o0) : "v"(x0), "v"(r0));
-    asm("v_max_f32 %0, %1, %2" : "=v"(o1) : "v"(x1), "v"(r1));
-    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{o0, o1}, b2));
-    float s0, s1;
-    asm("v_sub_f32 %0, %1, %2" : "=v"(s0) : "v"(o0), "v"(__uint_as_float(hi << 16)));
-    asm("v_sub_f32 %0, %1, %2" : "=v"(s1) : "v"(o1), "v"(__uint_as_float(hi & 0xffff0000u)));
-    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{s0, s1}, b2));
 #else
-    const f2 s = f2{x0, x1} * a;
-    float o0, o1;
-    asm("v_max_f32 %0, %1, %2" : "=v"(o0) : "v"(x0), "v"(s.x));
-    asm("v_max_f32 %0, %1, %2" : "=v"(o1) : "v"(x1), "v"(s.y));
-    const f2 o = f2{o0, o1};
-    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(o, b2));
-    const f2 hf = f2{__uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
-    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(o - hf, b2));
+    const f2 r = f2{x0, x1} * a;
+    const float r0 = r.x, r1 = r.y;
 #endif
+    const float o0 = __builtin_amdgcn_fmed3f(x0, r0, inf);
+    const float o1 = __builtin_amdgcn_fmed3f(x1, r1, inf);
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{o0, o1}, b2));
+    const float s0 = o0 - __uint_as_float(hi << 16);
+    const float s1 = o1 - __uint_as_float(hi & 0xffff0000u);
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{s0, s1}, b2));
 }
 
 // byte offset of unit u of patch pixel (R, C)

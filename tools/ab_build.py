@@ -7,7 +7,7 @@ real pipeline, alternating runs on the same box.
 usage: python tools/ab_build.py NAME X3TABLE WGTABLE [NAME X3TABLE WGTABLE ...]
   X3TABLE / WGTABLE: 'X(...) X(...) ...' for AA_X3_CFGS / AA_WG_CFGS, '-' keeps
   the in-tree table, '' an empty one
-writes tools/ab/libaa_NAME.so (the other objects come from the main build)."""
+writes tools/ablib/libaa_NAME.so (the other objects come from the main build)."""
 import os
 import subprocess
 import sys
@@ -20,7 +20,7 @@ from aa_amd import _build  # noqa: E402
 
 def build(name, table, wg="-"):
     _build.build()
-    out = ROOT / "tools" / "ab"
+    out = ROOT / "tools" / "ablib"
     out.mkdir(exist_ok=True)
     cc = _build.hipcc()
     obj = out / f"aa_cnn_{name}.o"

@@ -1,4 +1,4 @@
-"""Build tools/ab/libaa_NAME.so from the sources as they are at a git revision
+"""Build tools/ablib/libaa_NAME.so from the sources as they are at a git revision
 (default HEAD), for an in-pipeline A/B of uncommitted kernel changes against
 the committed ones (tools/ab.sh).  The other objects come from the main build.
 
@@ -23,7 +23,7 @@ def main(name, rev="HEAD"):
             rel = f.relative_to(ROOT).as_posix()
             src = subprocess.run(["git", "show", f"{rev}:{rel}"], cwd=ROOT, capture_output=True)
             (tmp / f.name).write_bytes(src.stdout if src.returncode == 0 else f.read_bytes())
-        out = ROOT / "tools" / "ab"
+        out = ROOT / "tools" / "ablib"
         out.mkdir(exist_ok=True)
         cc = _build.hipcc()
         objs = []

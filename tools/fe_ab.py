@@ -1,5 +1,5 @@
 """Front end of the working-tree library against another build (AA_LIB, e.g.
-tools/ab/libaa_base.so from tools/ab_head.py): the log-mel of the bench's
+tools/ablib/libaa_base.so from tools/ab_head.py): the log-mel of the bench's
 64 windows (htk / hop 640 and Slaney / hop 281 plans, power 2 and 1) must be
 bit-identical.
 

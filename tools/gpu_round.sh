@@ -16,7 +16,7 @@
 #                                             kernel-trace summary of its serial step
 #   bash tools/gpu_round.sh ab NAME [rounds]  CNN parity tests, then alternating bench
 #                                             runs of the in-tree library against
-#                                             tools/ab/libaa_NAME.so (tools/ab.sh)
+#                                             tools/ablib/libaa_NAME.so (tools/ab.sh)
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -87,7 +87,7 @@ ab)
   NAME=$1
   timeout -k 10 300 $PT tests/test_gpu_cnn.py tests/test_gpu_config_step.py > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
   tail -1 gpurun_out/ab_tests.log
-  bash tools/ab.sh ${2:-3} main tools/ab/libaa_$NAME.so
+  bash tools/ab.sh ${2:-3} main tools/ablib/libaa_$NAME.so
   ;;
 *)
   echo "unknown mode $MODE"; exit 64 ;;

@@ -1,5 +1,5 @@
 """signal_noise of the working-tree library against another build (AA_LIB,
-e.g. tools/ab/libaa_base.so from tools/ab_head.py): masks before morphology
+e.g. tools/ablib/libaa_base.so from tools/ab_head.py): masks before morphology
 and the component tables must be bit-identical; wall time per 60 s clip.
 
 usage: python tools/sn_ab.py OUT.npz           (run once per library)
