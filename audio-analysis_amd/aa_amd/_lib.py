@@ -95,6 +95,11 @@ class FlacInfo(C.Structure):
                 ("total_frames", C.c_int64)]
 
 
+class VorbisInfo(C.Structure):
+    _fields_ = [("sample_rate", C.c_int32), ("channels", C.c_int32), ("blocksize_0", C.c_int32),
+                ("blocksize_1", C.c_int32), ("total_frames", C.c_int64)]
+
+
 _lib = None
 
 _SIGS = {
@@ -167,6 +172,8 @@ _SIGS = {
                                              C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "aa_flac_info": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(FlacInfo)]),
     "aa_flac_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
+    "aa_vorbis_info": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(VorbisInfo)]),
+    "aa_vorbis_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -11,8 +11,11 @@ s24/s32 ``>> 16`` of the 32-bit value (truncation), float ``clip(lrint(x *
 precise ones.  FLAC streams are decoded natively (``aa_flac_decode`` in
 libaa.so, host code) and go through the same s16 conversion: ffmpeg's FLAC
 decoder left-justifies a b-bit sample into s16 (b <= 16) or s32, so the s16
-value is ``x << (16 - b)`` or ``x >> (b - 16)``.  Other containers (MP3, Ogg,
-AAC/M4A, Opus) need a codec this image does not have and are rejected.
+value is ``x << (16 - b)`` or ``x >> (b - 16)``.  Ogg Vorbis streams are
+decoded natively too (``aa_vorbis_decode``, host code): ffmpeg's Vorbis decoder
+outputs float, which libswresample converts to s16 as for float WAV
+(``clip(lrint(x * 32768))``).  Other lossy containers (MP3, AAC/M4A, Opus)
+need a codec this image does not have and are rejected.
 Resampling to 48 kHz (librosa soxr_hq in the reference) runs on the GPU with
 a filter designed to libsoxr's HQ specification (aa_amd.resample) -- parity
 with libsoxr's samples unpinned: libsoxr is not available.
@@ -63,14 +66,45 @@ def decode_flac(data):
     return q, info.channels, info.sample_rate
 
 
+def _float_to_s16(f):
+    """libswresample's packed float -> s16: av_clip_int16(lrint(x * 32768));
+    a NaN converts to the integer indefinite (INT_MIN) and clips to -32768."""
+    with np.errstate(invalid="ignore"):
+        q = np.clip(np.rint(f.astype(np.float64) * 32768.0), -32768, 32767)
+    return np.where(np.isnan(q), -32768.0, q)
+
+
+def decode_vorbis(data):
+    """Ogg Vorbis bytes -> (decoded float32 [frames * channels], channels, sr)."""
+    import ctypes as C
+    from ._lib import VorbisInfo, check, lib
+    buf = np.frombuffer(data, np.uint8)
+    info = VorbisInfo()
+    check(lib().aa_vorbis_info(buf.ctypes.data, buf.size, C.byref(info)), "aa_vorbis_info")
+    n = C.c_int64()
+    # the last granule bounds the output; without one (or an implausible one:
+    # Vorbis needs well over a bit per 64 samples) count the samples first
+    if info.total_frames <= 0 or info.total_frames > 64 * 8 * len(data) + (1 << 20):
+        check(lib().aa_vorbis_decode(buf.ctypes.data, buf.size, None, 0, C.byref(n)), "aa_vorbis_decode")
+        cap = n.value
+    else:
+        cap = info.total_frames
+    out = np.empty(max(cap, 1) * info.channels, np.float32)
+    check(lib().aa_vorbis_decode(buf.ctypes.data, buf.size, out.ctypes.data, cap, C.byref(n)), "aa_vorbis_decode")
+    return out[: n.value * info.channels], info.channels, info.sample_rate
+
+
 def decode(path):
     with open(path, "rb") as f:
         data = f.read()
     if _is_flac(data):
         q, channels, sr = decode_flac(data)
         return _to_mono(q, channels), int(sr)
+    if data[:4] == b"OggS":
+        f, channels, sr = decode_vorbis(data)
+        return _to_mono(_float_to_s16(f), channels), int(sr)
     if len(data) < 12 or data[:4] not in (b"RIFF", b"RF64") or data[8:12] != b"WAVE":
-        raise ValueError(f"{path}: not a RIFF/WAVE or FLAC file")
+        raise ValueError(f"{path}: not a RIFF/WAVE, FLAC or Ogg Vorbis file")
     mv = memoryview(data)  # chunk bodies as views: no copy of the sample payload
     pos, fmt, payload = 12, None, None
     while pos + 8 <= len(data):
@@ -109,11 +143,7 @@ def decode(path):
         if bits not in (32, 64):
             raise ValueError(f"{path}: {bits}-bit IEEE float unsupported")
         f = np.frombuffer(payload[:len(payload) // (bits // 8) * (bits // 8)], "<f4" if bits == 32 else "<f8")
-        with np.errstate(invalid="ignore"):
-            q = np.clip(np.rint(f.astype(np.float64) * 32768.0), -32768, 32767)
-        # a NaN converts to the integer indefinite (INT_MIN) and clips to -32768,
-        # as libswresample's packed float -> s16 conversion does
-        q = np.where(np.isnan(q), -32768.0, q)
+        q = _float_to_s16(f)
     else:
         raise ValueError(f"{path}: WAVE format tag {tag} unsupported")
     return _to_mono(q, channels), int(sr)

@@ -25,6 +25,8 @@
  *   aa_sn_*      signal_noise                       src/identify_tracks.py:650-706
  *   aa_flac_*    load_recording's ffmpeg decode     src/identify_tracks.py:49-62
  *                  (FLAC; host memory, no GPU)
+ *   aa_vorbis_*  load_recording's ffmpeg decode     src/identify_tracks.py:49-62
+ *                  (Ogg Vorbis; host memory, no GPU)
  *
  * Return values: AA_OK (0) or an aa_status code; aa_last_error() gives a
  * thread-local message for the last failing call on this thread.
@@ -361,6 +363,29 @@ int aa_flac_info(const uint8_t* data, size_t len, aa_flac_stream_info* info);
  * n_frames: frames (samples per channel) decoded.  AA_ERR_WORKSPACE when the
  * stream holds more than cap_frames. */
 int aa_flac_decode(const uint8_t* data, size_t len, int32_t* out, int64_t cap_frames, int64_t* n_frames);
+
+/* ---------------------------------------------------------- Ogg Vorbis decode */
+/* load_recording (src/identify_tracks.py:49-62) decodes through ffmpeg; these
+ * decode an Ogg Vorbis stream (RFC 3533 pages, Vorbis I codec: floor 0/1,
+ * residue 0/1/2, channel coupling, short/long blocks) held in HOST memory, on
+ * the calling thread.  Pages failing their CRC-32 are skipped; the first
+ * Vorbis logical stream is decoded.  Samples come out as float32 in [-1, 1]
+ * scale, interleaved, trimmed by the granule positions (Vorbis I A.2); the
+ * caller applies ffmpeg's float -> s16 conversion.  A damaged header is
+ * AA_ERR_INVALID with the reason in aa_last_error. */
+typedef struct aa_vorbis_stream_info {
+    int32_t sample_rate;
+    int32_t channels;        /* 1..255 */
+    int32_t blocksize_0;     /* short block, 64..8192 */
+    int32_t blocksize_1;     /* long block */
+    int64_t total_frames;    /* the last page's granule position (0 = none found) */
+} aa_vorbis_stream_info;
+
+int aa_vorbis_info(const uint8_t* data, size_t len, aa_vorbis_stream_info* info);
+/* out: host float32 [cap_frames][channels], or NULL to count only;
+ * n_frames: frames (samples per channel) decoded.  AA_ERR_WORKSPACE when the
+ * stream holds more than cap_frames. */
+int aa_vorbis_decode(const uint8_t* data, size_t len, float* out, int64_t cap_frames, int64_t* n_frames);
 
 #ifdef __cplusplus
 }

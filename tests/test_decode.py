@@ -67,9 +67,13 @@ def test_stereo_mean_of_s16(tmp_path):
 
 
 def test_rejects_non_wav(tmp_path):
-    p = tmp_path / "a.ogg"
-    p.write_bytes(b"OggS" + b"\0" * 64)
+    p = tmp_path / "a.mp3"
+    p.write_bytes(b"ID3" + b"\0" * 64)
     with pytest.raises(ValueError):
+        decode(p)
+    p = tmp_path / "a.ogg"  # an Ogg capture pattern without a valid page / Vorbis stream
+    p.write_bytes(b"OggS" + b"\0" * 64)
+    with pytest.raises(RuntimeError):
         decode(p)
     p = tmp_path / "a.flac"  # a FLAC marker with a broken metadata chain
     p.write_bytes(b"fLaC" + b"\0" * 64)
