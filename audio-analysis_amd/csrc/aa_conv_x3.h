@@ -230,10 +230,29 @@ __device__ __forceinline__ int x3_eoff(int p, int u) {  // float offset of unit 
     return p * BN + (((u + (p >> PSH)) & (U - 1)) << 2);
 }
 
+// the bias quad x3_store's thread tid applies (its channel unit is fixed)
+template <int BN, int NTHR>
+__device__ __forceinline__ float4 x3_store_bias(const float* __restrict__ bias, int cb, int tid) {
+    constexpr int U = BN / 4, NG16 = NTHR / 16, GPP = U >= 16 ? U / 16 : 1;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int a = (lane >> 2) & 7;
+    const int gi = 4 * wave + (__builtin_popcount(a) & 1) + 2 * (lane >> 5);
+    const int k = ((a >> 1) << 2) | (lane & 3);
+    const int u = U >= 16 ? (gi % GPP) * 16 + k : (k & 7);
+    (void)NG16;
+    return *reinterpret_cast<const float4*>(bias + cb * BN + u * 4);
+}
+
 template <int TH, int TW, int POOL, int BN, int NTHR, bool OUT_SPLIT, bool NOSTORE, int PSH>
 __device__ __forceinline__ void x3_store(const float* E, const float* __restrict__ bias, float* __restrict__ out, int n,
                                          int cb, int oh0, int ow0, int Hout, int Wout, int cout_store, int act,
-                                         float alpha) {
+                                         float alpha, int tid = -1, const float4* bias_pre = nullptr) {
+    // tid: the thread's index among the NTHR storing threads (default: the
+    // block's thread index; the producer waves of conv_x3pc pass their own,
+    // with the thread's bias quad loaded once (bias_pre, x3_store_bias):
+    // a bias load here would make the stores' s_waitcnt vmcnt also wait for
+    // every load the wave issued before it)
+    if (tid < 0) tid = threadIdx.x;
     constexpr int U = BN / 4;
     static_assert(U >= 8 && (U & (U - 1)) == 0, "a power-of-two count (>= 8) of units per pixel");
     static_assert(POOL == 1 || POOL % 2 == 1, "odd pool: neighbouring items alternate row parity");
@@ -242,7 +261,7 @@ __device__ __forceinline__ void x3_store(const float* E, const float* __restrict
     // units of one pooled pixel (U >= 16: GPP groups per pooled pixel)
     constexpr int NG16 = NTHR / 16, GPP = U >= 16 ? U / 16 : 1;
     static_assert(NG16 % GPP == 0, "a lane keeps its unit across passes");
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = tid & 63, wave = tid >> 6;
     const int a = (lane >> 2) & 7;
     const int gi = 4 * wave + (__builtin_popcount(a) & 1) + 2 * (lane >> 5);
     const int k = ((a >> 1) << 2) | (lane & 3);
@@ -250,7 +269,7 @@ __device__ __forceinline__ void x3_store(const float* E, const float* __restrict
     const int qo0 = U >= 16 ? gi / GPP : 2 * gi + (k >> 3);
     constexpr int QSTEP = U >= 16 ? NG16 / GPP : 2 * NG16;
     const int ch0 = cb * BN + u * 4;
-    const float4 bv = *reinterpret_cast<const float4*>(bias + ch0);  // bias is padded to cout_pad
+    const float4 bv = bias_pre ? *bias_pre : *reinterpret_cast<const float4*>(bias + ch0);  // bias is padded to cout_pad
     const int oh0s = oh0 / POOL, ow0s = ow0 / POOL;
     for (int qo = qo0; qo < NPO; qo += QSTEP) {
         const int pr = qo / PWo, pc = qo - (qo / PWo) * PWo;
