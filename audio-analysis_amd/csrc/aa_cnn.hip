@@ -1222,26 +1222,6 @@ static int launch_mfma(const Stage& s, const void* in, void* out, int n, hipStre
 #define AA_WG_CFGS(X) X(9, 64, 3, 1, 4, 3, 1, 39, 6, 0, 6, 1, 2)
 #endif
 
-// conv_wgf (aa_conv_wg.h: the fused first layer + 3x3/32 pooled conv on
-// F(6, 3)): output tile TH x TW, waves WM x WN, fragments MF x NF, pinned
-// waves per SIMD (0: free), B sets in flight BD, first-layer MFMA pairs in
-// flight NU.  48 x 6 tiles: the 156 x 222 conv output of the bench's windows
-// in 4 x 37 tiles, 48 group-pixels = 3 fragments, 53 KiB of LDS (3 blocks per
-// CU).  Opt-in (AA_WGF=1): parity-green, but 220 us against conv_x3's 120 us
-// in the pipeline (tools/wgf_check.hip ablations): at 3
-// waves per block and 3 blocks per CU its first layer, transform and main
-// loop are latency-bound, and with one M fragment per wave its B loads from
-// L2 cost more than the MFMAs they feed.
-#ifdef AA_WGF_ALT
-#define AA_WGF_CFGS(X) AA_WGF_ALT(X)
-#else
-#define AA_WGF_CFGS(X) X(48, 6, 3, 1, 1, 2, 0, 2, 2)
-#endif
-static bool wgf_enabled() {
-    const char* e = getenv("AA_WGF");
-    return e && strcmp(e, "1") == 0;
-}
-
 static int wg_bn(int kh, int kw, int cin, int pool) {
 #define AA_WBN(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS, BD) \
     if (kw == 3 && kh == KH && cin == CIN && pool == POOL) return WN * NF * 16;
@@ -1323,29 +1303,6 @@ static int launch_wg(const Stage& s, const void* in, void* out, int n, hipStream
     dim3 grid(tiles_h * tiles_w, s.cout_pad / BN, n);
     hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, st, (const float*)in, s.Hin, s.Win, (const bf16*)s.d_w,
                        s.d_b, (float*)out, s.Hout, s.Wout, s.cout, tiles_w, s.act, s.alpha);
-    AA_LAUNCH_CHECK();
-    return AA_OK;
-}
-
-template <int TH, int TW, int WM, int WN, int MF, int NF, int OCC, int BD, int NU, bool OUT_SPLIT>
-static int launch_wgf(const Stage& s, const void* in, void* out, int n, hipStream_t st, const Stage* first) {
-    auto k = conv_wgf<TH, TW, WM, WN, MF, NF, OCC, OUT_SPLIT, BD, NU>;
-    constexpr int BN = WN * NF * 16;
-    AA_CHECK(s.cout_pad == BN && s.kh == 3 && s.kw == 3 && s.cin == 32 && s.pool == 3 && s.wg == 6, AA_ERR_UNSUPPORTED,
-             "conv %s: not the fused Winograd pair", s.name.c_str());
-    AA_CHECK((double)first->Hin * first->Win * 4 < 2147483647.0, AA_ERR_UNSUPPORTED,
-             "conv %s: one window's log-mel exceeds 2 GiB", s.name.c_str());
-    const size_t lds = wgf_lds_bytes<TH, TW, BN>();
-    AA_CHECK(lds <= 160 * 1024, AA_ERR_UNSUPPORTED, "conv %s: %zu B LDS", s.name.c_str(), lds);
-    const float slope = first->act == ACT_LEAKY ? first->alpha : first->act == ACT_RELU ? 0.f : 1.f;
-    const FirstConv fc{(const float*)first->d_w, first->d_b, first->act, slope, first->has_mag,
-                       first->mag_exp, first->Hin, first->Win, s.lm_f16};
-    AA_DYN_LDS(k, lds);
-    const int tiles_h = (s.Hout * 3 + TH - 1) / TH;
-    const int tiles_w = (s.Wout * 3 + TW - 1) / TW;
-    dim3 grid(tiles_h * tiles_w, 1, n);
-    hipLaunchKernelGGL(k, grid, dim3(WM * WN * 64), lds, st, (const float*)in, s.Hin, s.Win, (const bf16*)s.d_w,
-                       s.d_b, (float*)out, s.Hout, s.Wout, s.cout, tiles_w, s.act, s.alpha, fc);
     AA_LAUNCH_CHECK();
     return AA_OK;
 }
@@ -1462,13 +1419,6 @@ static int launch_stage(const Model& m, const Stage& s, const void* in, void* ou
                  "no fused first-layer kernel for %s", s.name.c_str());
     }
     if constexpr (is_split<T>()) {
-        if (s.wg && s.fused_first) {
-#define AA_LAUNCHF(TH, TW, WM, WN, MF, NF, OCC, BD, NU)                                                         \
-            return s.out_split ? launch_wgf<TH, TW, WM, WN, MF, NF, OCC, BD, NU, true>(s, in, out, n, st, first)  \
-                               : launch_wgf<TH, TW, WM, WN, MF, NF, OCC, BD, NU, false>(s, in, out, n, st, first);
-            AA_WGF_CFGS(AA_LAUNCHF)
-#undef AA_LAUNCHF
-        }
         if (s.wg) {
 #define AA_LAUNCHW(KH, CIN, POOL, WM, WN, MF, NF, TH, TW, OCC, WO, NPASS, BD)                                       \
             if (s.kh == KH && s.cin == CIN && s.pool == POOL) {                                                   \
@@ -1790,12 +1740,6 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
         s.wg = 0;
         if (precision == AA_PREC_BF16X3 && s.kind == ST_MFMA && wg_bn(s.kh, s.kw, s.cin, s.pool) > 0)
             wg_form(s.kh, s.cin, s.pool, &s.wg, &s.wg_npass);
-        // the pair the first layer fuses into, on F(6, 3) (conv_wgf): its
-        // weights packed as conv_wg's (3 rows x 8 planes)
-        if (precision == AA_PREC_BF16X3 && m->st.size() == 1 && fusable_first(m->st[0], s) && wgf_enabled()) {
-            s.wg = 6;
-            s.wg_npass = 1;
-        }
         const bool rowmajor = s.kind == ST_SMALL || s.kind == ST_GENERIC;  // f32 [cout][K]
         s.cout_pad = rowmajor ? s.cout : (s.cout + bn_tile - 1) / bn_tile * bn_tile;
         // pack weights with the BN scale folded in: conv_small / generic
@@ -1969,15 +1913,15 @@ extern "C" int aa_model_create(const aa_layer* layers, int32_t n_layers, const f
             // a Winograd consumer transforms f32 values before it splits them: it
             // reads plain f32 (one 16-B load per 4 channels, not two 8-B loads and
             // a hi + lo sum); the split layout only pays for global_load_lds staging
-            if (b.wg && !getenv("AA_WG_SPLIT_IN")) continue;
+            if (b.wg) continue;
             a.out_split = 1;
             b.in_split = 1;
         }
     }
     // split-bf16: the 1x3/128 -> 256 conv before a 1x1 head (<= 32 labels) and
     // the head in one kernel (aa_conv_tail.h); the conv's 13 x 20 x 256
-    // activations never reach HBM.  AA_NO_TAIL=1 keeps them separate.
-    if (precision == AA_PREC_BF16X3 && m->st.size() >= 2 && !getenv("AA_NO_TAIL")) {
+    // activations never reach HBM.
+    if (precision == AA_PREC_BF16X3 && m->st.size() >= 2) {
         Stage& h = m->st.back();
         Stage& c = m->st[m->st.size() - 2];
         if (h.kind == ST_HEAD && h.cout <= 32 && h.cout_pad == 32 && h.cin == 256 && c.kind == ST_MFMA && !c.skipped &&

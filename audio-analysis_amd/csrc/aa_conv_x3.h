@@ -149,7 +149,7 @@ __device__ __forceinline__ void split2(float x0, float x1, uint32_t& hi, uint32_
 // inline-asm v_max_f32 of round 5 -- visible to the hazard recognizer, which
 // pads the first VALU read of an MFMA result with the wait states the matrix
 // pipe needs (an asm read right behind the MFMA took stale registers in
-// conv_wgf).  AA_X3_SCALAR_SPLIT 0: the multiply as one packed op.
+// the round-5 conv_wgf).  AA_X3_SCALAR_SPLIT 0: the multiply as one packed op.
 __device__ __forceinline__ void leaky_split2(float x0, float x1, float a, uint32_t& hi, uint32_t& lo) {
     typedef __attribute__((ext_vector_type(2))) float f2;
     typedef __attribute__((ext_vector_type(2))) __bf16 b2;

@@ -903,11 +903,8 @@ static int launch_stft4096(const FePlan& p, const float* pcm, const aa_window* w
     const int n_frames = p.T * n_win;
     // persistent grid: blocks resident together (LDS-limited, 2 per CU at the
     // CFG filterbank), a multiple of 8 for the XCD renumbering
-    static const int cu_cap = [] {  // (A/B knob AA_FE_PER_CU: blocks per CU the grid assumes)
-        const char* e = getenv("AA_FE_PER_CU");
-        return e ? std::max(1, std::atoi(e)) : 2;
-    }();
-    const int per_cu = std::max(1, std::min(cu_cap, (int)((160 * 1024) / lds)));
+    // (1 block per CU measured -1.5 % on the two-stream step, profiles/r05/ab_fe_per_cu.txt)
+    const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
     int grid = std::min((n_frames + kWpb - 1) / kWpb, 256 * per_cu);
     grid = (grid + 7) & ~7;
     hipLaunchKernelGGL(fe_stft_mel_4096<PM>, dim3(grid), dim3(64 * kWpb), lds, st, pcm, wins, stats, p.d_tw,

@@ -77,7 +77,7 @@ struct ConvGeom {
 typedef __attribute__((ext_vector_type(8))) __bf16 gbf16x8;
 typedef __attribute__((ext_vector_type(4))) float gf32x4;
 
-// LDS rows of the patch-staged convs (gconv_x3p / gconv_x3q): 32 bf16 +
+// LDS rows of the patch-staged conv (gconv_x3p): 32 bf16 +
 // GX_PAD.  8 (80 B rows, an odd multiple of 16 B, so the 16 rows of a
 // fragment read sit on distinct banks) instead of round 4's 16 (96 B): the
 // 3x3 32->16 patch kernel 125 -> 107 us -- the smaller patch (52 KiB) also
@@ -379,158 +379,6 @@ __global__ __launch_bounds__(256) void gconv_x3t(const float* __restrict__ in, c
         }
     };
     with_act(act, epi);
-}
-
-// gconv_x3q: stride-1 kernels larger than 1x1 at 64 output channels per
-// block.  The input patch of an 8 x 16 output tile is staged once per
-// 32-channel chunk (as gconv_x3p) and each tap's weight slice goes through a
-// two-slot LDS ring: thread (row r, quad q) loads its piece of tap t+1 into
-// registers before tap t's MFMAs, writes it to the other slot after them, and
-// one barrier per tap publishes it (every wave's reads of that slot, two taps
-// back, are done by then).  2 x 2 waves, each 64 pixels x 32 channels (MF = 4,
-// NF = 2: 24 MFMAs per tap).  Accumulation order: chunk-major, taps in order.
-template <int MF, int NF>
-__global__ __launch_bounds__(256) void gconv_x3q(const float* __restrict__ in, const uint16_t* __restrict__ wpk,
-                                                 const float* __restrict__ bias, float* __restrict__ out,
-                                                 ConvGeom g, int cout_pad, int act, float alpha, int tiles_w,
-                                                 const float* __restrict__ in_scale, const float* __restrict__ res) {
-    constexpr int WM = 2, WN = 2;
-    constexpr int BM = WM * MF * 16, BN = WN * NF * 16, TW = 16, TH = BM / TW;
-    static_assert(BN == 64, "one weight row per 4 threads");
-    extern __shared__ __attribute__((aligned(16))) uint16_t gsm[];
-    const int PH = TH - 1 + g.kh, PW = TW - 1 + g.kw, NP = PH * PW;
-    uint16_t* Ph = gsm;
-    uint16_t* Pl = gsm + NP * GX_ROW;
-    uint16_t* Bs = gsm + 2 * NP * GX_ROW;  // [slot][hi | lo][BN][GX_ROW]
-    const int n = blockIdx.z;
-    const int ty = blockIdx.x / tiles_w, tx = blockIdx.x - (blockIdx.x / tiles_w) * tiles_w;
-    const int oy0 = ty * TH, ox0 = tx * TW;
-    const int ch0 = blockIdx.y * BN;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave % WM, wn = wave / WM;
-    const int br = t >> 2, bq = t & 3;  // weight staging role
-    const int iy0 = oy0 - g.pt, ix0 = ox0 - g.pl;
-    const float* img = in + (size_t)n * g.Hin * g.Win * g.Cin;
-    const float* scl = in_scale ? in_scale + (size_t)n * g.Cin : nullptr;
-    const int ncc = g.cin_pad / 32;
-    const int ntap = g.kh * g.kw;
-    int pb[MF];
-#pragma unroll
-    for (int j = 0; j < MF; ++j) {
-        const int p = wm * MF * 16 + j * 16 + (lane & 15);
-        pb[j] = (p / TW) * PW + (p % TW);
-    }
-    const int ko = 8 * (lane >> 4);
-    gf32x4 acc[NF][MF];
-#pragma unroll
-    for (int i = 0; i < NF; ++i)
-#pragma unroll
-        for (int j = 0; j < MF; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
-    const bool vec = (g.Cin & 7) == 0;
-    uint4 wh, wl;
-    auto load_b = [&](int tap, int cc) {
-        const uint16_t* wrow = wpk + (((size_t)(tap * ncc + cc) * cout_pad) + ch0 + br) * 64;
-        wh = *reinterpret_cast<const uint4*>(wrow + 8 * bq);
-        wl = *reinterpret_cast<const uint4*>(wrow + 32 + 8 * bq);
-    };
-    auto store_b = [&](int slot) {
-        uint16_t* b = Bs + slot * (2 * BN * GX_ROW);
-        *reinterpret_cast<uint4*>(b + br * GX_ROW + 8 * bq) = wh;
-        *reinterpret_cast<uint4*>(b + BN * GX_ROW + br * GX_ROW + 8 * bq) = wl;
-    };
-    for (int cc = 0; cc < ncc; ++cc) {
-        load_b(0, cc);
-        // (the previous chunk's last tap ended on a barrier: patch and slots are free)
-        for (int it = t; it < NP * 4; it += 256) {
-            const int pix = it >> 2, q = it & 3;
-            const int R = pix / PW, C = pix - (pix / PW) * PW;
-            const int iy = iy0 + R, ix = ix0 + C;
-            const bool inside = iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
-            const int c0 = cc * 32 + 8 * q;
-            const float* px = img + ((size_t)(inside ? iy : 0) * g.Win + (inside ? ix : 0)) * g.Cin;
-            float v[8];
-            if (inside && vec && c0 + 8 <= g.Cin) {
-                const float4 a = *reinterpret_cast<const float4*>(px + c0);
-                const float4 b = *reinterpret_cast<const float4*>(px + c0 + 4);
-                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-                v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-                if (scl) {
-                    const float4 sa = *reinterpret_cast<const float4*>(scl + c0);
-                    const float4 sb = *reinterpret_cast<const float4*>(scl + c0 + 4);
-                    v[0] *= sa.x; v[1] *= sa.y; v[2] *= sa.z; v[3] *= sa.w;
-                    v[4] *= sb.x; v[5] *= sb.y; v[6] *= sb.z; v[7] *= sb.w;
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const bool ok = inside && c0 + e < g.Cin;
-                    v[e] = ok ? (scl ? px[c0 + e] * scl[c0 + e] : px[c0 + e]) : 0.f;
-                }
-            }
-            gbf16x8 h, l;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                h[e] = (__bf16)v[e];
-                l[e] = (__bf16)(v[e] - (float)h[e]);
-            }
-            *reinterpret_cast<gbf16x8*>(Ph + pix * GX_ROW + 8 * q) = h;
-            *reinterpret_cast<gbf16x8*>(Pl + pix * GX_ROW + 8 * q) = l;
-        }
-        store_b(0);
-        __syncthreads();
-        for (int tap = 0; tap < ntap; ++tap) {
-            if (tap + 1 < ntap) load_b(tap + 1, cc);
-            const uint16_t* b = Bs + (tap & 1) * (2 * BN * GX_ROW);
-            const int toff = (tap / g.kw) * PW + (tap - (tap / g.kw) * g.kw);
-            gbf16x8 w_h[NF], w_l[NF];
-#pragma unroll
-            for (int i = 0; i < NF; ++i) {
-                const int wr = (wn * NF * 16 + i * 16 + (lane & 15)) * GX_ROW + ko;
-                w_h[i] = *reinterpret_cast<const gbf16x8*>(b + wr);
-                w_l[i] = *reinterpret_cast<const gbf16x8*>(b + BN * GX_ROW + wr);
-            }
-#pragma unroll
-            for (int j = 0; j < MF; ++j) {
-                const int xr = (pb[j] + toff) * GX_ROW + ko;
-                const gbf16x8 x_h = *reinterpret_cast<const gbf16x8*>(Ph + xr);
-                const gbf16x8 x_l = *reinterpret_cast<const gbf16x8*>(Pl + xr);
-#pragma unroll
-                for (int i = 0; i < NF; ++i) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h[i], x_h, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_l[i], x_h, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_h[i], x_l, acc[i][j], 0, 0, 0);
-                }
-            }
-            if (tap + 1 < ntap) store_b((tap + 1) & 1);
-            __syncthreads();
-        }
-    }
-    const int HWo = g.Hout * g.Wout;
-#pragma unroll
-    for (int j = 0; j < MF; ++j) {
-        const int p = wm * MF * 16 + j * 16 + (lane & 15);
-        const int oy = oy0 + p / TW, ox = ox0 + p % TW;
-        if (oy >= g.Hout || ox >= g.Wout) continue;
-        const int Pj = oy * g.Wout + ox;
-        float* o = out + ((size_t)n * HWo + Pj) * g.Cout;
-        const float* rp = res ? res + ((size_t)n * HWo + Pj) * g.Cout : nullptr;
-#pragma unroll
-        for (int i = 0; i < NF; ++i) {
-            const int c = ch0 + wn * NF * 16 + i * 16 + 4 * (lane >> 4);
-            float y[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float z = acc[i][j][e] + (c + e < g.Cout ? bias[c + e] : 0.f);
-                if (rp && c + e < g.Cout) z += rp[c + e];
-                y[e] = gact(z, act, alpha);
-            }
-            if (c + 4 <= g.Cout && (g.Cout & 3) == 0) {
-                *reinterpret_cast<float4*>(o + c) = make_float4(y[0], y[1], y[2], y[3]);
-            } else {
-                for (int e = 0; e < 4 && c + e < g.Cout; ++e) o[c + e] = y[e];
-            }
-        }
-    }
 }
 
 // the split-K slices of a pointwise conv added in slice order, then the

@@ -604,16 +604,9 @@ static void graph_fuse(Graph* G) {
     }
 }
 
-// a pointwise conv over >= 384 channels on a small map (<= split_hw() pixels
+// a pointwise conv over >= 384 channels on a small map (<= kSplitHW pixels
 // per window) is a short grid of long K loops: its K is split over blocks
-// (A/B knob AA_GRAPH_SPLITHW)
-static int split_hw() {
-    static const int v = [] {
-        const char* e = getenv("AA_GRAPH_SPLITHW");
-        return e ? std::atoi(e) : 128;
-    }();
-    return v;
-}
+constexpr int kSplitHW = 128;
 
 static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float* blob, int64_t blob_len) {
     auto get = [&](int64_t off, int64_t n) -> const float* {
@@ -699,7 +692,7 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
                 N.bytes = 4.0 * (H * W * C + N.H * N.W * N.C);
                 // split K over blocks on small maps (shape-only choice: the
                 // sums do not depend on n)
-                if (N.mfma && pointwise && N.H * N.W <= split_hw() && getenv("AA_GRAPH_NOSPLIT") == nullptr) {
+                if (N.mfma && pointwise && N.H * N.W <= kSplitHW) {
                     const int ncc = N.g.cin_pad / 32;
                     for (int cs : {6, 7, 4, 5, 8, 9})
                         if (ncc >= 12 && ncc % cs == 0) {
@@ -862,87 +855,24 @@ static int graph_build(Graph* G, const aa_node* nodes, int n_nodes, const float*
     return AA_OK;
 }
 
-// 128 x 64 tiles (A/B knob AA_GRAPH_WIDE: "k" for kernels larger than 1x1,
-// "all" for every MFMA conv with 64-channel blocks)
-static bool wide_tile(bool spatial) {
-    static const int mode = [] {
-        const char* e = getenv("AA_GRAPH_WIDE");
-        return !e ? 0 : std::strcmp(e, "k") == 0 ? 1 : std::strcmp(e, "all") == 0 ? 2 : 0;
-    }();
-    return mode == 2 || (mode == 1 && spatial);
-}
-
-// largest KC of the 64 x 64 tiles (A/B knob AA_GRAPH_KC, default 2: KC = 4
-// halves the blocks per CU)
-static int kc_max() {
-    static const int k = [] {
-        const char* e = getenv("AA_GRAPH_KC");
-        return e ? std::max(1, std::min(4, std::atoi(e))) : 2;
-    }();
-    return k;
-}
-
-// 64 x 128 tiles for short-K pointwise convs with C_out a multiple of 128
-// (A/B knob AA_GRAPH_NOWIDEN: 42.3k -> 43.2k audio-s/s on the EfficientNetV2 graph)
-static bool wide_n() {
-    static const bool w = getenv("AA_GRAPH_NOWIDEN") == nullptr;
-    return w;
-}
-// 64 x 128 tiles for kernels larger than 1x1 too (A/B knob AA_GRAPH_NOWIDEN3
-// turns it off: 3x3 32->128 160 -> 147 us alone, 139 us with the XCD order,
-// profiles/r04/graph_ab_xcd.txt)
-static bool wide_n3() {
-    static const bool w = getenv("AA_GRAPH_NOWIDEN3") == nullptr;
-    return w;
-}
-
-// channel quads per block of the depthwise conv + pool (A/B knob AA_GRAPH_DWQ:
-// 16 = 64 channels x 32 pixel stripes per 512-thread block, 8 = 32 channels
-// per 256-thread block; the per-channel stripe sums, and so the results, are
-// the same either way.  8: 45.0k -> 45.4k audio-s/s, stage sum unchanged --
-// the smaller blocks pack beside the other stream's kernels,
-// profiles/r04/graph_ab_dwq.txt)
-static int dw_q() {
-    static const int q = [] {
-        const char* e = getenv("AA_GRAPH_DWQ");
-        return e && std::atoi(e) == 16 ? 16 : 8;
-    }();
-    return q;
-}
-
-// AA_GRAPH_DW_ROWWALK=1: the 3x3 depthwise convs pixel by pixel (no
-// chunks; A/B and test knob -- the same sums up to the sign of a zero)
-static bool dw_rowwalk() {
-    static const bool r = getenv("AA_GRAPH_DW_ROWWALK") != nullptr;
-    return r;
-}
-// K steps in flight in the one-chunk 64 x 64 gconv_x3t launches over >= 8
-// chunks (A/B knob AA_GRAPH_PD = 1, 2 or 3; 2: the 672 -> 112 project convs
-// 46 -> 42 us, the step unchanged; 64 / 128 x 224 / 192 / 112 tiles for the
-// pointwise convs measured slower, 112 -> 672 35 -> 46 us:
-// profiles/r05/graph_ab_pw.txt)
-static int gx_pd() {
-    static const int r = [] {
-        const char* e = getenv("AA_GRAPH_PD");
-        const int v = e ? std::atoi(e) : 2;
-        return v >= 1 && v <= 3 ? v : 2;
-    }();
-    return r;
-}
-
-// pixels per thread whose taps are loaded together in the 3x3 depthwise
-// convs (A/B knob AA_GRAPH_DW_PX = 1, 2 or 3).  The dwconv stages of the
-// EfficientNet step: 526 us as round 5's column walk, 363 / 390 / 436 us at
-// 1 / 2 / 3 pixels (4: 456, 252 VGPRs) -- the balance over the stripes and
-// the occupancy matter, not the loads' depth (profiles/r05/graph_ab_dw.txt)
-static int dw_chunk() {
-    static const int r = [] {
-        const char* e = getenv("AA_GRAPH_DW_PX");
-        const int v = e ? std::atoi(e) : 1;
-        return v >= 1 && v <= 3 ? v : 1;
-    }();
-    return r;
-}
+// Tile and kernel choices of the graph's convs, fixed from in-pipeline A/B
+// runs (rounds 4-5; the rejected alternatives are no longer built):
+//  * 64 x 128 gconv_x3t tiles for short-K convs with C_out a multiple of 128,
+//    1x1 and larger kernels (42.3k -> 43.2k audio-s/s on the EfficientNetV2
+//    graph; 3x3 32->128 160 -> 147 us, profiles/r04/graph_ab_xcd.txt);
+//    128 x 64 tiles measured slower;
+//  * KC <= 2 chunks per K step (KC = 4 halves the blocks per CU);
+//  * two K steps in flight in the one-chunk 64 x 64 launches over >= 8 chunks
+//    (the 672 -> 112 project convs 46 -> 42 us; 3 steps and 64 / 128 x 224 /
+//    192 / 112 pointwise tiles slower, profiles/r05/graph_ab_pw.txt);
+//  * the depthwise conv + pool at 8 channel quads per 256-thread block and one
+//    pixel's taps per load batch (dwconv stages 526 -> 363 us against round
+//    5's column walk; 2 / 3 pixels 390 / 436 us, profiles/r05/graph_ab_dw.txt);
+//  * XCD-aware block order (stage sum 3016 -> 2923 us, graph_ab_xcd.txt);
+//  * gconv_x3p (patch-staged) for kernels > 1x1 at C_out <= 16 on 256-pixel
+//    tiles (3x3/32->16 212 -> 149 us); 128-pixel tiles and the stride-1
+//    patch + weight-ring kernel at 64 channels measured slower.
+constexpr int kGxKcMax = 2;
 
 static int graph_run_node(const Graph& G, const GNode& N, const float* x, float* ws, int n, hipStream_t st) {
     const aa_node& d = N.d;
@@ -972,12 +902,7 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     nz = 1;
                     scale_hw = N.H * N.W;
                 }
-                // XCD-aware block order (aa_gconv.h xcd_order; AA_GRAPH_XCD=0 turns it off:
-                // stage sum 3016 -> 2923 us, profiles/r04/graph_ab_xcd.txt)
-                static const int xo = [] {
-                    const char* e = getenv("AA_GRAPH_XCD");
-                    return e ? atoi(e) : 1;
-                }();
+                constexpr int xo = 1;  // XCD-aware block order (aa_gconv.h xcd_order)
                 const float* scl = N.scale_src >= 0 ? buf(N.scale_src) : nullptr;
                 const float* res = N.res_src >= 0 ? buf(N.res_src) : nullptr;
                 const int HWo = g.Hout * g.Wout;
@@ -988,46 +913,25 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                 // 178, 3x3/2 16->64 97 -> 176 us -- its per-tap B loads from L2
                 // stall the short tap loop: gconv_x3t keeps those.)
                 int BM = 0, TW = 0;
-                static const bool nopatch = getenv("AA_GRAPH_NOPATCH") != nullptr;  // (A/B knob)
-                // (A/B knob AA_GRAPH_P128: 128-pixel tiles, 8 x 16, for more blocks per CU)
-                static const bool p128 = getenv("AA_GRAPH_P128") != nullptr;
-                if (d.kh * d.kw > 1 && N.bn == 16 && !nopatch) {
-                    BM = p128 ? 128 : 256;
-                    TW = BM == 64 ? 8 : 16;
+                if (d.kh * d.kw > 1 && N.bn == 16) {
+                    BM = 256;
+                    TW = 16;
                     const int TH = BM / TW;
                     // every patch pixel staged (GX_P_STG items per thread) and the
                     // patch within 64 KiB; otherwise gconv_x3t
                     if (!gconv_x3p_fits((TH - 1) * d.sh + d.kh, (TW - 1) * d.sw + d.kw)) BM = 0;
                 }
-                // (A/B knob AA_GRAPH_Q=1: measured slower -- 3x3 32->128 161 -> 197 us,
-                // 48->192 118 -> 148 us: two waves per SIMD wait out a barrier per tap)
-                static const bool useq = getenv("AA_GRAPH_Q") != nullptr;
-                if (!BM && useq && N.bn == 64 && d.kh * d.kw > 1 && d.kh <= 3 && d.kw <= 3 && d.sh == 1 &&
-                    d.sw == 1) {
-                    // stride 1 at 64 channels per block: patch + two-slot weight ring
-                    const int tiles_w = (N.W + 15) / 16, tiles_h = (N.H + 7) / 8;
-                    const size_t lds = ((size_t)(7 + d.kh) * (15 + d.kw) * 2 + 4 * 64) * GX_ROW * 2;
-                    const dim3 grid((unsigned)(tiles_w * tiles_h), N.cout_pad / 64, n);
-                    hipLaunchKernelGGL((gconv_x3q<4, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w, N.d_b,
-                                       out, g, N.cout_pad, act, d.alpha, tiles_w, scl, res);
-                } else if (BM) {
+                if (BM) {
                     const int TH = BM / TW;
                     const int tiles_w = (N.W + TW - 1) / TW, tiles_h = (N.H + TH - 1) / TH;
                     const size_t lds = (size_t)((TH - 1) * d.sh + d.kh) * ((TW - 1) * d.sw + d.kw) * GX_ROW * 4;
                     const dim3 grid((unsigned)(tiles_w * tiles_h), N.cout_pad / N.bn, n);
-                    if (N.bn == 16 && BM == 128)
-                        hipLaunchKernelGGL((gconv_x3p<4, 1, 2, 1, 16>), grid, dim3(256), lds, st, a,
-                                           (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w,
-                                           scl, res, xo);
-                    else if (N.bn == 16)
+                    if (N.bn == 16)
                         hipLaunchKernelGGL((gconv_x3p<4, 1, 4, 1, 16>), grid, dim3(256), lds, st, a,
                                            (const uint16_t*)N.d_w, N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w,
                                            scl, res, xo);
                     else if (N.bn == 32)
                         hipLaunchKernelGGL((gconv_x3p<4, 1, 2, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
-                                           N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res, xo);
-                    else if (BM == 128)
-                        hipLaunchKernelGGL((gconv_x3p<2, 2, 4, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
                                            N.d_b, out, g, N.cout_pad, act, d.alpha, TW, tiles_w, scl, res, xo);
                     else
                         hipLaunchKernelGGL((gconv_x3p<2, 2, 2, 2>), grid, dim3(256), lds, st, a, (const uint16_t*)N.d_w,
@@ -1041,17 +945,14 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                         AA_X3T(dim3((HWo + 255) / 256, N.cout_pad / 16, nz), 4, 1, 4, 1, 1, 1, 0, nullptr);
                     else if (N.bn == 32)
                         AA_X3T(dim3((HWo + 127) / 128, N.cout_pad / 32, nz), 4, 1, 2, 2, 1, 1, 0, nullptr);
-                    else if (wide_n() && (d.kh * d.kw == 1 || wide_n3()) && N.C >= 128 && N.g.cin_pad <= 256 &&
-                             N.cout_pad % 128 == 0)
+                    else if (N.C >= 128 && N.g.cin_pad <= 256 && N.cout_pad % 128 == 0)
                         // 64 x 128 tiles: half the re-reads of the pixel tile
                         AA_X3T(dim3((HWo + 63) / 64, N.cout_pad / 128, nz), 2, 2, 2, 4, 1, 1, 0, nullptr);
-                    else if (wide_tile(d.kh * d.kw > 1))
-                        AA_X3T(dim3((HWo + 127) / 128, N.cout_pad / 64, nz), 2, 2, 4, 2, 1, 1, 0, nullptr);
                     else if (N.split > 1 && nz == 1) {
                         // split K: slices of cslice chunks on blockIdx.z, then the ordered sum
                         float* part = ws + G.part_off * (size_t)n;
                         const dim3 grid((HWo + 63) / 64, N.cout_pad / 64, N.split);
-                        if (N.cslice % 2 == 0 && kc_max() >= 2) AA_X3T(grid, 2, 2, 2, 2, 2, 1, N.cslice, part);
+                        if (N.cslice % 2 == 0) AA_X3T(grid, 2, 2, 2, 2, 2, 1, N.cslice, part);
                         else AA_X3T(grid, 2, 2, 2, 2, 1, 1, N.cslice, part);
                         AA_LAUNCH_CHECK();
                         const size_t total = (size_t)HWo * N.C;
@@ -1060,15 +961,11 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                     } else {
                         // 64 x 64 tiles, KC 32-channel chunks per K step (the same
                         // products summed in the same order whatever KC is)
-                        const int ncc = N.g.cin_pad / 32, kmax = kc_max();
-                        const int KC = ncc % 4 == 0 && kmax >= 4 ? 4 : ncc % 3 == 0 && kmax >= 3 ? 3
-                                       : ncc % 2 == 0 && kmax >= 2 ? 2 : 1;
+                        const int ncc = N.g.cin_pad / 32;
+                        const int KC = ncc % 2 == 0 && kGxKcMax >= 2 ? 2 : 1;
                         const dim3 grid((HWo + 63) / 64, N.cout_pad / 64, nz);
-                        if (KC == 4) AA_X3T(grid, 2, 2, 2, 2, 4, 1, 0, nullptr);
-                        else if (KC == 3) AA_X3T(grid, 2, 2, 2, 2, 3, 1, 0, nullptr);
-                        else if (KC == 2) AA_X3T(grid, 2, 2, 2, 2, 2, 1, 0, nullptr);
-                        else if (gx_pd() == 2 && ncc >= 8) AA_X3T(grid, 2, 2, 2, 2, 1, 2, 0, nullptr);
-                        else if (gx_pd() == 3 && ncc >= 8) AA_X3T(grid, 2, 2, 2, 2, 1, 3, 0, nullptr);
+                        if (KC == 2) AA_X3T(grid, 2, 2, 2, 2, 2, 1, 0, nullptr);
+                        else if (ncc >= 8) AA_X3T(grid, 2, 2, 2, 2, 1, 2, 0, nullptr);
                         else AA_X3T(grid, 2, 2, 2, 2, 1, 1, 0, nullptr);
                     }
 #undef AA_X3T
@@ -1081,8 +978,7 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                                    out, Cin, N.C, act, d.alpha);
             } else if (d.kh * d.kw * Cin <= GF32_KMAX) {
                 const dim3 grid((N.H * N.W + 255) / 256, (N.C + 31) / 32, n);
-                static const bool nosgpr = getenv("AA_GRAPH_NOSGPR") != nullptr;  // (A/B knob)
-                if (N.d_ws && !nosgpr)  // an RGB-style stem, weights through the scalar cache
+                if (N.d_ws)  // an RGB-style stem, weights through the scalar cache
                     hipLaunchKernelGGL((gconv_f32_s<3, 3, 3>), grid, dim3(256), 0, st, a, (const float*)N.d_ws, N.d_b,
                                        out, N.g, act, d.alpha);
                 else if (d.kh == 3 && d.kw == 3 && Cin == 3)
@@ -1109,21 +1005,11 @@ static int graph_run_node(const Graph& G, const GNode& N, const float* x, float*
                        st, a, (const float*)N.d_w, N.d_b, out, pooled, Hin, Win, Cin, N.H, N.W, d.kh, d.kw, d.sh,    \
                        d.sw, d.pt, d.pl, act, d.alpha, P.d.act, P.d.alpha)
                     const bool k3 = d.kh == 3 && d.kw == 3;
-                    const int cs = k3 && d.sh == d.sw && (d.sh == 1 || d.sh == 2) && !dw_rowwalk() ? d.sh : 0;
-                    const int px = dw_chunk();
-                    if (dw_q() == 8) {
-                        if (cs == 1 && px == 2) AA_DWP(8, 3, 1, 2);
-                        else if (cs == 1 && px == 3) AA_DWP(8, 3, 1, 3);
-                        else if (cs == 1) AA_DWP(8, 3, 1, 1);
-                        else if (cs == 2 && px == 2) AA_DWP(8, 3, 2, 2);
-                        else if (cs == 2 && px == 3) AA_DWP(8, 3, 2, 3);
-                        else if (cs == 2) AA_DWP(8, 3, 2, 1);
-                        else if (k3) AA_DWP(8, 3, 0, 1);
-                        else AA_DWP(8, 0, 0, 1);
-                    } else if (cs == 1) AA_DWP(16, 3, 1, 1);
-                    else if (cs == 2) AA_DWP(16, 3, 2, 1);
-                    else if (k3) AA_DWP(16, 3, 0, 1);
-                    else AA_DWP(16, 0, 0, 1);
+                    const int cs = k3 && d.sh == d.sw && (d.sh == 1 || d.sh == 2) ? d.sh : 0;
+                    if (cs == 1) AA_DWP(8, 3, 1, 1);
+                    else if (cs == 2) AA_DWP(8, 3, 2, 1);
+                    else if (k3) AA_DWP(8, 3, 0, 1);
+                    else AA_DWP(8, 0, 0, 1);
 #undef AA_DWP
                 } else {
                     hipLaunchKernelGGL(gdwconv_pool, dim3((Cin + 63) / 64, n), dim3(64 * GP_STRIPES), 0, st, a,
@@ -1257,10 +1143,9 @@ extern "C" int aa_graph_forward(void* graph, const float* x, int32_t n, float* l
     hipStream_t st = static_cast<hipStream_t>(stream);
     float* ws = static_cast<float*>(workspace);
     const size_t in_per = (size_t)G->in_h * G->in_w * G->in_c;
-    static const bool no_capture = getenv("AA_GRAPH_NOCAPTURE") != nullptr;  // (A/B knob)
     // replay a captured forward (not while timing nodes: the events would be
     // baked into the capture; not on the legacy null stream, which cannot capture)
-    if (n <= CHUNK && G->time_stage == -2 && st != nullptr && !no_capture) {
+    if (n <= CHUNK && G->time_stage == -2 && st != nullptr) {
         std::lock_guard<std::mutex> lk(G->cap_mu);
         auto same = [&](const Graph::Captured& c) {
             return c.x == x && c.n == n && c.ws == workspace && c.logits == logits && c.probs == probs && c.st == st;

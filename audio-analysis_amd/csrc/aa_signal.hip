@@ -71,17 +71,8 @@ struct SnPlan {
     int wmin = 0, hmin = 0;  // kept: width >= wmin, height >= hmin (:689-691)
     double2* d_tab = nullptr;  // sn_stft64's tables (kS64Tab*)
     StageTimer timer;          // HIP events around the launches of the stages in timer.mask
-    bool select_reg = false;   // row medians by sn_select_reg (AA_SN_SELECT=reg; A/B knob) or sn_select
-    bool stft_r8 = false;      // the transform by sn_stft64r8 (AA_SN_STFT=r8; A/B knob) or sn_stft64
     bool tw_chain = true;      // sn_stft64's twiddle ladders from 7 table values (AA_SN_TW=table: all 22;
                                // 99 -> 94.5 us per 60 s clip, S bit-identical on the tests' clips)
-    bool colmed_fused = false; // column medians inside sn_stft64 (AA_SN_COLMED=fused; A/B knob: 188 us per
-                               // clip against 98 + 44 as two launches) or their own launch
-    bool colmed_bs = false;    // column medians by bit-serial search (AA_SN_COLMED=bs; A/B knob: 52 us against
-                               // the LDS-histogram radix select's 44) or radix select
-    int diag = 0;              // AA_SN_DIAG: ablation bits of sn_select_reg (tools only; results then invalid)
-    int stft_blocks = 1024;    // sn_stft64 grid (AA_SN_STFT_BLOCKS; A/B knob): 1024 = 4 resident blocks per
-                               // CU, persistent; more blocks leave the frame balance to the dispatcher
 };
 
 __device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
@@ -300,11 +291,6 @@ static_assert(16 * kS64R1 <= kS64Buf && (kS64Mag + 2049) * 4 <= kS64Buf * 16, "s
 // split's per-thread base.
 __device__ unsigned wave_median_2049(const unsigned (&v)[33], unsigned* hists, int lane);
 
-// colmed (may be null; A/B variant AA_SN_COLMED=fused): the frame's median
-// over bins, by wave 0 from the LDS copy of the magnitudes while wave 1 waits
-// at the frame's last barrier.  Measured 188 us per clip against 98 + 44 us as
-// two launches: the select holds the block -- and its 36 KiB of LDS -- far
-// longer than the transform, and 4 blocks per CU leave nothing to fill in.
 // TWC (default; AA_SN_TW=table for all table values): per frame only W^1, W^2, W^4 (W^8) of each twiddle
 // ladder come from the tables (L2); the other powers are their products in
 // f64 (<= 3 roundings of 2^-53: the f32 magnitudes can move only on rounding
@@ -314,7 +300,7 @@ template <bool TWC>
 __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) void sn_stft64(
     const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const double2* __restrict__ win2,
     const double2* __restrict__ tw1, const double2* __restrict__ tw3, const double2* __restrict__ twS,
-    float* __restrict__ S, int ld, unsigned* __restrict__ gmax, unsigned* __restrict__ colmed = nullptr) {
+    float* __restrict__ S, int ld, unsigned* __restrict__ gmax) {
     __shared__ double2 buf[kS64Buf];
     const int t = threadIdx.x;
     const bool z = t == 0;
@@ -494,16 +480,6 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
             srow[2048] = m;
             wmax = max(wmax, __float_as_uint(m));
         }
-        if (colmed && t < 64) {
-            unsigned vv[33];
-#pragma unroll
-            for (int i = 0; i < 32; ++i) vv[i] = __float_as_uint(mag[t + 64 * i]);
-            vv[32] = z ? __float_as_uint(mag[2048]) : 0u;
-            // histograms after the magnitudes (floats 64 .. 2112 of the buffer)
-            unsigned* hists = reinterpret_cast<unsigned*>(buf) + 2176;
-            const unsigned med = wave_median_2049(vv, hists, t);
-            if (z) colmed[fi] = med;
-        }
         __syncthreads();  // the buffer is rewritten by the next frame
     }
     if (gmax) {
@@ -513,135 +489,6 @@ __global__ __launch_bounds__(kS64T) __attribute__((amdgpu_waves_per_eu(2, 2))) v
     }
 }
 
-// sn_stft64r8: the same transform on 256 threads per frame, 2048 = 8 x 8 x 8 x
-// 4, every stage on all threads (8 points each), so a thread holds half the
-// registers of sn_stft64 and a CU keeps 4 frames of 4 waves in flight (LDS
-// 36,864 B per block) instead of 4 frames of 2 waves.  n = 256 a + m, m = 32 b
-// + r, r = 4 c + d; k = k1 + 8 k2 + 64 k3 + 512 k4:
-//   1. thread m: DFT-8 over a, twiddle W2048^(m k1)            -> [k1][m]
-//   2. thread (r, k1): DFT-8 over b, twiddle W256^(r k2)       -> [k2][k1][r]
-//   3. thread (d, k1, k2): DFT-8 over c, twiddle W32^(d k3)    -> [d][k1 + 8 k2 + 64 k3]
-//   4. thread q, q + 256 (q = k1 + 8 k2 + 64 k3): DFT-4 over d -> Z[q + 512 k4]
-//   then thread t splits bins k = t + 256 i and 2048 - k (i < 4; thread 0 also
-//   bin 1024), writing the magnitudes straight to the S row (both runs
-//   coalesced).  Exchange layouts padded so every ds_read/write_b128 wave
-//   group touches 16 distinct 16-B bank groups: [k2][k1][r] with strides 288 /
-//   36 (36 = 4 mod 16: stage 3's lanes (d, k1 < 4) land on 4 k1 + d), [d][q]
-//   with stride 516.
-constexpr int kR8T = 256;
-constexpr int kR8K1 = 36, kR8K2 = 288, kR8D = 516, kR8Buf = 8 * kR8K2;
-// SnPlan::d_tab after sn_stft64's tables: tw1 [7][256] W2048^(m k1) | tw2 [7][32]
-// W256^(r k2) | tw3 [7][4] W32^(d k3) | split bases [256] W4096^t
-constexpr int kR8Tw1 = kS64TabN, kR8Tw2 = kR8Tw1 + 7 * 256, kR8Tw3 = kR8Tw2 + 7 * 32, kR8TwS = kR8Tw3 + 7 * 4,
-              kR8TabN = kR8TwS + 256;
-static_assert(7 * kR8K2 + 7 * kR8K1 + 32 <= kR8Buf && 3 * kR8D + 512 <= kR8Buf, "sn_stft64r8 LDS");
-
-__global__ __launch_bounds__(kR8T) __attribute__((amdgpu_waves_per_eu(4, 4))) void sn_stft64r8(
-    const float* __restrict__ pcm, int n_samples, int hop, int n_frames, const double2* __restrict__ win2,
-    const double2* __restrict__ tw1, const double2* __restrict__ tw2, const double2* __restrict__ tw3,
-    const double2* __restrict__ twS, float* __restrict__ S, int ld, unsigned* __restrict__ gmax) {
-    __shared__ double2 buf[kR8Buf];
-    const int t = threadIdx.x;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)pcm, 0, n_samples * 4, 0x00020000);
-    const double2 tb = twS[t];
-    const int r2 = t & 31, k1b = t >> 5;                         // stage 2
-    const int d3 = t & 3, k1c = (t >> 2) & 7, k2c = t >> 5;      // stage 3
-    unsigned wmax = 0;
-    const int nbx = gridDim.x >> 3;
-    const int xcd = blockIdx.x & 7;
-    const int f_end = (int)((long long)(xcd + 1) * n_frames / 8);
-#pragma unroll 1
-    for (int fi = (int)((long long)xcd * n_frames / 8) + (blockIdx.x >> 3); fi < f_end; fi += nbx) {
-        // opaque table indices: the loop-invariant twiddle loads stay per frame
-        int iw = t, i1 = t, i2 = r2, i3 = d3;
-        __asm__ volatile("" : "+v"(iw), "+v"(i1), "+v"(i2), "+v"(i3));
-        double2 v[8];
-        {
-            const int off = fi * hop - 2048 + 2 * t;
-            int offo = off + 1;  // (a merged dwordx2 would be range-checked as a unit)
-            __asm__ volatile("" : "+v"(offo));
-#pragma unroll
-            for (int a = 0; a < 8; ++a) {
-                const float xe = load_view(rs, off + 512 * a), xo = load_view(rs, offo + 512 * a);
-                const double2 w = win2[256 * a + iw];
-                v[a] = make_double2((double)xe * w.x, (double)xo * w.y);
-            }
-        }
-        // ---- 1 ----
-        ddft8(v);
-#pragma unroll
-        for (int k = 1; k < 8; ++k) v[k] = dmul(v[k], tw1[(k - 1) * 256 + i1]);
-        __syncthreads();  // the previous frame's split has read the buffer
-#pragma unroll
-        for (int k = 0; k < 8; ++k) buf[k * 256 + t] = v[k];
-        __syncthreads();
-        // ---- 2 ----
-#pragma unroll
-        for (int b = 0; b < 8; ++b) v[b] = buf[k1b * 256 + 32 * b + r2];
-        ddft8(v);
-#pragma unroll
-        for (int k = 1; k < 8; ++k) v[k] = dmul(v[k], tw2[(k - 1) * 32 + i2]);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 8; ++k) buf[k * kR8K2 + k1b * kR8K1 + r2] = v[k];
-        __syncthreads();
-        // ---- 3 ----
-#pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = buf[k2c * kR8K2 + k1c * kR8K1 + 4 * c + d3];
-        ddft8(v);
-#pragma unroll
-        for (int k = 1; k < 8; ++k) v[k] = dmul(v[k], tw3[(k - 1) * 4 + i3]);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 8; ++k) buf[d3 * kR8D + k1c + 8 * k2c + 64 * k] = v[k];
-        __syncthreads();
-        // ---- 4 ----
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int d = 0; d < 4; ++d) v[4 * h + d] = buf[d * kR8D + t + 256 * h];
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            ddft4(v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) buf[t + 256 * h + 512 * k] = v[4 * h + k];
-        }
-        __syncthreads();
-        // ---- real split (the window carries its 1/2): a = Z[k], b = Z[2048 - k],
-        // X[k] = E + W4096^k O, X[2048 - k] = conj(E - W4096^k O); k = 0 gives the
-        // DC and Nyquist bins (a = b = Z[0], W = 1) ----
-        float* srow = S + (size_t)fi * ld;
-        auto split = [&](int ka, double2 w) {
-            const double2 a = buf[ka], b = buf[(2048 - ka) & 2047];
-            const double2 E = make_double2(a.x + b.x, a.y - b.y);
-            const double2 O = make_double2(a.y + b.y, b.x - a.x);
-            const double2 q = dmul(w, O);
-            const float m1 = np_cabsf(E.x + q.x, E.y + q.y), m2 = np_cabsf(E.x - q.x, q.y - E.y);
-            srow[ka] = m1;
-            srow[2048 - ka] = m2;
-            // (bit patterns of non-negative floats order like the values; NaN / inf on top)
-            wmax = max(wmax, max(__float_as_uint(m1), __float_as_uint(m2)));
-        };
-        split(t, tb);
-        split(t + 256, w16<1>(tb));
-        split(t + 512, w16<2>(tb));
-        split(t + 768, w16<3>(tb));
-        if (t == 0) {  // bin 1024 pairs with itself: W4096^1024 = -i
-            const double2 a = buf[1024];
-            const double2 E = make_double2(a.x + a.x, 0.0);
-            const double2 q = dnegi(make_double2(a.y + a.y, 0.0));
-            const float m = np_cabsf(E.x + q.x, E.y + q.y);
-            srow[1024] = m;
-            wmax = max(wmax, __float_as_uint(m));
-        }
-    }
-    if (gmax) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (unsigned)__shfl_xor((int)wmax, o, 64));
-        if ((t & 63) == 0 && wmax) atomicMax(gmax, wmax);
-    }
-}
 
 // ---------------------------------------------------------------------------
 // The median over bins of one frame (numpy, odd count 2049: the middle
@@ -706,60 +553,14 @@ __device__ __forceinline__ unsigned wave_median_2049(const unsigned (&v)[33], un
     return prefix;
 }
 
-// The same median by a bit-serial search with no LDS (A/B variant, measured
-// slower: VALU-bound at ~27 bits x 70 ops per frame): from the bits below the
-// frame's common min / max prefix down, keep a candidate bit when fewer than
-// rank + 1 values lie below the candidate.  A count is 33 compare-and-adds per
-// lane and a DPP reduction (popcounting the 33 ballots instead kept the one
-// scalar unit a CU shares busy: 52 us against the histograms' 44); the
-// histogram atomics and their bank conflicts are gone.  Values outside the frame (v[32] of lanes
-// other than 0) are 0xFFFFFFFF: never below a candidate.  The result is the
-// exact (rank)-th smallest pattern, as wave_median_2049's.
-__device__ __forceinline__ unsigned wave_median_2049_bs(const unsigned (&v)[33], int lane) {
-    unsigned mn = v[0], mx = v[0];
-#pragma unroll
-    for (int i = 1; i < 33; ++i) {
-        if (i == 32 && lane != 0) break;
-        mn = min(mn, v[i]);
-        mx = max(mx, v[i]);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
-        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
-    }
-    mn = __builtin_amdgcn_readfirstlane(mn);
-    mx = __builtin_amdgcn_readfirstlane(mx);
-    if (mn == mx) return mn;
-    const int hb = 31 - __clz(mn ^ mx);
-    unsigned ans = hb == 31 ? 0u : (mn & (0xFFFFFFFFu << (hb + 1)));
-    const unsigned rank = kSnBins / 2;
-#pragma unroll 1
-    for (int b = hb; b >= 0; --b) {
-        const unsigned cand = ans | (1u << b);
-        unsigned c = 0;  // the lane's values below the candidate (compare + carry-add each)
-#pragma unroll
-        for (int i = 0; i < 33; ++i) c += v[i] < cand ? 1u : 0u;
-        // the wave's sum: within rows of 16 lanes by DPP, then the four row sums
-        c += (unsigned)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-        c += (unsigned)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-        c += (unsigned)__builtin_amdgcn_update_dpp(0, (int)c, 0x124, 0xF, 0xF, false);  // row_ror:4
-        c += (unsigned)__builtin_amdgcn_update_dpp(0, (int)c, 0x128, 0xF, 0xF, false);  // row_ror:8
-        const unsigned cnt = __builtin_amdgcn_readlane(c, 0) + __builtin_amdgcn_readlane(c, 16) +
-                             __builtin_amdgcn_readlane(c, 32) + __builtin_amdgcn_readlane(c, 48);
-        if (cnt <= rank) ans = cand;  // (wave-uniform)
-    }
-    return ans;
-}
 
 // sn_colmed: one wave per frame, the frame's S row (2049 floats, just
 // written by sn_stft64: L2 / Infinity-Cache resident) into registers, its
 // median over bins into colmed[f].  Four frames per 256-thread block, 4 KiB
 // of histograms per wave.
-template <bool BS>
 __global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, int ld, int n_frames,
                                                  unsigned* __restrict__ colmed) {
-    __shared__ unsigned hists[BS ? 1 : 4][BS ? 1 : 4 * kSnHist];
+    __shared__ unsigned hists[4][4 * kSnHist];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.x * 4 + wave;
     if (f >= n_frames) return;  // wave-uniform; no block barrier below
@@ -767,14 +568,8 @@ __global__ __launch_bounds__(256) void sn_colmed(const float* __restrict__ S, in
     unsigned v[33];
 #pragma unroll
     for (int i = 0; i < 32; ++i) v[i] = row[lane + 64 * i];
-    unsigned med;
-    if constexpr (BS) {
-        v[32] = lane == 0 ? row[2048] : 0xFFFFFFFFu;
-        med = wave_median_2049_bs(v, lane);
-    } else {
-        v[32] = lane == 0 ? row[2048] : 0u;
-        med = wave_median_2049(v, hists[wave], lane);
-    }
+    v[32] = lane == 0 ? row[2048] : 0u;
+    const unsigned med = wave_median_2049(v, hists[wave], lane);
     if (lane == 0) colmed[f] = med;
 }
 
@@ -912,201 +707,11 @@ __global__ __launch_bounds__(256) void sn_select(const float* __restrict__ X, in
     }
 }
 
-// ---------------------------------------------------------------------------
-// sn_select_reg: the row median and mask of sn_select with the row held in
-// registers (512 threads x 24 values: rows of up to 12,288 frames; longer
-// rows take sn_select<false>).  One block-wide 8-bit radix pass (per-wave
-// histograms, folded, every wave picking the same bucket) usually leaves a
-// few hundred candidates in the median's bucket; they are compacted into LDS
-// and wave 0 finishes the select over them in registers with wave-local
-// histograms -- no further block barriers, no re-read of the row.  Buckets
-// larger than kSelCand (long runs of equal values, e.g. digital silence) take
-// more block-wide passes first.  Then the mask bits from the same registers.
-// ---------------------------------------------------------------------------
-constexpr int kSelT = 512, kSelPer = 24, kSelCand = 1024;
-constexpr int kSelNW = kSelT / 64;
-
-__global__ __launch_bounds__(kSelT) __attribute__((amdgpu_waves_per_eu(4))) void sn_select_reg(const float* __restrict__ X, int ld, int n,
-                                                      const unsigned* __restrict__ gmax,
-                                                      const float* __restrict__ c3, int words,
-                                                      unsigned long long* __restrict__ M, int diag) {
-    __shared__ unsigned hist[kSelNW][256];
-    __shared__ unsigned cand[kSelCand];
-    __shared__ unsigned red[64];
-    const unsigned* grow = reinterpret_cast<const unsigned*>(X) + (size_t)blockIdx.x * ld;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    unsigned v[kSelPer];
-    unsigned mn = 0xFFFFFFFFu, mx = 0;
-#pragma unroll
-    for (int i = 0; i < kSelPer; ++i) {
-        const int f = tid + kSelT * i;
-        v[i] = f < n ? grow[f] : 0u;
-        if (f < n) {
-            mn = min(mn, v[i]);
-            mx = max(mx, v[i]);
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
-        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
-    }
-    if (lane == 0) {
-        red[wv] = mn;
-        red[kSelNW + wv] = mx;
-    }
-    reinterpret_cast<uint4*>(&hist[0][0])[tid] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
-    mn = red[0];
-    mx = red[kSelNW];
-#pragma unroll
-    for (int w = 1; w < kSelNW; ++w) {
-        mn = min(mn, red[w]);
-        mx = max(mx, red[kSelNW + w]);
-    }
-    unsigned rlo = mn, rhi = mn;  // a constant row (block-uniform): its value
-    if (mn != mx && !(diag & 1)) {
-        const int hb = 31 - __clz(mn ^ mx);
-        unsigned pmask = hb == 31 ? 0u : (0xFFFFFFFFu << (hb + 1));
-        unsigned prefix = mn & pmask, rank = (unsigned)(n - 1) / 2, cnt = 0;
-        int shift = max(hb - 7, 0);
-        bool done = false;
-        // ---- block-wide passes until the median's bucket fits kSelCand ----
-#pragma unroll 1
-        for (;;) {
-#pragma unroll
-            for (int i = 0; i < kSelPer; ++i)
-                hist_add(&hist[wv][0], (v[i] >> shift) & 255u, tid + kSelT * i < n && (v[i] & pmask) == prefix);
-            __syncthreads();
-            if (tid < 256) {
-                unsigned s = hist[0][tid];
-#pragma unroll
-                for (int w = 1; w < kSelNW; ++w) s += hist[w][tid];
-                hist[0][tid] = s;
-            }
-            __syncthreads();
-            unsigned below, c;  // every wave picks the same bucket
-            const unsigned dig = hist_pick(&hist[0][0], rank, lane, &below, &c);
-            prefix = (prefix & ~(255u << shift)) | (dig << shift);
-            pmask |= 255u << shift;
-            rank -= below;
-            cnt = c;
-            if (shift == 0) {
-                done = true;
-                break;
-            }
-            if (cnt <= (unsigned)kSelCand) break;  // block-uniform
-            __syncthreads();  // every wave has read the folded copy
-            reinterpret_cast<uint4*>(&hist[0][0])[tid] = make_uint4(0u, 0u, 0u, 0u);
-            __syncthreads();
-            shift = max(shift - 8, 0);
-        }
-        if (!done) {
-            // ---- compact the bucket's cnt values (block exclusive scan of the
-            // per-thread counts), then wave 0 selects among them ----
-            unsigned mine = 0;
-#pragma unroll
-            for (int i = 0; i < kSelPer; ++i) mine += (tid + kSelT * i < n && (v[i] & pmask) == prefix) ? 1u : 0u;
-            const unsigned incl = wave_incl_scan(mine, lane);
-            if (lane == 63) red[16 + wv] = incl;
-            __syncthreads();
-            unsigned pos = incl - mine;
-            for (int w = 0; w < wv; ++w) pos += red[16 + w];
-#pragma unroll
-            for (int i = 0; i < kSelPer; ++i)
-                if (tid + kSelT * i < n && (v[i] & pmask) == prefix) cand[pos++] = v[i];
-            __syncthreads();
-            if (wv == 0) {
-                unsigned cv[kSelCand / 64];
-#pragma unroll
-                for (int j = 0; j < kSelCand / 64; ++j) {
-                    const int idx = lane + 64 * j;
-                    cv[j] = idx < (int)cnt ? cand[idx] : 0u;
-                }
-#pragma unroll 1
-                do {
-                    shift = max(shift - 8, 0);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(&hist[q][0])[lane] = make_uint4(0u, 0u, 0u, 0u);
-                    wave_sync();
-#pragma unroll
-                    for (int j = 0; j < kSelCand / 64; ++j)
-                        hist_add(&hist[lane & 3][0], (cv[j] >> shift) & 255u,
-                                 lane + 64 * j < (int)cnt && (cv[j] & pmask) == prefix);
-                    wave_sync();
-                    uint4 c4 = reinterpret_cast<const uint4*>(&hist[0][0])[lane];
-#pragma unroll
-                    for (int q = 1; q < 4; ++q) {
-                        const uint4 u = reinterpret_cast<const uint4*>(&hist[q][0])[lane];
-                        c4.x += u.x;
-                        c4.y += u.y;
-                        c4.z += u.z;
-                        c4.w += u.w;
-                    }
-                    unsigned below, c;
-                    const unsigned dig = hist_pick4(c4, rank, lane, &below, &c);
-                    prefix = (prefix & ~(255u << shift)) | (dig << shift);
-                    pmask |= 255u << shift;
-                    rank -= below;
-                    cnt = c;
-                    wave_sync();
-                } while (shift > 0);
-                if (lane == 0) {
-                    red[32] = prefix;
-                    red[33] = rank;
-                    red[34] = cnt;
-                }
-            }
-            __syncthreads();
-            prefix = red[32];
-            rank = red[33];
-            cnt = red[34];
-        }
-        // prefix: the rank-(n-1)/2 element, `rank` its place among the cnt equal ones
-        rlo = rhi = prefix;
-        if ((n & 1) == 0 && rank + 1 >= cnt) {  // block-uniform: rank n/2 is the next larger value
-            unsigned m2 = 0xFFFFFFFFu;
-#pragma unroll
-            for (int i = 0; i < kSelPer; ++i)
-                if (tid + kSelT * i < n && v[i] > prefix) m2 = min(m2, v[i]);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) m2 = min(m2, (unsigned)__shfl_xor((int)m2, o, 64));
-            if (lane == 0) red[40 + wv] = m2;
-            __syncthreads();
-            rhi = red[40];
-#pragma unroll
-            for (int w = 1; w < kSelNW; ++w) rhi = min(rhi, red[40 + w]);
-        }
-    }
-    // ---- the row's mask (sn_select's numpy f32 steps): bit f % 64 of word
-    // f / 64; lane l of wave w holds frame 512 i + 64 w + l at iteration i ----
-    const float a = __uint_as_float(*gmax);
-    float dr = __fdiv_rn(__uint_as_float(rlo), a);
-    if ((n & 1) == 0) dr = __fmul_rn(__fadd_rn(dr, __fdiv_rn(__uint_as_float(rhi), a)), 0.5f);
-    const float rb = __fmul_rn(3.f, dr);
-    if (diag & 2) {  // ablation: no mask
-        if (tid == 0) M[(size_t)blockIdx.x * words] = rlo ^ rhi;
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < kSelPer; ++i) {
-        const int w = kSelNW * i + wv;
-        if (w >= words) break;  // wave-uniform
-        const int f = tid + kSelT * i;
-        bool bit = false;
-        if (f < n) {
-            const float d = __fdiv_rn(__uint_as_float(v[i]), a);
-            bit = d > c3[f] && d > rb;
-        }
-        const unsigned long long m = __ballot(bit);
-        if (lane == 0) M[(size_t)blockIdx.x * words + w] = m;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // sn_select_row: the row median and mask of sn_select with the row in
-// registers: 256 threads x 40 values (rows of up to 10,240 frames -- a 57 s
-// recording; sn_select_reg / sn_select above that) so that 6 blocks share a
+// registers: 256 threads x 41 values (rows of up to 10,496 frames -- a 58 s
+// recording; sn_select above that) so that 6 blocks share a
 // CU: the row's passes are latency chains (histogram, barrier, pick), and
 // rows in flight are what hides them.  Per pass every wave counts its values
 // into its own 256-bucket histogram (wave-aggregated atomics), then every
@@ -1596,22 +1201,19 @@ static int sn_components(SnPlan& p, const SnWs& ws, const SnBatch& nb, bool with
 // sn_stft64 over one recording: persistent blocks (4 per CU, the LDS limit),
 // a multiple of 8 so every XCD owns an equal share of the blocks
 static int sn_launch_stft(SnPlan& p, const float* pcm, int64_t n, int F, float* S, int ld, unsigned* gmax,
-                          hipStream_t st, unsigned* colmed = nullptr) {
-    int grid = std::min(F, p.stft_blocks);
+                          hipStream_t st) {
+    int grid = std::min(F, 1024);  // 1024 = 4 resident blocks per CU, persistent
     grid = (grid + 7) & ~7;
     const double2* tab = p.d_tab;
     hipEvent_t e0;
     int rc = p.timer.begin(SN_STAGE_STFT, st, &e0);
     if (rc != AA_OK) return rc;
-    if (p.stft_r8)
-        hipLaunchKernelGGL(sn_stft64r8, dim3(grid), dim3(kR8T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
-                           tab + kR8Tw1, tab + kR8Tw2, tab + kR8Tw3, tab + kR8TwS, S, ld, gmax);
-    else if (p.tw_chain)
+    if (p.tw_chain)
         hipLaunchKernelGGL(sn_stft64<true>, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
-                           tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax, colmed);
+                           tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax);
     else
         hipLaunchKernelGGL(sn_stft64<false>, dim3(grid), dim3(kS64T), 0, st, pcm, (int)n, p.cfg.hop_length, F, tab,
-                           tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax, colmed);
+                           tab + kS64TabTw1, tab + kS64TabTw3, tab + kS64TabTwS, S, ld, gmax);
     AA_LAUNCH_CHECK();
     return p.timer.end(SN_STAGE_STFT, st, e0);
 }
@@ -1645,22 +1247,13 @@ static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const i
         unsigned* colmed = sn_at(ws.colmed, ws.pf, k);
         float* c3 = sn_at(ws.c3, ws.pf, k);
         unsigned long long* M0 = sn_at(ws.M0, ws.pf, k);
-        // column medians as their own sn_colmed launch (default), or inside
-        // sn_stft64 with AA_SN_COLMED=fused
-        const bool fused = p->colmed_fused && !p->stft_r8 && !p->colmed_bs;
-        int rc = sn_launch_stft(*p, lens[k] ? pcm + offs[k] : pcm, lens[k], F, ws.S, kSnLd, gmax, st,
-                                fused ? colmed : nullptr);
+        int rc = sn_launch_stft(*p, lens[k] ? pcm + offs[k] : pcm, lens[k], F, ws.S, kSnLd, gmax, st);
         if (rc != AA_OK) return rc;
-        if (!fused) {
-            hipEvent_t e1;
-            if ((rc = p->timer.begin(SN_STAGE_COLMED, st, &e1)) != AA_OK) return rc;
-            if (p->colmed_bs)
-                hipLaunchKernelGGL(sn_colmed<true>, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
-            else
-                hipLaunchKernelGGL(sn_colmed<false>, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
-            AA_LAUNCH_CHECK();
-            if ((rc = p->timer.end(SN_STAGE_COLMED, st, e1)) != AA_OK) return rc;
-        }
+        hipEvent_t e1;
+        if ((rc = p->timer.begin(SN_STAGE_COLMED, st, &e1)) != AA_OK) return rc;
+        hipLaunchKernelGGL(sn_colmed, dim3((F + 3) / 4), dim3(256), 0, st, ws.S, kSnLd, F, colmed);
+        AA_LAUNCH_CHECK();
+        if ((rc = p->timer.end(SN_STAGE_COLMED, st, e1)) != AA_OK) return rc;
         const int words = (F + 63) / 64, ldt = words * 64;
         hipEvent_t e0;
         if ((rc = p->timer.begin(SN_STAGE_TRANSPOSE, st, &e0)) != AA_OK) return rc;
@@ -1669,11 +1262,8 @@ static int sn_run_impl(SnPlan* p, const float* pcm, const int64_t* offs, const i
         AA_LAUNCH_CHECK();
         if ((rc = p->timer.end(SN_STAGE_TRANSPOSE, st, e0)) != AA_OK) return rc;
         if ((rc = p->timer.begin(SN_STAGE_SELECT, st, &e0)) != AA_OK) return rc;
-        if (!p->select_reg && F <= kRowT * kRowPer)
+        if (F <= kRowT * kRowPer)
             hipLaunchKernelGGL(sn_select_row, dim3(kSnBins), dim3(kRowT), 0, st, ws.ST, ldt, F, gmax, c3, words, M0);
-        else if (p->select_reg && F <= kSelT * kSelPer)
-            hipLaunchKernelGGL(sn_select_reg, dim3(kSnBins), dim3(kSelT), 0, st, ws.ST, ldt, F, gmax, c3, words, M0,
-                               p->diag);
         else if (F <= kSnStageMax)
             hipLaunchKernelGGL(sn_select<true>, dim3(kSnBins), dim3(256), sizeof(unsigned) * F, st, ws.ST, ldt, F, gmax,
                                c3, words, M0);
@@ -1730,21 +1320,13 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
         delete p;
         return rc;
     }
-    if (const char* e = std::getenv("AA_SN_SELECT")) p->select_reg = std::strcmp(e, "reg") == 0;
-    if (const char* e = std::getenv("AA_SN_DIAG")) p->diag = std::atoi(e);
-    if (const char* e = std::getenv("AA_SN_STFT")) p->stft_r8 = std::strcmp(e, "r8") == 0;
     if (const char* e = std::getenv("AA_SN_TW")) p->tw_chain = std::strcmp(e, "table") != 0;
-    if (const char* e = std::getenv("AA_SN_STFT_BLOCKS")) p->stft_blocks = std::max(8, std::atoi(e));
-    if (const char* e = std::getenv("AA_SN_COLMED")) {
-        p->colmed_bs = std::strcmp(e, "bs") == 0;
-        p->colmed_fused = std::strcmp(e, "fused") == 0;
-    }
     // sn_stft64's tables, rounded from long double
     auto wexp = [](long long e, long long m) {  // exp(-2 pi i e / m)
         const long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)(e % m) / (long double)m;
         return make_double2((double)cosl(a), (double)sinl(a));
     };
-    std::vector<double2> tab(kR8TabN);
+    std::vector<double2> tab(kS64TabN);
     {  // scipy.signal.get_window('hann', 4096, fftbins=True) (librosa 0.11's window, :654): general_cosine
        // over np.linspace(-pi, pi, 4097)[:4096], w = 0.5 + 0.5 cos(fac) in float64
         const double start = -M_PI, step = (M_PI - start) / 4096.0;
@@ -1761,12 +1343,6 @@ extern "C" int aa_sn_create(const aa_sn_config* cfg, void** plan) {
     for (int n3 = 1; n3 < 8; ++n3)
         for (int t = 0; t < kS64T; ++t) tab[kS64TabTw3 + (n3 - 1) * kS64T + t] = wexp((long long)n3 * t, 2048);
     for (int t = 0; t < kS64T; ++t) tab[kS64TabTwS + t] = wexp(t ? t : 128, 4096);
-    for (int k = 1; k < 8; ++k) {  // sn_stft64r8
-        for (int m = 0; m < 256; ++m) tab[kR8Tw1 + (k - 1) * 256 + m] = wexp((long long)m * k, 2048);
-        for (int r = 0; r < 32; ++r) tab[kR8Tw2 + (k - 1) * 32 + r] = wexp((long long)r * k, 256);
-        for (int d = 0; d < 4; ++d) tab[kR8Tw3 + (k - 1) * 4 + d] = wexp((long long)d * k, 32);
-    }
-    for (int t = 0; t < 256; ++t) tab[kR8TwS + t] = wexp(t, 4096);
     hipError_t e = hipMalloc((void**)&p->d_tab, sizeof(double2) * tab.size());
     if (e == hipSuccess) e = hipMemcpy(p->d_tab, tab.data(), sizeof(double2) * tab.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {

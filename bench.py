@@ -645,6 +645,14 @@ def main_step(args, world, rank, dev, emit=True):
                 "traffic_source": traffic_src,
                 "stages_ms": {c["name"]: round(c["avg_ms"], 4) for c in calib},
                 "stages_sum_ms": round(sum(c["avg_ms"] for c in calib), 4)}
+    # an in-run anchor: an HBM-streaming kernel whose code has not changed
+    # since round 3 (fe_stats), timed in the same calibration pass, so a kernel
+    # time compared across rounds (boxes differ by ~5 %) can be read as a ratio
+    anc = next((c for c in calib if c["name"] == "fe_stats"), None)
+    if anc is not None and anc["avg_ms"] > 0:
+        roofline["anchor"] = {"kernel": "fe_stats", "avg_ms": round(anc["avg_ms"], 5),
+                              "dominant_over_anchor": round(dom["avg_ms"] / anc["avg_ms"], 3),
+                              "step_over_anchor": round((elapsed / args.steps * 1e3) / anc["avg_ms"], 2)}
     # every stage against its own bound (the dominant one above): algorithmic
     # flops or bytes of the calibration pass / its event-timed average
     per = {}

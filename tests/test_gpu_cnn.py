@@ -68,26 +68,6 @@ def test_cnn_bf16x3_parity(gpu, model_root, name, T):
     assert np.abs(pr - rpr).max() <= LOGIT_TOL
 
 
-@pytest.mark.parametrize("T", [226, 513])
-def test_cnn_bf16x3_wgf_variant(gpu, model_root, T, monkeypatch, tmp_path):
-    """The opt-in fused first layer + F(6,3) Winograd pair (conv_wgf, AA_WGF=1,
-    read when the model is planned) holds the same gate, MagTransform's
-    prologue included."""
-    monkeypatch.setenv("AA_WGF", "1")
-    for name in ("model1", "model3", "mag"):
-        if name == "mag":
-            path = make_model(tmp_path / "magw", name="magmodel", seed=11, mag=2)
-            x = calibration_input(3, 160, T, False, np.random.default_rng(5))
-        else:
-            path = model_root / name / "audioModel.safetensors"
-            x = calibration_input(6, 160, T, True, np.random.default_rng(T + len(name)))
-        lg, _ = _run(path, x, "bf16x3")
-        rlg, _ = cnn_oracle.forward(path, x)
-        err = np.abs(lg - rlg).max()
-        print(f"{name} T={T} conv_wgf max|dlogit|={err:.3e}")
-        assert err <= LOGIT_TOL
-
-
 @pytest.mark.parametrize("T,n", [(226, 600), (513, 300)])
 def test_cnn_bf16x3_large_batch(gpu, model_root, T, n):
     """Batches above the old 2^31-byte launch limit (~473 windows at T = 226,

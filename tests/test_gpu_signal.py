@@ -86,18 +86,14 @@ def test_spectrogram_bit_exact(gpu, n, seed):
     _assert_s_equal(got, want)
 
 
-@pytest.mark.parametrize("variant", ["r8", "base", "table"])
+@pytest.mark.parametrize("variant", ["base", "table"])
 @pytest.mark.parametrize("n,seed", [(60 * SR, 35), (7 * SR + 999, 36), (5000, 37)])
 def test_spectrogram_variants_bit_exact(gpu, monkeypatch, variant, n, seed):
-    """Both STFT kernels (sn_stft64: 128 threads, 16 x 16 x 8; sn_stft64r8: 256
-    threads, 8 x 8 x 8 x 4; AA_SN_STFT picks one at plan creation), and
-    sn_stft64 with every twiddle from the tables instead of the default
-    W, W^2, W^4 ladders (AA_SN_TW=table), give the reference's magnitudes, and
-    the detector built on any of them gives its mask."""
+    """sn_stft64 with its default W, W^2, W^4 twiddle ladders and with every
+    twiddle from the tables (AA_SN_TW=table) gives the reference's
+    magnitudes, and the detector built on either gives its mask."""
     if variant == "table":
         monkeypatch.setenv("AA_SN_TW", "table")
-    else:
-        monkeypatch.setenv("AA_SN_STFT", variant)
     x = _clip(n / SR, seed)
     det = _det(gpu)
     got = det.spectrogram(torch.from_numpy(x).to(gpu)).cpu().numpy()
@@ -112,20 +108,39 @@ def test_spectrogram_variants_bit_exact(gpu, monkeypatch, variant, n, seed):
         assert stats.tolist() == ref_stats.tolist()
 
 
-@pytest.mark.parametrize("colmed", ["fused", "sep", "bs"])
-def test_column_median_variants(gpu, monkeypatch, colmed):
-    """Every column-median form -- radix select as its own launch (the
-    default), the same select inside the STFT kernel (AA_SN_COLMED=fused), the
-    bit-serial search (AA_SN_COLMED=bs) -- gives the oracle's mask."""
-    monkeypatch.setenv("AA_SN_COLMED", colmed)
-    x = _clip(60.0, 38)
-    det = _det(gpu)
-    F = det.n_frames(len(x))
-    mask_dev = torch.empty((2049, det.words(F)), dtype=torch.int64, device=gpu)
-    stats = det.components(torch.from_numpy(x).to(gpu), mask_out=mask_dev)
-    _, ref_mask, ref_stats = so.signal_noise(x, SR, HOP)
-    assert int((_unpack(mask_dev.cpu().numpy(), F) != ref_mask).sum()) == 0
-    assert stats.tolist() == ref_stats.tolist()
+def test_twiddle_chain_vs_table_over_many_clips(gpu, monkeypatch):
+    """the default chained twiddle powers (f64 products) against
+    the table values, over 24 seeded clips of 2-20 s (about 45,000 frames x
+    2,049 bins = 92 M magnitudes).  A product a few f64 ulps off a table value
+    moves an f32 magnitude only where the f64 magnitude sits on an f32
+    rounding tie: measured, 1 magnitude in 92 M differs (round 6,
+    profiles/r06/pytest_gpu.log).  The tolerance, as for any two f64 FFT
+    factorisations against numpy's pocketfft (_assert_s_equal): at most one
+    differing magnitude per recording, one f32 ulp apart, and wherever the two
+    differ the oracle's (numpy) value is one of them."""
+    from oracle.fe_oracle import stft_mag
+    rng = np.random.default_rng(77)
+    clips = [_clip(float(rng.uniform(2.0, 20.0)), 100 + i) for i in range(24)]
+    det_chain = _det(gpu)
+    chain = [det_chain.spectrogram(torch.from_numpy(x).to(gpu)).cpu().numpy() for x in clips]
+    monkeypatch.setenv("AA_SN_TW", "table")
+    det_table = _det(gpu)
+    total = 0
+    for x, c in zip(clips, chain):
+        t = det_table.spectrogram(torch.from_numpy(x).to(gpu)).cpu().numpy()
+        bad = c.view(np.uint32) != t.view(np.uint32)
+        n_bad = int(bad.sum())
+        total += n_bad
+        assert n_bad <= 1, n_bad
+        if n_bad:
+            ulp = np.abs(c.view(np.int32)[bad].astype(np.int64) - t.view(np.int32)[bad].astype(np.int64))
+            assert int(ulp.max()) == 1
+            ref = stft_mag(x, 4096, HOP)
+            assert bool(np.all((ref[bad] == c[bad]) | (ref[bad] == t[bad])))
+    print(f"chained vs table twiddles: {total} of {sum(c.size for c in chain)} magnitudes differ")
+    assert total <= 4
+
+
 
 
 def _assert_s_equal(got, want):

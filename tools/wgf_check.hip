@@ -4,6 +4,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include
 //   tools/wgf_check.hip audio-analysis_amd/csrc/aa_api.cpp -o tools/wgf_check ; run on the GPU box.
 #include "../audio-analysis_amd/csrc/aa_cnn.hip"
+#include "conv_wgf.h"  // the rejected fused Winograd pair (not in libaa.so)
 
 #include <cmath>
 #include <cstdio>
