@@ -20,9 +20,15 @@ ARCH = os.environ.get("AA_OFFLOAD_ARCH", "gfx950")
 # the wave-per-frame kernel past its 128-VGPR budget (spills)
 # the CNN kernels keep MFMA accumulators in VGPRs: no AGPR copies
 # (v_accvgpr_read) between the fused first layer's MFMAs and its activation
-# split (in-pipeline A/B: step +0.5 %)
+# split (in-pipeline A/B: step +0.5 %); and no SLP packing there either: the
+# fused first conv is bound by the SIMD's vector issue (VALU issue + the 8
+# cycles each MFMA holds it, profiles/r06/pmc_fused_first_conv.txt), and the
+# packed v_pk_add_f32 the vectoriser formed in the activation split costs
+# more issue than two scalar subtracts (fused conv 127 -> 120 us, step
+# 270.8k -> 275.4k audio-s/s, profiles/r06/ab_slp.txt)
 EXTRA_FLAGS = {"aa_frontend.hip": ["-fno-slp-vectorize"], "aa_signal.hip": ["-fno-slp-vectorize"],
-               "aa_cnn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "aa_graph.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+               "aa_cnn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"],
+               "aa_graph.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def hipcc() -> str:

@@ -163,6 +163,9 @@ __device__ __forceinline__ void leaky_split2(float x0, float x1, float a, uint32
     const float o0 = __builtin_amdgcn_fmed3f(x0, r0, inf);
     const float o1 = __builtin_amdgcn_fmed3f(x1, r1, inf);
     hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{o0, o1}, b2));
+    // (scalar subtracts: aa_cnn.hip is built with -fno-slp-vectorize, which
+    // keeps them from being packed into v_pk_add_f32 -- an expensive issue
+    // beside MFMAs: fused conv 127 -> 120 us, profiles/r06/ab_slp.txt)
     const float s0 = o0 - __uint_as_float(hi << 16);
     const float s1 = o1 - __uint_as_float(hi & 0xffff0000u);
     lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{s0, s1}, b2));

@@ -16,7 +16,8 @@ DOC = ROOT / "INTEGRATION.md"
 
 # header struct -> the Python class name used by _lib.py and INTEGRATION.md
 NAMES = {"aa_window": "Window", "aa_fe_config": "FeConfig", "aa_layer": "Layer",
-         "aa_sn_config": "SnConfig", "aa_sn_component": "SnComponent", "aa_flac_stream_info": "FlacInfo"}
+         "aa_sn_config": "SnConfig", "aa_sn_component": "SnComponent", "aa_flac_stream_info": "FlacInfo",
+         "aa_vorbis_stream_info": "VorbisInfo"}
 CTYPES = {"int32_t": C.c_int32, "int64_t": C.c_int64, "float": C.c_float, "double": C.c_double}
 
 
