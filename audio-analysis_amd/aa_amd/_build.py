@@ -28,7 +28,10 @@ ARCH = os.environ.get("AA_OFFLOAD_ARCH", "gfx950")
 # 270.8k -> 275.4k audio-s/s, profiles/r06/ab_slp.txt)
 EXTRA_FLAGS = {"aa_frontend.hip": ["-fno-slp-vectorize"], "aa_signal.hip": ["-fno-slp-vectorize"],
                "aa_cnn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"],
-               "aa_graph.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+               # same for the graph route: the split-bf16 1x1 / expand convs are
+               # VALU-issue-bound too (effnetv2 step 61.0k -> 62.5k audio-s/s,
+               # profiles/r06/ab_graph_noslp.txt)
+               "aa_graph.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"]}
 
 
 def hipcc() -> str:
