@@ -54,14 +54,17 @@ def gather_documents(local: dict, device=None, group=None) -> dict:
     return dict(sorted(out.items()))
 
 
-# host lanes (threads, each with its own HIP streams) of the batched path: 5
-# with 8 hardware queues measured 138k audio-s/s against 131k (4) and 117k
-# (3) on one box, three rounds each (profiles/r05/corpus_lanes.txt).  That was
-# measured with GPU_MAX_HW_QUEUES=8 (corpus.main and bench.py set it); with
-# HIP's default 4 queues the lanes' compute + copy streams would share queues,
-# so a library user who did not raise it keeps the 3 lanes measured there.
-DEFAULT_LANES = 5
-DEFAULT_LANES_4Q = 3
+# host lanes (threads, each with its own compute + copy HIP streams) of the
+# batched path, by the process's hardware queues: a lane needs two queues of
+# its own, or its streams share a queue with another lane's and run back to
+# back.  Measured on one box each, two or three rounds (configs[3] secondary,
+# audio-s/s): 4 queues / 3 lanes 114-124k; 8 / 5 114-149k; 8 / 6 130-131k;
+# 16 / 8 131-149k; 24 / 12 132-148k; 32 / 16 107-131k (the host threads then
+# contend for the GIL) -- profiles/r05/corpus_lanes.txt,
+# profiles/r06/corpus_queues_lanes.txt.  corpus.main and bench.py raise
+# GPU_MAX_HW_QUEUES to 16 before the first GPU call; a library user who did
+# not keeps the lanes measured for HIP's default 4.
+LANES_BY_QUEUES = ((16, 8), (8, 5), (0, 3))
 
 
 def default_lanes() -> int:
@@ -74,7 +77,18 @@ def default_lanes() -> int:
         queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     except ValueError:
         queues = 4
-    return DEFAULT_LANES if queues >= 8 else DEFAULT_LANES_4Q
+    return next(lanes for q, lanes in LANES_BY_QUEUES if queues >= q)
+
+
+def raise_hw_queues(n: int = 16):
+    """GPU_MAX_HW_QUEUES to at least n (HIP reads it once, at initialisation:
+    call before the process's first GPU call)."""
+    try:
+        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)
+    except ValueError:
+        cur = 0
+    if cur < n:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(n)
 
 
 def run(files, bird_models, analyse_tracks=False, examine_fn=None, rank=0, world=1, device=None, batch=16):
@@ -199,7 +213,7 @@ def main(argv=None):
     # hardware queues for the batch lanes' compute + copy streams (HIP's
     # default 4 puts some of them on one queue; read once, before the first
     # GPU call of the process: bench.py does the same)
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    raise_hw_queues()
     args = parse_args(argv)
     init_logging()
     if "WORLD_SIZE" in os.environ:

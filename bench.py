@@ -37,11 +37,14 @@ import time
 from pathlib import Path
 
 # hardware queues per process: HIP maps streams onto them round-robin, and two
-# streams on one queue run back to back.  The corpus path keeps 3 lanes x
-# (compute + copy) streams busy beside the headline's two lanes; HIP's default
-# of 4 queues made some of them share (configs[3] line 108.5k -> 121.1k with 8,
-# same box; profiles/r05/hw_queues.txt).  Read once, at HIP's initialisation.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# streams on one queue run back to back.  The corpus path keeps 8 lanes x
+# (compute + copy) streams busy; HIP's default of 4 queues makes them share
+# (configs[3] secondary 114-121k with 4 queues / 3 lanes, 130-149k with 16 /
+# 8, same box; profiles/r06/corpus_queues_lanes.txt).  Raised, never lowered
+# (a value above 16 that the environment set stays), and read once, at HIP's
+# initialisation: before anything below touches the GPU.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = Path(__file__).resolve().parent
 for p in (str(ROOT), str(ROOT / "audio-analysis_amd")):
