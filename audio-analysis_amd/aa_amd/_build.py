@@ -45,7 +45,8 @@ def _stale() -> bool:
     if not LIB.exists():
         return True
     t = LIB.stat().st_mtime
-    deps = [CSRC / s for s in SOURCES] + list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
+    # this file too: a change of the per-source flags rebuilds
+    deps = [CSRC / s for s in SOURCES] + list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h")) + [Path(__file__)]
     return any(p.stat().st_mtime > t for p in deps)
 
 
