@@ -121,3 +121,23 @@ def test_corpus_gpu_two_ranks_match_one(gpu, model_root, tmp_path):
     assert "species_identify" in single
     outs = _spawn(_gpu_worker, 2, files, models)
     assert outs[0] == single and outs[1] == single
+
+
+def test_lanes_follow_hardware_queues(monkeypatch):
+    """Batch lanes by GPU_MAX_HW_QUEUES (two queues per lane: compute + copy
+    streams), AA_BATCH_LANES overriding; raise_hw_queues only ever raises."""
+    from aa_amd import corpus
+    monkeypatch.delenv("AA_BATCH_LANES", raising=False)
+    for q, lanes in (("4", 3), ("7", 3), ("8", 5), ("12", 5), ("16", 8), ("32", 8), ("junk", 3)):
+        monkeypatch.setenv("GPU_MAX_HW_QUEUES", q)
+        assert corpus.default_lanes() == lanes, q
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES")
+    assert corpus.default_lanes() == 3  # HIP's default 4
+    monkeypatch.setenv("AA_BATCH_LANES", "6")
+    assert corpus.default_lanes() == 6
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    corpus.raise_hw_queues()
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "16"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "24")
+    corpus.raise_hw_queues()
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "24"
