@@ -444,16 +444,31 @@ __global__ __launch_bounds__(NFFT / 16) void fe_stft_mel(
 // band slots of the wave-per-frame kernel's CSR image: whole rounds of 64 lanes
 __host__ __device__ constexpr int fe_mel_slots(int n_mels) { return (n_mels + 63) / 64 * 64; }
 
-#ifndef AA_FE_ORDER
-#define AA_FE_ORDER 1  // frame -> wave order: 0 block-major (round 2), 1 per-XCD wave-major
-#endif
 #ifndef AA_FE_WPB
 #define AA_FE_WPB 8
+#endif
+#ifndef AA_FE_MEL_G
+#define AA_FE_MEL_G 2  // mel rows: float4 groups whose loads are issued together (0: one per loop trip)
+#endif
+#ifndef AA_FE_MEL_P
+#define AA_FE_MEL_P 1  // mel rows: slots (rounds of 64) whose first groups load together
 #endif
 constexpr int kWpb = AA_FE_WPB;         // waves per block (2 blocks per CU)
 
 // DIAG (tools/fe_bench.hip only): 1 skip the PCM loads, 4 the FFT (steps 1-5),
 // 8 the real split, 16 Hann and power, 32 the mel rows, 64 the output stores.
+// DIAG & 128 (tools/fe_bench.hip): per-wave s_memtime totals of the frame's
+// phases into fe_stamps[global wave][phase][lane] (every lane stores: vector
+// stores only) -- 0 loads + Hann, 1 DFT-32 #1, 2 twiddles, 3 transpose,
+// 4 DFT-32 #2, 5 radix-2, 6 split + power, 7 mel rows
+constexpr int kFeStampPh = 8;
+__device__ unsigned long long* fe_stamps = nullptr;
+#define FE_STAMP(k)                                                              \
+    if constexpr ((DIAG & 128) != 0) {                                           \
+        const unsigned long long tn = __builtin_amdgcn_s_memtime();              \
+        st_acc[k] += tn - st_prev;                                               \
+        st_prev = tn;                                                            \
+    }
 template <int PM, int DIAG = 0>
 __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb / 2, kWpb / 2))) void fe_stft_mel_4096(
     const float* __restrict__ pcm, const aa_window* __restrict__ wins, const float4* __restrict__ stats,
@@ -480,13 +495,41 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
     const float2 te = tw4096[2 * lane], to = tw4096[2 * lane + 1];
     const float2 hwe = make_float2(te.x, -te.y), hwo = make_float2(to.x, -to.y);
     __syncthreads();                     // vmcnt(0): the CSR image has landed
+    unsigned long long st_acc[kFeStampPh] = {}, st_prev = 0;
+    // the PCM samples of frame fl into yy (step 0): lane c gets z[c + 64 r]
+    auto load_frame = [&](int fl, float2 (&yy)[32]) {
+        const int wl = fl / T;
+        const aa_window dl = wins[wl];
+        const int i0l = (fl - wl * T) * hop - 2048;
+        // per-lane sample index, opaque to the optimiser: otherwise it hoists the
+        // 64 loop-invariant load offsets and edge masks out of the frame loop
+        // and spills them
+        int l2l = 2 * lane;
+        __asm__ volatile("" : "+v"(l2l));
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(pcm + dl.src), 0, dl.n_valid * 4, 0x00020000);
+        // even and odd samples through two address registers: the backend
+        // must not fuse a pair into one 8-byte load, whose range check would
+        // not zero the two samples independently
+        const int offe = i0l - dl.pad_left + l2l;
+        const int v0 = i0l - dl.pad_left;  // the frame's first sample in the view
+        if (v0 >= 0 && v0 + 4096 <= dl.n_valid) {
+            // frame inside the view (wave-uniform): no sample is range checked,
+            // so a lane's pair comes in one 8-byte load (32 fully used 512-B
+            // wave-instructions instead of 64 half-used)
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                const uint2 v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, (offe + 128 * r) * 4, 0, 0));
+                yy[r] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+            }
+        } else {
+            int offo = offe + 1;
+            __asm__ volatile("" : "+v"(offo));
+#pragma unroll
+            for (int r = 0; r < 32; ++r) yy[r] = make_float2(load_view(rs, offe + 128 * r), load_view(rs, offo + 128 * r));
+        }
+    };
 
-#if AA_FE_ORDER == 0
-    const int nb = gridDim.x;  // a multiple of 8 (host)
-    const int blk = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
-    const int G = nb * kWpb;
-    for (int fi = blk * kWpb + wave; fi < n_frames; fi += G) {
-#else
     // XCD x (block b runs on XCD b % 8) owns frames [x n / 8, (x + 1) n / 8);
     // its waves take them round-robin, wave-major over its blocks, so the last,
     // partial round is spread over every XCD, CU and SIMD (a block's waves w
@@ -495,11 +538,11 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
     const int xcd = blockIdx.x & 7;
     const int f_end = (int)((long long)(xcd + 1) * n_frames / 8);
     const int G = nbx * kWpb;
-    for (int fi = (int)((long long)xcd * n_frames / 8) + wave * nbx + (blockIdx.x >> 3); fi < f_end; fi += G) {
-#endif
+    const int f_first = (int)((long long)xcd * n_frames / 8) + wave * nbx + (blockIdx.x >> 3);
+    for (int fi = f_first; fi < f_end; fi += G) {
         const int w = fi / T;
         const int t = fi - w * T;
-        const aa_window d = wins[w];
+        if constexpr ((DIAG & 128) != 0) st_prev = __builtin_amdgcn_s_memtime();
         float apow = 1.f, beta = 0.f;
         if (normalize) {
             float lo = INFINITY, hi = -INFINITY;
@@ -530,28 +573,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
 #pragma unroll
                 for (int r = 0; r < 32; ++r) y[r] = make_float2((float)(lane + r), (float)(t - r));
             } else {
-                const __amdgpu_buffer_rsrc_t rs =
-                    __builtin_amdgcn_make_buffer_rsrc((void*)(pcm + d.src), 0, d.n_valid * 4, 0x00020000);
-                // even and odd samples through two address registers: the
-                // backend must not fuse a pair into one 8-byte load, whose range
-                // check would not zero the two samples independently
-                const int offe = i0 - d.pad_left + l2;
-                const int v0 = i0 - d.pad_left;  // the frame's first sample in the view
-                if (v0 >= 0 && v0 + 4096 <= d.n_valid) {
-                    // frame inside the view (wave-uniform): no sample is range
-                    // checked, so a lane's pair comes in one 8-byte load (32
-                    // fully used 512-B wave-instructions instead of 64 half-used)
-#pragma unroll
-                    for (int r = 0; r < 32; ++r) {
-                        const uint2 v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, (offe + 128 * r) * 4, 0, 0));
-                        y[r] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
-                    }
-                } else {
-                    int offo = offe + 1;
-                    __asm__ volatile("" : "+v"(offo));
-#pragma unroll
-                    for (int r = 0; r < 32; ++r) y[r] = make_float2(load_view(rs, offe + 128 * r), load_view(rs, offo + 128 * r));
-                }
+                load_frame(fi, y);
             }
             if (normalize && (i0 < 0 || i0 + 4096 > win_len)) {  // edge frame: + beta, centre padding 0
 #pragma unroll
@@ -578,6 +600,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
                 y[r].x *= fmaf(-a, ce, a);
                 y[r].y *= fmaf(-a, co, a);
             }
+            FE_STAMP(0)
             if constexpr ((DIAG & 4) != 0) {
 #pragma unroll
                 for (int j = 0; j < 32; ++j) u[j] = y[j];
@@ -602,6 +625,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
                 // ---- 1. DFT-32 over r ----
                 // (the (-1)^r of the upper half rides on its Hann weights, above)
                 dft32(y);
+                FE_STAMP(1)
                 // ---- 2. twiddle W2048^(c row) = (W^8c)^(row/8) (W^c)^(row%8),
                 // row = k (+16 mod 32 in the upper half); ladders rebuilt per frame
                 // (<= 4 roundings per twiddle; not kept live across the loop) ----
@@ -624,6 +648,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
                     const float2 tk = (k & 7) == 0 ? p8[k >> 3] : cmul(p8[k >> 3], p1[k & 7]);
                     y[dperm(k)] = cmul(y[dperm(k)], tk);
                 }
+                FE_STAMP(2)
                 // ---- 3. transpose in two passes: pass p moves registers
                 // 16p..16p+15 (rows (16p + 16 [c >= 32]) % 32 + 0..15 of column
                 // c) and lane (k1, h) takes columns h + 2m, m in the 16-range
@@ -638,11 +663,13 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
                     for (int i = 0; i < 16; ++i) u[16 * pass + i] = src[2 * i];
                     wave_sync();
                 }
+                FE_STAMP(3)
                 // ---- 4. DFT-32 over m (input rotated by 16 in the upper half:
                 // output k times (-1)^k) ----
                 dft32(u);
 #pragma unroll
                 for (int k = 1; k < 32; k += 2) u[dperm(k)] = flip(u[dperm(k)]);
+                FE_STAMP(4)
                 // ---- 5. radix-2 across the lane pair: lane h = 1 sends
                 // W64^j E1, lane h = 0 sends E0; then Z = E0 + W E1 (h = 0) and
                 // E0 - W E1 (h = 1) are recv +- own ----
@@ -655,6 +682,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
                     const float2 rv = make_float2(swap_pair(g.x), swap_pair(g.y));
                     u[dperm(j)] = make_float2(fmaf(sg, g.x, rv.x), fmaf(sg, g.y, rv.y));
                 }
+                FE_STAMP(5)
             }
         }
         // lane holds Z[k1 + 32 (32 h + j)] in u[dperm(j)]
@@ -711,17 +739,82 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
             }
         }
         wave_sync();
+        FE_STAMP(6)
         // ---- 8. mel rows ----
         // rows of the CSR image are zero-padded to whole float4s (value
         // offsets 16-B aligned); the padding adds exact zeros
         float fmx = 0.f;
         float* orow = melF + (size_t)fi * n_mels;  // fi = w T + t
         const int nslot = fe_mel_slots(n_mels);
-        for (int si = lane; si < ((DIAG & 32) ? 0 : nslot); si += 64) {
-            // slot si holds band rw.w (-1: empty, length 0) covering bins
-            // [x, x + L): its values are stored reversed and front-padded to
-            // L4 = roundup(L, 4) (fe_cimg4096), so with P reversed the row is
-            // an ascending run pv[0 .. L4)
+#if AA_FE_MEL_G > 0
+        // the slot index opaque per frame: the rows' descriptors and value
+        // addresses are frame-invariant, and hoisted out of the frame loop they
+        // would stay live through the FFT (spills)
+        int si0 = lane;
+        __asm__ volatile("" : "+v"(si0));
+#else
+        const int si0 = lane;
+#endif
+        // slot si holds band rw.w (-1: empty, length 0) covering bins [x, x +
+        // L): its values are stored reversed and front-padded to L4 = roundup(L,
+        // 4) (fe_cimg4096), so with P reversed the row is an ascending run
+        // pv[0 .. L4)
+#if AA_FE_MEL_G > 0
+        // P slots per trip, the first G float4 groups of each: every load issued
+        // before the first FMA (one LDS round trip for P x G groups instead of
+        // one per group), then each row's FMA chain in the order of the plain
+        // loop (identical sums; fe_bench's hash, profiles/r06/fe_mel_groups.txt)
+        constexpr int G = AA_FE_MEL_G, NP = AA_FE_MEL_P;
+        for (int si = si0; si < ((DIAG & 32) ? 0 : nslot); si += 64 * NP) {
+            int4 rw[NP];
+            const float4* wv[NP];
+            const float* pv[NP];
+            float4 wa[NP][G];
+            float pa[NP][G][4];
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const int sq = si + 64 * q;
+                // a slot past the last round is an empty row (its loads stay
+                // inside the wave's power buffer, as fe_cimg4096's empty slots)
+                rw[q] = sq < nslot ? srows[sq] : make_int4(kmin + 3, 0, 0, -1);
+                wv[q] = reinterpret_cast<const float4*>(svals + rw[q].z);
+                pv[q] = Pt - rw[q].x - (rw[q].y - 1);  // bins x + L4 - 1 down to x
+                // (groups past the row re-read its last group: in range, unused)
+                const int glast = max((rw[q].y >> 2) - 1, 0);
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int gi = min(g, glast);
+                    wa[q][g] = wv[q][gi];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) pa[q][g][e] = pv[q][4 * gi + e];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                float s = 0.f;
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    if (4 * g < rw[q].y) {
+                        s = fmaf(wa[q][g].x, pa[q][g][0], s);
+                        s = fmaf(wa[q][g].y, pa[q][g][1], s);
+                        s = fmaf(wa[q][g].z, pa[q][g][2], s);
+                        s = fmaf(wa[q][g].w, pa[q][g][3], s);
+                    }
+                }
+                for (int i = 4 * G; i < rw[q].y; i += 4) {
+                    const float4 a = wv[q][i >> 2];
+                    s = fmaf(a.x, pv[q][i], s);
+                    s = fmaf(a.y, pv[q][i + 1], s);
+                    s = fmaf(a.z, pv[q][i + 2], s);
+                    s = fmaf(a.w, pv[q][i + 3], s);
+                }
+                s *= apow;
+                if (!(DIAG & 64) && rw[q].w >= 0) orow[rw[q].w] = s;
+                fmx = fmaxf(fmx, s);
+            }
+        }
+#else
+        for (int si = si0; si < ((DIAG & 32) ? 0 : nslot); si += 64) {
             const int4 rw = srows[si];
             const float4* wv = reinterpret_cast<const float4*>(svals + rw.z);
             const float* pv = Pt - rw.x - (rw.y - 1);  // bins x + L4 - 1 down to x
@@ -737,9 +830,16 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kWpb 
             if (!(DIAG & 64) && rw.w >= 0) orow[rw.w] = s;
             fmx = fmaxf(fmx, s);
         }
+#endif
         fmx = wave_max(fmx);
         if (lane == 0 && !(DIAG & 64)) pmax[fi] = fmx;
         wave_sync();  // the buffer is rewritten by the next frame
+        FE_STAMP(7)
+    }
+    if constexpr ((DIAG & 128) != 0) {
+        const size_t gw = (size_t)blockIdx.x * kWpb + wave;
+#pragma unroll
+        for (int k = 0; k < kFeStampPh; ++k) fe_stamps[(gw * kFeStampPh + k) * 64 + lane] = st_acc[k];
     }
 }
 
@@ -1010,7 +1110,9 @@ extern "C" int aa_fe_create(const aa_fe_config* cfg, const float* melfb, void** 
         // stay close (round-robin rows gave lane 31 the 3 widest-spaced rows:
         // 52 bins against a mean of 32).  Empty slots have length 0.
         const int nslot = fe_mel_slots(cfg->n_mels);
-        std::vector<int4> prow(nslot, make_int4(0, 0, 0, -1));
+        // (an empty slot's first bin: kmin + 3, so that the grouped loads of an
+        // empty row, AA_FE_MEL_G, read inside the wave's power buffer)
+        std::vector<int4> prow(nslot, make_int4(kmin + 3, 0, 0, -1));
         std::vector<float> pval;
         std::vector<int> order(rows.size());
         for (size_t m = 0; m < rows.size(); ++m) order[m] = (int)m;
