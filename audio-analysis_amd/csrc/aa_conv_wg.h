@@ -129,6 +129,74 @@ constexpr size_t wg_lds_bytes() {
 // distinct 16-B slots across a store's 8 lanes when WO >> PSH is odd
 constexpr int wg_psh(int wo) { return wo == 4 ? 2 : wo == 3 ? 0 : 1; }
 
+// Stage (group g, planes e0 .. e0 + PPS - 1) of the transformed patch: per
+// (group-pixel v, channel quad cq) the A input columns WO jp .. WO jp + A - 1,
+// transformed (u = B^T d, f32), split into bf16 hi / lo, into the planes
+// (128 B per group-pixel, aa_conv_x3.h's rotation swizzle on v)
+template <int WO, int PPS, int E0, int NP, int PV, int NTHR, int ITEMS, typename Load4>
+__device__ __forceinline__ void wg_stage(char* patch, int oh0, int ow0, int Hin, int Win, int g, Load4&& load4) {
+    constexpr int A = WO + 2;
+    for (int idx = threadIdx.x; idx < ITEMS; idx += NTHR) {
+        const int v = idx >> 3, cq = idx & 7;
+        const int R = v / NP, jp = v - (v / NP) * NP;
+        const int gh = min(oh0 + R, Hin - 1);
+        float4 d[A];
+#pragma unroll
+        for (int c = 0; c < A; ++c) d[c] = load4(gh, min(ow0 + WO * jp + c, Win - 1), g, cq);
+        const int unit = (((cq >> 1) + v) & 7) << 4;
+        // F(6, 3): the factored input transform (shared partial sums,
+        // 26 operations per channel instead of the 44 non-zeros of B^T)
+        float4 u6[WO == 6 ? 8 : 1];
+        if constexpr (WO == 6) {
+            auto f = [&](auto get, auto put) {
+                const float d0 = get(d[0]), d1 = get(d[1]), d2 = get(d[2]), d3 = get(d[3]);
+                const float d4 = get(d[4]), d5 = get(d[5]), d6 = get(d[6]), d7 = get(d[7]);
+                put(0, fmaf(5.25f, d2 - d4, d6 - d0));
+                put(7, fmaf(5.25f, d3 - d5, d7 - d1));
+                const float a12 = fmaf(-4.25f, d4, d2 + d6), b12 = fmaf(-4.25f, d3, d1 + d5);
+                put(1, a12 + b12);
+                put(2, a12 - b12);
+                const float a34 = fmaf(-1.25f, d4, fmaf(0.25f, d2, d6));
+                const float b34 = fmaf(2.f, d5, fmaf(-2.5f, d3, 0.5f * d1));
+                put(3, a34 + b34);
+                put(4, a34 - b34);
+                const float a56 = fmaf(-5.f, d4, fmaf(4.f, d2, d6));
+                const float b56 = fmaf(0.5f, d5, fmaf(-2.5f, d3, 2.f * d1));
+                put(5, a56 + b56);
+                put(6, a56 - b56);
+            };
+            f([](const float4& x) { return x.x; }, [&](int e, float y) { u6[e].x = y; });
+            f([](const float4& x) { return x.y; }, [&](int e, float y) { u6[e].y = y; });
+            f([](const float4& x) { return x.z; }, [&](int e, float y) { u6[e].z = y; });
+            f([](const float4& x) { return x.w; }, [&](int e, float y) { u6[e].w = y; });
+        }
+#pragma unroll
+        for (int el = 0; el < PPS; ++el) {
+            float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (WO == 6) u = u6[E0 + el];
+#pragma unroll
+            for (int t = 0; t < (WO == 6 ? 0 : A); ++t) {
+                const float b = wg_bt(WO, E0 + el, t);
+                if (b == 0.f) continue;
+                if (b == 1.f) {
+                    u.x += d[t].x; u.y += d[t].y; u.z += d[t].z; u.w += d[t].w;
+                } else if (b == -1.f) {
+                    u.x -= d[t].x; u.y -= d[t].y; u.z -= d[t].z; u.w -= d[t].w;
+                } else {
+                    u.x = fmaf(b, d[t].x, u.x); u.y = fmaf(b, d[t].y, u.y);
+                    u.z = fmaf(b, d[t].z, u.z); u.w = fmaf(b, d[t].w, u.w);
+                }
+            }
+            uint32_t h0, l0, h1, l1;
+            split2(u.x, u.y, h0, l0);
+            split2(u.z, u.w, h1, l1);
+            const int a = (el * PV + v) * 128 + unit + (cq & 1) * 8;
+            *reinterpret_cast<uint2*>(patch + a) = make_uint2(h0, h1);
+            *reinterpret_cast<uint2*>(patch + (a ^ 64)) = make_uint2(l0, l1);
+        }
+    }
+}
+
 // DIAG (tools/conv_bench_x3.hip only): bit 0 skips the staging, bit 1 the MFMA steps
 template <int KH, int CIN, int WM, int WN, int MF, int NF, int POOL, int TH, int TW, int OCC = 0,
           bool IN_SPLIT = false, bool OUT_SPLIT = false, int DIAG = 0, int WO = 2, int NPASS = 1, int BD = 2>
@@ -266,70 +334,8 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
         wg_static_for<0, NPASS>([&](auto pc) {
             constexpr int pass = decltype(pc)::value;
             if (g > 0 || pass > 0) __syncthreads();  // every wave is done with the previous planes
-            // ---- stage (group g, pass): per (group-pixel v, channel quad cq) the
-            // A input columns WO jp .. WO jp + A - 1, transformed, split, into
-            // the pass's planes ----
-            constexpr int ITEMS = (DIAG & 1) ? 0 : PV * 8;
-            for (int idx = threadIdx.x; idx < ITEMS; idx += NTHR) {
-                const int v = idx >> 3, cq = idx & 7;
-                const int R = v / NP, jp = v - (v / NP) * NP;
-                const int gh = min(oh0 + R, Hin - 1);
-                float4 d[A];
-#pragma unroll
-                for (int c = 0; c < A; ++c) d[c] = load4(gh, min(ow0 + WO * jp + c, Win - 1), g, cq);
-                const int unit = (((cq >> 1) + v) & 7) << 4;
-                // F(6, 3): the factored input transform (shared partial sums,
-                // 26 operations per channel instead of the 44 non-zeros of B^T)
-                float4 u6[WO == 6 ? 8 : 1];
-                if constexpr (WO == 6) {
-                    auto f = [&](auto get, auto put) {
-                        const float d0 = get(d[0]), d1 = get(d[1]), d2 = get(d[2]), d3 = get(d[3]);
-                        const float d4 = get(d[4]), d5 = get(d[5]), d6 = get(d[6]), d7 = get(d[7]);
-                        put(0, fmaf(5.25f, d2 - d4, d6 - d0));
-                        put(7, fmaf(5.25f, d3 - d5, d7 - d1));
-                        const float a12 = fmaf(-4.25f, d4, d2 + d6), b12 = fmaf(-4.25f, d3, d1 + d5);
-                        put(1, a12 + b12);
-                        put(2, a12 - b12);
-                        const float a34 = fmaf(-1.25f, d4, fmaf(0.25f, d2, d6));
-                        const float b34 = fmaf(2.f, d5, fmaf(-2.5f, d3, 0.5f * d1));
-                        put(3, a34 + b34);
-                        put(4, a34 - b34);
-                        const float a56 = fmaf(-5.f, d4, fmaf(4.f, d2, d6));
-                        const float b56 = fmaf(0.5f, d5, fmaf(-2.5f, d3, 2.f * d1));
-                        put(5, a56 + b56);
-                        put(6, a56 - b56);
-                    };
-                    f([](const float4& x) { return x.x; }, [&](int e, float y) { u6[e].x = y; });
-                    f([](const float4& x) { return x.y; }, [&](int e, float y) { u6[e].y = y; });
-                    f([](const float4& x) { return x.z; }, [&](int e, float y) { u6[e].z = y; });
-                    f([](const float4& x) { return x.w; }, [&](int e, float y) { u6[e].w = y; });
-                }
-#pragma unroll
-                for (int el = 0; el < PPS; ++el) {
-                    constexpr int e0 = pass * PPS;
-                    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if constexpr (WO == 6) u = u6[e0 + el];
-#pragma unroll
-                    for (int t = 0; t < (WO == 6 ? 0 : A); ++t) {
-                        const float b = wg_bt(WO, e0 + el, t);
-                        if (b == 0.f) continue;
-                        if (b == 1.f) {
-                            u.x += d[t].x; u.y += d[t].y; u.z += d[t].z; u.w += d[t].w;
-                        } else if (b == -1.f) {
-                            u.x -= d[t].x; u.y -= d[t].y; u.z -= d[t].z; u.w -= d[t].w;
-                        } else {
-                            u.x = fmaf(b, d[t].x, u.x); u.y = fmaf(b, d[t].y, u.y);
-                            u.z = fmaf(b, d[t].z, u.z); u.w = fmaf(b, d[t].w, u.w);
-                        }
-                    }
-                    uint32_t h0, l0, h1, l1;
-                    split2(u.x, u.y, h0, l0);
-                    split2(u.z, u.w, h1, l1);
-                    const int a = (el * PV + v) * 128 + unit + (cq & 1) * 8;
-                    *reinterpret_cast<uint2*>(patch + a) = make_uint2(h0, h1);
-                    *reinterpret_cast<uint2*>(patch + (a ^ 64)) = make_uint2(l0, l1);
-                }
-            }
+            // ---- stage (group g, pass) ----
+            wg_stage<WO, PPS, pass * PPS, NP, PV, NTHR, (DIAG & 1) ? 0 : PV * 8>(patch, oh0, ow0, Hin, Win, g, load4);
             __syncthreads();
             if constexpr (AA_WG_PRIO > 0) __builtin_amdgcn_s_setprio(AA_WG_PRIO);  // (A/B knob, as AA_X3_PRIO)
             if constexpr ((DIAG & 2) == 0) {

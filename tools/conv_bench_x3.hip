@@ -3,6 +3,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include
 //   tools/conv_bench_x3.hip audio-analysis_amd/csrc/aa_api.cpp -o tools/conv_bench_x3 ; run on the GPU box.
 #include "../audio-analysis_amd/csrc/aa_cnn.hip"
+#include "conv_wgp.h"  // the rejected plane-split Winograd conv (profiles/r06/wgp_rejected.txt)
 
 #include <cstdio>
 #include <cstdlib>
@@ -176,6 +177,81 @@ int main(int argc, char** argv) {
         W5O(2, 2, 4, 2, 39, 6, 2, 3, 2) W5O(1, 4, 3, 1, 39, 6, 2, 3, 6)
         W5O(1, 4, 3, 1, 39, 6, 0, 0, 6) W5O(1, 4, 3, 1, 39, 6, 3, 0, 6)
         return 0;
+    }
+    if (which == 31) {  // the shipped F(6,3) 9x3 tile (f32 in, split out): full, no staging, no MFMA steps (PMC)
+#define W5S(D) time_wg<9, 64, 1, 4, 3, 1, 3, 39, 6, 0, false, true, D, 6>("c5", n, 48, 70, 128, in, w, b, out, 2);
+        W5S(0) W5S(1) W5S(2) W5S(3)
+        return 0;
+    }
+    if (which == 34) {  // conv_wg vs conv_wgp ablations: 1 no staging, 2 no MFMA steps
+#define WGA(D) time_wg<9, 64, 1, 4, 3, 1, 3, 39, 6, 0, false, true, D, 6>("c5", n, 48, 70, 128, in, w, b, out, it);
+#define WGPA(D) WGPX(4, 0, D)
+#define WGPX(NWV, OCCV, D)                                                                                        \
+        {                                                                                                         \
+            auto k1 = conv_wgp<9, 64, NWV, 3, 4, 3, 39, 6, OCCV, false, true, D, 6, 2>;                          \
+            const size_t l1 = wgp_lds_bytes<9, 39, 6, 6, 3>();                                                   \
+            (void)hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1);     \
+            dim3 grid(11, 2, n);                                                                              \
+            for (int i = 0; i < 3; ++i)                                                                           \
+                hipLaunchKernelGGL(k1, grid, dim3(64 * NWV), l1, 0, (const float*)in, 48, 70, (const bf16*)w, b, (float*)out, 13, 22, 128, 11, 1, 0.3f); \
+            hipEvent_t e0, e1;                                                                                    \
+            (void)hipEventCreate(&e0);                                                                            \
+            (void)hipEventCreate(&e1);                                                                            \
+            (void)hipEventRecord(e0, 0);                                                                          \
+            for (int i = 0; i < it; ++i)                                                                          \
+                hipLaunchKernelGGL(k1, grid, dim3(64 * NWV), l1, 0, (const float*)in, 48, 70, (const bf16*)w, b, (float*)out, 13, 22, 128, 11, 1, 0.3f); \
+            (void)hipEventRecord(e1, 0);                                                                          \
+            (void)hipEventSynchronize(e1);                                                                        \
+            float ms = 0;                                                                                         \
+            (void)hipEventElapsedTime(&ms, e0, e1);                                                               \
+            printf("wgp nw%d occ%d d%d %7.1f us\n", NWV, OCCV, D, 1e3f * ms / it);                                                      \
+        }
+        for (int r = 0; r < 2; ++r) {
+            WGA(0) WGPA(0) WGPX(8, 0, 0) WGPX(8, 4, 0) WGA(1) WGPA(1) WGPX(8, 0, 1) WGA(2) WGPA(2) WGPX(8, 0, 2) WGA(3) WGPA(3)
+        }
+        return 0;
+    }
+    if (which == 32 || which == 33) {  // conv_wg (channel split) vs conv_wgp (plane split): outputs compared, then timed
+        const int iters = which == 33 ? 2 : it;
+        const int Hin = 48, Win = 70, cout = 128, Hc = Hin - 8, Wc = Win - 2, Hout = Hc / 3, Wout = Wc / 3;
+        const int tiles_h = (Hout * 3 + 38) / 39, tiles_w = (Wout * 3 + 5) / 6;
+        const size_t on = (size_t)n * Hout * Wout * cout;
+        void* out2;
+        (void)hipMalloc(&out2, on * 4);
+        auto k0 = conv_wg<9, 64, 1, 4, 3, 1, 3, 39, 6, 0, false, true, 0, 6, 1, 2>;
+        auto k1 = conv_wgp<9, 64, 4, 3, 4, 3, 39, 6, 0, false, true, 0, 6, 2>;
+        const size_t l0 = wg_lds_bytes<9, 64, 39, 6, 6, 1, 4>(), l1 = wgp_lds_bytes<9, 39, 6, 6, 3>();
+        (void)hipFuncSetAttribute((const void*)k0, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l0);
+        (void)hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1);
+        dim3 grid(tiles_h * tiles_w, cout / 64, n);
+        auto r0 = [&](void* o) { hipLaunchKernelGGL(k0, grid, dim3(256), l0, 0, (const float*)in, Hin, Win, (const bf16*)w, b, (float*)o, Hout, Wout, cout, tiles_w, 1, 0.3f); };
+        auto r1 = [&](void* o) { hipLaunchKernelGGL(k1, grid, dim3(256), l1, 0, (const float*)in, Hin, Win, (const bf16*)w, b, (float*)o, Hout, Wout, cout, tiles_w, 1, 0.3f); };
+        (void)hipMemset(out, 0xff, on * 4);
+        (void)hipMemset(out2, 0xee, on * 4);
+        r0(out);
+        r1(out2);
+        if (hipDeviceSynchronize() != hipSuccess) { printf("kernel error\n"); return 2; }
+        std::vector<uint32_t> a(on), c(on);
+        (void)hipMemcpy(a.data(), out, on * 4, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(c.data(), out2, on * 4, hipMemcpyDeviceToHost);
+        size_t nd = 0;
+        for (size_t i = 0; i < on; ++i) nd += a[i] != c[i];
+        printf("LDS wg %zu wgp %zu: %zu of %zu output words differ\n", l0, l1, nd, on);
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        for (int round = 0; round < 3; ++round)
+            for (int v = 0; v < 2; ++v) {
+                for (int i = 0; i < 2; ++i) v ? r1(out2) : r0(out);
+                (void)hipEventRecord(e0, 0);
+                for (int i = 0; i < iters; ++i) v ? r1(out2) : r0(out);
+                (void)hipEventRecord(e1, 0);
+                (void)hipEventSynchronize(e1);
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, e0, e1);
+                printf("%s %7.1f us\n", v ? "conv_wgp (plane split)  " : "conv_wg (channel split) ", 1e3f * ms / iters);
+            }
+        return nd ? 1 : 0;
     }
     if (which == 21) {  // the shipped fused kernel, three timings (variant A/B across builds)
         FS(0) FS(0) FS(0)
