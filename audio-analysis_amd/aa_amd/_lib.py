@@ -35,6 +35,13 @@ AA_OP = {
     "dense": 9,
 }
 
+# aa_status (include/aa.h)
+AA_OK = 0
+AA_ERR_INVALID = 1
+AA_ERR_HIP = 2
+AA_ERR_UNSUPPORTED = 3
+AA_ERR_WORKSPACE = 4
+
 AA_WIN_OK = 0
 AA_WIN_NONFINITE = 1
 
@@ -174,6 +181,7 @@ _SIGS = {
     "aa_flac_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
     "aa_vorbis_info": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(VorbisInfo)]),
     "aa_vorbis_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
+    "aa_read_file": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -135,16 +135,22 @@ class SlotPool:
 
 
 def decode_into(path, pool: SlotPool):
-    """Decode one file; PCM16 48 kHz WAV lands in a pinned slot untouched."""
+    """Decode one file; PCM16 48 kHz WAV lands in a pinned slot untouched.
+    The file comes in with one aa_read_file call (stat, open, read, close
+    without the interpreter lock: the decoder threads otherwise queued for it
+    behind the lanes' Python at every step)."""
+    import ctypes as C
     from . import identify_tracks as it
-    size = os.path.getsize(path)
-    if size <= pool.bytes:
-        i = pool.get()
+    i = pool.get()
+    got = C.c_int64(0)
+    rc = _lib.lib().aa_read_file(os.fsencode(path), pool.t[i].data_ptr(), pool.bytes, C.byref(got))
+    if rc == _lib.AA_ERR_INVALID:
+        pool.put(i)
+        raise OSError(_lib.lib().aa_last_error().decode(errors="replace"))
+    if rc == _lib.AA_OK:
         try:
             buf = pool.np[i]
-            with open(path, "rb", buffering=0) as f:
-                got = f.readinto(memoryview(buf)[:size])
-            w = _wav_pcm16(buf, got)
+            w = _wav_pcm16(buf, got.value)
             if w is not None and w[3] == SR:
                 off, nb, ch, sr = w
                 t = pool.t[i][off:off + nb].view(torch.int16)
@@ -153,7 +159,7 @@ def decode_into(path, pool: SlotPool):
         except Exception:
             pool.put(i)
             raise
-        pool.put(i)
+    pool.put(i)  # (larger than a slot, or not a 48 kHz PCM16 WAV)
     # FLAC, other WAV encodings; other rates are resampled on the device at upload
     frames, sr = it.load_recording(str(path), resample=None)
     from .resample import out_length
@@ -162,18 +168,33 @@ def decode_into(path, pool: SlotPool):
 
 
 class _Laps:
-    """Wall time per host phase of the batch loop (AA_BATCH_PROFILE=1 prints it)."""
+    """Wall time per host phase of the batch loop (AA_BATCH_PROFILE=1 prints it;
+    AA_BATCH_TRACE=path also keeps every (thread, phase, start, end) interval,
+    CLOCK_MONOTONIC ns like rocprofv3's kernel trace, written there as JSON)."""
 
     def __init__(self):
         self.t = {}
+        self.cpu = {}  # the calling thread's CPU time per phase (time.thread_time)
+        self._c0 = {}
+        self.events = [] if os.environ.get("AA_BATCH_TRACE") else None
 
     def lap(self, name, t0):
+        import threading
         t1 = time.perf_counter()
         self.t[name] = self.t.get(name, 0.0) + (t1 - t0)
+        tid = threading.get_ident()
+        c1 = time.thread_time()
+        if tid in self._c0:
+            self.cpu[name] = self.cpu.get(name, 0.0) + (c1 - self._c0[tid])
+        self._c0[tid] = c1
+        if self.events is not None:
+            import threading
+            now = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+            self.events.append((threading.get_ident(), name, now - int((t1 - t0) * 1e9), now))
         return t1
 
     def report(self):
-        return " ".join(f"{k}={1e3 * v:.1f}ms" if isinstance(v, float) else f"{k}={v}" for k, v in self.t.items())
+        return " ".join(f"{k}={1e3 * v:.1f}ms (cpu {1e3 * self.cpu.get(k, 0.0):.1f})" for k, v in self.t.items())
 
 
 @dataclass
@@ -537,4 +558,8 @@ class BatchAnalyser:
             raise errors[0]
         if os.environ.get("AA_BATCH_PROFILE"):
             logging.warning("batch phases over %d files (%d lanes): %s", len(jobs), len(lanes), self.timing.report())
+        if self.timing.events is not None:
+            import json
+            with open(os.environ["AA_BATCH_TRACE"], "w") as f:
+                json.dump(self.timing.events, f)
         return dict(sorted(results.items()))

@@ -980,10 +980,12 @@ def run_corpus(args, world, rank, dev, files=None, roofline=False):
     cdev = dev if (world > 1 and dist.get_backend() == "nccl") else torch.device("cpu")  # collectives
     n_gpus = max(1, world // ppg)
     # warm-up (untimed): plans, kernels, model upload, and every pinned staging
-    # slot the timed run holds (aa_amd.batch: (lanes + 2) batches; a slot pool
+    # slot the timed run holds (aa_amd.batch: (lanes + PREFETCH) batches; a slot pool
     # grown inside the timed run allocated ~6 MB of pinned memory per slot there)
+    from aa_amd import batch as _batch
     lanes = corpus.default_lanes()
-    corpus.run([files[0]] * (max(4, lanes + 2) * max(args.batch, 1)), models, rank=0, world=1, batch=args.batch)
+    corpus.run([files[0]] * (max(4, lanes + _batch.PREFETCH) * max(args.batch, 1)), models, rank=0, world=1,
+               batch=args.batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -387,6 +387,16 @@ int aa_vorbis_info(const uint8_t* data, size_t len, aa_vorbis_stream_info* info)
  * stream holds more than cap_frames. */
 int aa_vorbis_decode(const uint8_t* data, size_t len, float* out, int64_t cap_frames, int64_t* n_frames);
 
+/* ---- file input of the batched corpus path (aa_amd/batch.py) ----
+ * The whole file at path into buf (cap bytes; a pinned staging slot), in one
+ * call: open, size, read, close -- the reference reads each file through
+ * ffmpeg (src/identify_tracks.py:49-62); the corpus decoder threads read
+ * PCM16 WAVs raw and parse the RIFF header themselves.  *size: the file's
+ * size.  AA_ERR_WORKSPACE (nothing read) when it exceeds cap;
+ * AA_ERR_INVALID when it cannot be opened or read (the reason in
+ * aa_last_error). */
+int aa_read_file(const char* path, void* buf, int64_t cap, int64_t* size);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,3 +61,26 @@ def test_signal_geometry_matches_reference_arithmetic():
         dh, dw = (height, width) if height and width else (3, 3)
         eh, ew = (height // 10, width) if height // 10 and width else (3, 3)
         assert tuple(g) == (dh, dw, eh, ew, int(0.65 * width) + 1, height - height // 10 + 1)
+
+
+def test_read_file(tmp_path):
+    """aa_read_file: the whole file in one call; AA_ERR_WORKSPACE (nothing
+    read) past the buffer; AA_ERR_INVALID with the reason for a missing file."""
+    import ctypes as C
+    from aa_amd import _lib
+    L = _lib.lib()
+    data = bytes(range(256)) * 40 + b"tail"
+    p = tmp_path / "f.bin"
+    p.write_bytes(data)
+    buf = C.create_string_buffer(len(data) + 7)
+    got = C.c_int64(-1)
+    assert L.aa_read_file(str(p).encode(), buf, len(data) + 7, C.byref(got)) == _lib.AA_OK
+    assert got.value == len(data) and buf.raw[:len(data)] == data
+    small = C.create_string_buffer(16)
+    assert L.aa_read_file(str(p).encode(), small, 16, C.byref(got)) == _lib.AA_ERR_WORKSPACE
+    assert got.value == len(data) and small.raw == b"\0" * 16
+    empty = tmp_path / "empty.bin"
+    empty.write_bytes(b"")
+    assert L.aa_read_file(str(empty).encode(), small, 16, C.byref(got)) == _lib.AA_OK and got.value == 0
+    assert L.aa_read_file(str(tmp_path / "missing.wav").encode(), small, 16, C.byref(got)) == _lib.AA_ERR_INVALID
+    assert b"missing.wav" in L.aa_last_error()
