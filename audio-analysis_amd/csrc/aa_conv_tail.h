@@ -94,7 +94,9 @@ __global__ __launch_bounds__(TAIL_NW * 64) void conv_tail_x3(
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
         int p = i * 16 + (lane & 15);
-        if (p >= TP) p = 0;  // padding rows: computed, never used
+        // padding rows (computed, never used): the pixel 16 k back, whose
+        // swizzle slot is the lane's own (no second address on a busy slot)
+        if (p >= TP) p = max(p - 16 * ((p - TP) / 16 + 1), 0);
         const int r = p / TW, c = p - (p / TW) * TW;
         abase[i] = (r * PW + c) * 128;
         aph[i] = p + q;

@@ -242,7 +242,11 @@ void conv_wg(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
         int p = (wm * MF + i) * 16 + (lane & 15);
-        if (p >= TP) p = 0;  // padding rows: computed, never stored
+        // padding rows (computed, never stored): the pixel 16 k rows back, whose
+        // swizzle slot is the lane's own -- a padding lane reading pixel 0 put a
+        // second address on a busy slot of its ds_read_b128 group (the 9x3
+        // layer's MFMA loop: 6.5 M of its 7.5 M bank-conflict cycles per launch)
+        if (p >= TP) p = max(p - 16 * ((p - TP) / 16 + 1), 0);
         abase[i] = p * 128;
         aph[i] = p + q;
     }

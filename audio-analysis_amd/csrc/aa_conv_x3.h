@@ -393,7 +393,11 @@ void conv_x3(const float* __restrict__ in, int Hin, int Win, const bf16* __restr
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
         int p = (wm * MF + i) * 16 + (lane & 15);
-        if (p >= TH * TW || (DIAG & 8)) p = 0;  // padding rows: computed, never stored
+        // padding rows (computed, never stored): the pixel 16 k back, whose
+        // swizzle slot is the lane's own (pixel 0 would put a second address on
+        // a busy slot of the lane's ds_read_b128 group)
+        if (p >= TH * TW) p = max(p - 16 * ((p - TH * TW) / 16 + 1), 0);
+        if (DIAG & 8) p = 0;
         const int r = p / TW, c = p - (p / TW) * TW;
         abase[i] = (r * PW + c) * 128;
         aph[i] = p + q;  // v = r*TW + c = p
