@@ -13,7 +13,7 @@ CSRC = PKG.parent / "csrc"
 INCLUDE = PKG.parent.parent / "include"
 LIB = PKG / "libaa.so"
 SOURCES = ["aa_api.cpp", "aa_frontend.hip", "aa_cnn.hip", "aa_scan.hip", "aa_signal.hip", "aa_flac.cpp",
-           "aa_vorbis.cpp", "aa_resample.hip", "aa_graph.hip"]
+           "aa_vorbis.cpp", "aa_tracks.cpp", "aa_resample.hip", "aa_graph.hip"]
 ARCH = os.environ.get("AA_OFFLOAD_ARCH", "gfx950")
 # per-source flags: the FFT front end is written in scalar f32; SLP packing it
 # into v_pk_* ops needs paired SGPR constants and register shuffles that push

@@ -182,6 +182,8 @@ _SIGS = {
     "aa_vorbis_info": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(VorbisInfo)]),
     "aa_vorbis_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
     "aa_read_file": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
+    "aa_tracks_from_signals": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_double, C.c_int32, C.c_void_p,
+                                         C.c_int64, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -235,6 +235,17 @@ def species_identify(file_name, bird_models, analyse_tracks):
     return species_result(res, meta_data, analyse_tracks, bird_models is not None)
 
 
+def _signal_arrays(signals):
+    """[s.to_array() for s in signals] (rounded to 0.1 as the reference's
+    Signal.to_array, :944-951) in one numpy rounding: the same np.float64
+    elements when every row is a float row (a float start makes it one);
+    otherwise row by row."""
+    if not signals or any(type(s.start) is not float for s in signals):
+        return [s.to_array() for s in signals]
+    import numpy as np
+    return [list(r) for r in np.round(np.array([[s.start, s.end, s.freq_start, s.freq_end] for s in signals]), 1)]
+
+
 def species_result(res, meta_data, analyse_tracks, have_models=True):
     """species_identify's result document from classify()'s return value
     (src/analyse.py:129-175); shared by the per-file path and the batched
@@ -249,7 +260,7 @@ def species_result(res, meta_data, analyse_tracks, have_models=True):
                 filter_by_location(meta_data, tracks)
             for t in tracks:
                 t.set_master_tag()
-            rec_signals = [s.to_array() for s in signals]
+            rec_signals = _signal_arrays(signals)
             chirps = get_chirps(tracks, bird_labels, signals)
             cacophony_index, version = calc_cacophony_index(filter_tracks(tracks), length)
             labels.extend(t.get_meta() for t in tracks)

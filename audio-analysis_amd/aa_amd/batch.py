@@ -392,7 +392,7 @@ class BatchAnalyser:
                 recs[k].signals = [Signal(*tu) for tu in det.to_tuples(stats)]
 
     def _classify(self, lane, pcm, recs):
-        from .identify_tracks import MAX_FRQUENCY, Signal, get_tracks_from_signals
+        from .identify_tracks import MAX_FRQUENCY, Signal, tracks_from_signals
         from .pipeline import BatchRec
         todo = []
         for r in recs:
@@ -409,7 +409,7 @@ class BatchAnalyser:
                     s.track_id = t["id"]
                     tracks.append(s)
             else:
-                tracks = get_tracks_from_signals([s.copy() for s in r.signals], r.length)
+                tracks = tracks_from_signals(r.signals, r.length)
             if len(tracks) == 0:
                 r.res = ([], r.length, [], raw_length, [])
                 continue
@@ -521,7 +521,10 @@ class BatchAnalyser:
                 prof = None
                 if os.environ.get("AA_BATCH_CPROFILE"):  # host-side profile of this lane (tools)
                     import cProfile
-                    prof = cProfile.Profile()
+                    # AA_BATCH_CPROFILE_CPU=1: the lane thread's CPU time (what
+                    # holds the GIL) instead of wall time (GPU waits included)
+                    cpu = os.environ.get("AA_BATCH_CPROFILE_CPU") == "1"
+                    prof = cProfile.Profile(time.thread_time) if cpu else cProfile.Profile()
                     prof.enable()
                 try:
                     while True:

@@ -99,12 +99,23 @@ class ModelResult:
 
 class Signal:
     def __init__(self, start, end, freq_start, freq_end):
+        self._set(start, end, freq_start, freq_end, mel_freq(freq_start), mel_freq(freq_end))
+
+    @classmethod
+    def _with_mel(cls, start, end, freq_start, freq_end, mel_start, mel_end):
+        """A Signal whose mel values are already known (the native track
+        builder returns them with the frequencies they belong to)."""
+        s = cls.__new__(cls)
+        s._set(start, end, freq_start, freq_end, mel_start, mel_end)
+        return s
+
+    def _set(self, start, end, freq_start, freq_end, mel_start, mel_end):
         self.start = start
         self.end = end
         self.freq_start = freq_start
         self.freq_end = freq_end
-        self.mel_freq_start = mel_freq(freq_start)
-        self.mel_freq_end = mel_freq(freq_end)
+        self.mel_freq_start = mel_start
+        self.mel_freq_end = mel_end
         self.results = []
         self.master_tag = None
         self.master_model = None
@@ -353,6 +364,65 @@ def get_tracks_from_signals(signals, end):
     return signals
 
 
+_MEL_INT = None
+_MEL_INT_PTR = 0
+
+
+def _mel_int_table():
+    """mel_freq of the integer frequencies 0 .. 2^17 - 1 (enlarge's int()
+    results) in one numpy evaluation, for aa_tracks_from_signals; checked
+    against mel_freq's scalar path on every 64th entry (numpy's log10 is its
+    own, not libm's; its array and scalar paths agree -- where they would
+    not, False: the Python builder runs)."""
+    global _MEL_INT, _MEL_INT_PTR
+    if _MEL_INT is None:
+        t = 2595.0 * np.log10(1.0 + np.arange(1 << 17, dtype=np.float64) / 700.0)
+        ok = all(t[f] == 2595.0 * np.log10(1.0 + f / 700.0) for f in range(0, 1 << 17, 64))
+        _MEL_INT = t if ok else False
+        _MEL_INT_PTR = t.ctypes.data if ok else 0
+    return _MEL_INT
+
+
+def _is_int(v):
+    t = type(v)
+    if t is float or t is np.float64:
+        return 0
+    return int(t is int or (isinstance(v, (int, np.integer)) and t is not bool))
+
+
+def tracks_from_signals(signals, end):
+    """get_tracks_from_signals (:795-842) of copies of ``signals`` (they are
+    left as they are), through libaa's host builder aa_tracks_from_signals
+    (csrc/aa_tracks.cpp: the same double arithmetic, ints kept ints): the same
+    tracks, field for field and type for type.  Python's own builder runs
+    where the native one declines (a zero mel range, where Python raises; a
+    frequency past the mel table)."""
+    import ctypes as C
+    from . import _lib
+    n = len(signals)
+    lut = _mel_int_table()
+    if n == 0 or lut is False:
+        return get_tracks_from_signals([s.copy() for s in signals], end)
+    # one f64 buffer: n input rows, then n output rows; one i32 buffer: n
+    # input kinds, then n output kinds
+    buf = np.empty((2 * n, 6), dtype=np.float64)
+    buf[:n] = [(s.start, s.end, s.freq_start, s.freq_end, s.mel_freq_start, s.mel_freq_end) for s in signals]
+    kind = np.empty(2 * n, dtype=np.int32)
+    kind[:n] = [_is_int(s.start) | _is_int(s.end) << 1 | _is_int(s.freq_start) << 2 | _is_int(s.freq_end) << 3
+                for s in signals]
+    b, k = buf.ctypes.data, kind.ctypes.data
+    m = C.c_int64(0)
+    rc = _lib.lib().aa_tracks_from_signals(b, k, n, float(end), _is_int(end), _MEL_INT_PTR, lut.size,
+                                           b + 48 * n, k + 4 * n, C.byref(m))
+    if rc in (_lib.AA_ERR_INVALID, _lib.AA_ERR_UNSUPPORTED):
+        return get_tracks_from_signals([s.copy() for s in signals], end)
+    _lib.check(rc, "aa_tracks_from_signals")
+    m = m.value
+    return [Signal._with_mel(int(r[0]) if f & 1 else r[0], int(r[1]) if f & 2 else r[1],
+                             int(r[2]) if f & 4 else r[2], int(r[3]) if f & 8 else r[3], r[4], r[5])
+            for r, f in zip(buf[n:n + m].tolist(), kind[n:n + m].tolist())]
+
+
 # ---------------------------------------------------------------------------
 # classify
 # ---------------------------------------------------------------------------
@@ -390,7 +460,7 @@ def classify(file, models, analyse_tracks, meta_data=None, precision=None, devic
             s.track_id = t["id"]
             tracks.append(s)
     else:
-        tracks = get_tracks_from_signals([s.copy() for s in signals], length)
+        tracks = tracks_from_signals(signals, length)
     if len(tracks) == 0:
         return [], length, [], raw_length, []
     clf = Classifier.shared(precision=precision, device=dev)

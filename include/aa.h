@@ -397,6 +397,22 @@ int aa_vorbis_decode(const uint8_t* data, size_t len, float* out, int64_t cap_fr
  * aa_last_error). */
 int aa_read_file(const char* path, void* buf, int64_t cap, int64_t* size);
 
+/* ---- track builder (host) ----
+ * get_tracks_from_signals (src/identify_tracks.py:795-842, with
+ * merge_signals :725-792): the signals' merge sweeps until stable, then the
+ * enlarge / absorb pass and the narrow-track drop, in Python's double
+ * arithmetic.  sig: n rows of (start, end, freq_start, freq_end,
+ * mel_freq_start, mel_freq_end); kind: per row, which of the first four are
+ * Python ints (bits 0-3: start, end, freq_start, freq_end).  end: the
+ * recording's length (end_is_int: a Python int).  mel_int[f]: the mel of
+ * integer frequency f (numpy's 2595 log10(1 + f / 700)), n_mel entries.
+ * Out: *n_tracks rows (<= n) of the same layout into track / track_kind.
+ * AA_ERR_INVALID where the Python divides by a zero mel range (it raises
+ * there); AA_ERR_UNSUPPORTED when an enlarged frequency is outside mel_int. */
+int aa_tracks_from_signals(const double* sig, const int32_t* kind, int64_t n, double end, int32_t end_is_int,
+                           const double* mel_int, int64_t n_mel, double* track, int32_t* track_kind,
+                           int64_t* n_tracks);
+
 #ifdef __cplusplus
 }
 #endif
