@@ -12,6 +12,7 @@ for r in $(seq 1 $R); do
     python - "${V:--}" <<'PY'
 import json, sys
 d = json.loads(open("gpurun_out/gab.log").read().strip().splitlines()[-1])
+d = json.load(open("gpurun_out/bench_full.json")) if "stages_ms" not in d["roofline"] else d  # (the printed line is compact)
 import re
 g = {}
 for k, v in d["roofline"]["stages_ms"].items():
