@@ -147,6 +147,14 @@ extern "C" int aa_tracks_from_signals(const double* sig_in, const int32_t* kind_
     AA_CHECK(n >= 0 && n_tracks && (n == 0 || (sig_in && kind_in && track_out && kind_out)) && mel_int && n_mel > 0,
              AA_ERR_INVALID, "aa_tracks_from_signals: bad arguments");
     *n_tracks = 0;
+    // NaN keys would break the sorts' strict weak order (Python's sort copes):
+    // such inputs stay with the Python builder
+    bool nan = std::isnan(end);
+    for (int64_t k = 0; k < 6 * n; ++k) nan = nan || std::isnan(sig_in[k]);
+    if (nan) {
+        aa::set_error("aa_tracks_from_signals: NaN in the signals or the end");
+        return AA_ERR_UNSUPPORTED;
+    }
     std::vector<Sig> sig((size_t)n);
     std::vector<int> live((size_t)n);
     for (int64_t k = 0; k < n; ++k) {

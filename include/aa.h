@@ -408,7 +408,8 @@ int aa_read_file(const char* path, void* buf, int64_t cap, int64_t* size);
  * integer frequency f (numpy's 2595 log10(1 + f / 700)), n_mel entries.
  * Out: *n_tracks rows (<= n) of the same layout into track / track_kind.
  * AA_ERR_INVALID where the Python divides by a zero mel range (it raises
- * there); AA_ERR_UNSUPPORTED when an enlarged frequency is outside mel_int. */
+ * there); AA_ERR_UNSUPPORTED when an enlarged frequency is outside mel_int or
+ * an input is NaN (the caller's Python builder takes those). */
 int aa_tracks_from_signals(const double* sig, const int32_t* kind, int64_t n, double end, int32_t end_is_int,
                            const double* mel_int, int64_t n_mel, double* track, int32_t* track_kind,
                            int64_t* n_tracks);

@@ -135,6 +135,10 @@ def test_native_track_builder_edges():
     # enlarged past the 2^17-entry mel table: the Python builder takes it, same result
     sig = [Signal(1.0, 2.0, 100000.0, 130000.0), Signal(1.2, 2.5, 101000.0, 131000.0)]
     assert _fields(tracks_from_signals(sig, 60.0)) == _fields(get_tracks_from_signals([s.copy() for s in sig], 60.0))
+    # NaN anywhere: the Python builder's result (the native sorts need a strict weak order)
+    sig = [Signal(1.0, 2.0, 500.0, 4000.0), Signal(float("nan"), 3.0, 600.0, 4500.0), Signal(1.5, 2.5, 550.0, 4200.0)]
+    got, want = tracks_from_signals(sig, 60.0), get_tracks_from_signals([s.copy() for s in sig], 60.0)
+    assert repr(_fields(got)) == repr(_fields(want)) and "nan" in repr(_fields(got))  # (nan != nan)
     # one signal shorter than min_length: no tracks; one clipped to an int end
     assert tracks_from_signals([Signal(1.0, 1.2, 500.0, 4000.0)], 60.0) == []
     got = tracks_from_signals([Signal(9.5, 10.0, 500.0, 4000.0)], 10)
